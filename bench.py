@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark: asset-days backtested per second on the fused signal -> rank -> portfolio pass.
+
+Workload (BASELINE.json north_star / configs[3]): C4 = 100,000 assets x 10,000 business days
+per GPU (bdate_range('1985-01-01'), 461 months), J=12 skip=1 K=1 equal-weight deciles,
+long-short.  N GPUs = one process per GPU (torchrun), date-sharded in whole months; with
+--scaling weak (default) every rank owns a C4-sized month range of an N x 10,000-day panel.
+
+A step = one full pass over the resident panel: month-end aggregation, [summary all-gather +
+carry fold when N>1], ret/mom/next_ret scan, per-date qcut labels fused with decile means,
+[per-date row all-gather when N>1], long-short.  Inputs are in HBM before timing starts.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+CONFIGS = {
+    "c4": dict(N=100_000, days=10_000, start="1985-01-01",
+               name="C4: 100k assets x 10k bdays per GPU, J=12 skip=1 K=1 EW decile long-short"),
+    "c2": dict(N=5_000, days=6_522, start="2000-01-03",
+               name="C2: 5k assets x 25y bdays (6522), J=12 skip=1 K=1 EW decile long-short"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--assets", type=int, default=None)
+    ap.add_argument("--days", type=int, default=None)
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-assets", type=int, default=50000)
+    ap.add_argument("--seed", type=int, default=4)
+    return ap.parse_args()
+
+
+def cpu_baseline(n_assets: int, days: int, start: str):
+    """The CPU oracle (NumPy port of the reference path) on a bounded sample of the same
+    workload shape: n_assets x days, one pass, 1 host thread."""
+    from oracle import csmom_oracle as O
+    from oracle.synth_np import make_panel
+
+    pan = make_panel(n_assets, days, seed=4, start=start, with_volume=False)
+    t0 = time.perf_counter()
+    PM, _ = O.month_end(pan["P"], pan["month_start"])
+    _, M, NR, _ = O.momentum_scan(PM, 12, 1)
+    L = O.assign_deciles(M, 10)
+    O.portfolio_ew(L, NR, 10)
+    dt = time.perf_counter() - t0
+    return dict(value=n_assets * days / dt, unit="asset-days/s", cores=1, kind="port",
+                sample=f"oracle (NumPy restatement) month-end+scan+deciles+EW on "
+                       f"{n_assets} assets x {days} bdays, one pass {dt:.1f} s")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import csmom
+    from csmom.distributed import DateShardPipeline
+    from csmom.synth import make_device_panel, shard_calendar
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torchrun (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = dict(CONFIGS[args.config])
+    N = args.assets or cfg["N"]
+    days_per_rank = args.days or cfg["days"]
+    total_days = days_per_rank * world if args.scaling == "weak" else days_per_rank
+    days, ms_host, mend, months = shard_calendar(cfg["start"], total_days, world, rank)
+    panel = make_device_panel(N, days, ms_host, seed=args.seed * 1000 + rank, device=dev)
+    T_d, T_m = len(days), len(ms_host) - 1
+
+    eng = csmom.Engine(local)
+    J, skip, nb = 12, 1, 10
+    pipe = DateShardPipeline(eng, months, J, skip, nb) if world > 1 else None
+
+    # preallocated outputs: the timed loop performs no allocation
+    PM = eng.empty((T_m, N))
+    M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
+    L = eng.empty((T_m, N), torch.int8)
+    EW, CNT = eng.empty((T_m, nb)), eng.empty((T_m, nb), torch.int32)
+    LS = eng.empty((T_m,))
+    stage_names = ["month_end", "scan", "deciles", "long_short"]
+    nst = len(stage_names) + 1
+    step_events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst)]
+                   for _ in range(args.steps)]
+    scratch_events = [torch.cuda.Event(enable_timing=True) for _ in range(nst)]
+
+    def step(ev=scratch_events):
+        if pipe is not None:
+            r = pipe.run(panel.P, panel.month_start)
+            return r.LS
+        ev[0].record()
+        eng.month_end(panel.P, panel.month_start, PM=PM)
+        ev[1].record()
+        eng.momentum(PM, J, skip, out=(None, M, NR))
+        ev[2].record()
+        eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
+        ev[3].record()
+        eng.long_short(EW, CNT, LS)
+        ev[4].record()
+        return LS
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    stage_ms = np.zeros(len(stage_names))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(step_events[k])   # HIP events on the launch stream; read after the loop
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if world == 1:
+        for ev in step_events:
+            stage_ms += [ev[i].elapsed_time(ev[i + 1]) for i in range(len(stage_names))]
+    else:
+        stage_ms[:] = np.nan
+
+    # decile match vs the oracle on sampled dates (metric: "decile match %")
+    match = None
+    if rank == 0:
+        from oracle import csmom_oracle as O
+        if world > 1:
+            r = pipe.run(panel.P, panel.month_start)
+            Mh, Lh = r.M, r.L
+        else:
+            Mh, Lh = M, L
+        dates = sorted({T_m // 3, T_m // 2, T_m - 2})
+        tot = ok = 0
+        for t in dates:
+            row = Mh[t].cpu().numpy()
+            ref = np.full(N, -1, dtype=np.int8)
+            v = ~np.isnan(row)
+            if v.any():
+                lab = O.qcut_labels(row[v], nb)
+                ref[v] = np.where(np.isnan(lab), -1, lab).astype(np.int8)
+            got = Lh[t].cpu().numpy()
+            ok += int((got == ref).sum())
+            tot += N
+        match = dict(pct=100.0 * ok / tot, sample=f"{len(dates)} dates x {N} assets vs oracle qcut")
+
+    ms_per_step = 1000.0 * elapsed / args.steps
+    units = N * T_d * world if args.scaling == "weak" else N * total_days
+    value = units * args.steps / elapsed
+    out = None
+    if rank == 0:
+        alg_pipe = 8.0 * N * T_d + 17.0 * N * T_m + 8.0 * T_m * (nb + 1)   # SURVEY 8(d), per rank
+        roofline = None
+        if world == 1:
+            me_ms = stage_ms[0] / args.steps
+            alg_me = 8.0 * N * T_d + 8.0 * N * T_m          # read P once, write PM once
+            achieved = alg_me / (me_ms * 1e-3) / 1e9
+            traffic = None
+            pmc = ROOT / "profiles" / "pmc_month_end.json"
+            if pmc.exists():
+                try:
+                    pj = json.loads(pmc.read_text())
+                    if pj.get("N") == N and pj.get("T_d") == T_d:
+                        traffic = pj.get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roofline = dict(bound="hbm", kernel="k_month_end", achieved=round(achieved, 1),
+                            peak=HBM_PEAK_GBS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
+                            traffic=traffic, algorithmic_bytes_per_launch=alg_me,
+                            avg_launch_ms=round(me_ms, 4))
+        pipe_gbs = alg_pipe * world / (ms_per_step * 1e-3) / 1e9
+        out = {
+            "metric": "asset-periods backtested/sec (1/2/4/8 GPU) + % HBM peak BW; decile match %",
+            "value": value,
+            "unit": "asset-days/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic seeded GBM panel generated in HBM (late listings, delistings, "
+                    "NaN days, absent and all-NaN months)",
+            "config": {"workload": cfg["name"] if args.assets is None and args.days is None
+                       else f"custom: {N} assets x {T_d} bdays per GPU",
+                       "assets": N, "bdays_per_gpu": T_d, "months_per_gpu": T_m, "J": J,
+                       "skip": skip, "K": 1, "n_bins": nb, "weighting": "equal",
+                       "parallelism": f"date-shard x{world}"},
+            "roofline": roofline,
+            "pipeline_roofline": {"bound": "hbm", "achieved": round(pipe_gbs, 1),
+                                  "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                                  "frac": round(pipe_gbs / (HBM_PEAK_GBS * world), 4),
+                                  "algorithmic_bytes_per_pass_per_gpu": alg_pipe},
+            "stage_ms": ({k: round(v / args.steps, 4) for k, v in zip(stage_names, stage_ms)}
+                         if world == 1 else None),
+            "decile_match_pct": match["pct"] if match else None,
+            "decile_check": match["sample"] if match else None,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_assets, T_d, cfg["start"])
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

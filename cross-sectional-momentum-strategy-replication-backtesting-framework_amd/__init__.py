@@ -1,0 +1,27 @@
+"""csmom -- MI355X-native engine for the cross-sectional momentum backtest hot path of
+AkshayJha22/Cross-Sectional-Momentum-Strategy-Replication-Backtesting-Framework.
+
+Import it as ``csmom`` (the repo-root ``csmom.py`` aliases this directory, whose name is not
+a Python identifier).  Public API (reference file:line it replaces):
+
+  compute_monthly_momentum_from_daily   src/features.py:5-57       (GPU)
+  compute_monthly_turnover              src/features.py:60-107     (host; unused by the path)
+  assign_deciles_per_date               run_demo.py:18-29          (GPU)
+  monthly_replication                   run_demo.py:31-79          (GPU + host summary)
+  sharpe / ensure_dir / save_plot       src/utils.py:5-21          (host)
+  Engine                                dense device pipeline (bench / multi-GPU)
+"""
+from ._lib import ABSENT_BITS, CsmError, CsmUnavailable, lib_path, load_library
+from .engine import Engine, PipelineOut, absent_tensor, is_absent, quantile_table
+from .features import compute_monthly_momentum_from_daily, compute_monthly_turnover, get_engine
+from .panel import DensePanel, from_long, month_offsets, monthly_frame
+from .replication import ReplicationResult, assign_deciles_per_date, monthly_replication
+from .utils import ensure_dir, save_plot, sharpe
+
+__all__ = [
+    "ABSENT_BITS", "CsmError", "CsmUnavailable", "lib_path", "load_library", "Engine",
+    "PipelineOut", "absent_tensor", "is_absent", "quantile_table",
+    "compute_monthly_momentum_from_daily", "compute_monthly_turnover", "get_engine",
+    "DensePanel", "from_long", "month_offsets", "monthly_frame", "ReplicationResult",
+    "assign_deciles_per_date", "monthly_replication", "ensure_dir", "save_plot", "sharpe",
+]

@@ -1,0 +1,94 @@
+"""ctypes binding of libcsmom.so (the C ABI declared in include/csmom.h).
+
+The library is built in-tree (``python -c "import __graft_entry__ as g; g.build()"`` or
+``make -C <pkg>/csrc``).  There is no fallback: if the shared object is missing or cannot
+be loaded, every compute entry point raises ``CsmUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_NAME = "libcsmom.so"
+PKG_DIR = Path(__file__).resolve().parent
+CSM_OK = 0
+CSM_E_INVAL = -1
+CSM_E_HIP = -2
+ABSENT_BITS = 0x7FF4000000000001
+
+EXPORTS = (
+    "csm_abi_version", "csm_create", "csm_destroy", "csm_last_error", "csm_set_stream",
+    "csm_sync", "csm_month_end", "csm_momentum", "csm_deciles", "csm_long_short",
+    "csm_shard_summary", "csm_fold_carry",
+)
+
+
+class CsmUnavailable(RuntimeError):
+    """libcsmom.so is missing or failed to load (the engine has no CPU fallback)."""
+
+
+class CsmError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"csmom status {status}: {msg}")
+        self.status = status
+
+
+def lib_path() -> Path:
+    return Path(os.environ.get("CSMOM_LIB", PKG_DIR / LIB_NAME))
+
+
+_LIB = None
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+
+def _declare(lib):
+    sig = {
+        "csm_abi_version": (ctypes.c_int, []),
+        "csm_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+        "csm_destroy": (ctypes.c_int, [_p]),
+        "csm_last_error": (ctypes.c_char_p, [_p]),
+        "csm_set_stream": (ctypes.c_int, [_p, _p]),
+        "csm_sync": (ctypes.c_int, [_p]),
+        "csm_month_end": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i32, _p, _p]),
+        "csm_momentum": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p]),
+        "csm_deciles": (ctypes.c_int, [_p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
+        "csm_long_short": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p]),
+        "csm_shard_summary": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p]),
+        "csm_fold_carry": (ctypes.c_int, [_p, _p, _i32, _i32, _i64, _i32, _i32, _p, _p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def load_library():
+    """Load (once) and return the ctypes handle; raises CsmUnavailable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not path.exists():
+        raise CsmUnavailable(
+            f"{path} not found: build the HIP engine first (__graft_entry__.build()); "
+            "csmom has no CPU fallback")
+    try:
+        lib = ctypes.CDLL(str(path))
+    except OSError as e:  # pragma: no cover - depends on the host
+        raise CsmUnavailable(f"cannot load {path}: {e}") from e
+    missing = [n for n in EXPORTS if not hasattr(lib, n)]
+    if missing:
+        raise CsmUnavailable(f"{path} lacks exports {missing}")
+    _LIB = _declare(lib)
+    return _LIB
+
+
+def check(lib, ctx, status: int, what: str):
+    if status != CSM_OK:
+        msg = lib.csm_last_error(ctx)
+        raise CsmError(status, f"{what}: {msg.decode() if msg else '?'}")

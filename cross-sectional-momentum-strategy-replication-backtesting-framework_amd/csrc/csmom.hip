@@ -1,0 +1,1088 @@
+// csmom.hip -- hand-written gfx950 (CDNA4) kernels + C ABI for the momentum backtest hot path.
+//
+// Every kernel here is HBM- or latency-bound integer/fp64 work; nothing is a contraction, so
+// no MFMA.  Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (the fp64 products and
+// lerps must not be contracted into FMAs -- bit-exactness with NumPy/pandas depends on it).
+//
+// Reference behaviour restated (file:line into the reference):
+//   month-end         src/features.py:34-39   (groupby ticker x Grouper('ME'): last / sum)
+//   ret/mom scan      src/features.py:44-52   (pct_change ffill; shift(skip).rolling(J) prod)
+//   next_ret          run_demo.py:48          (pct_change within the ranked subset, shift(-1))
+//   deciles           run_demo.py:18-29,46    (pd.qcut(q=n, labels=False, duplicates='drop'))
+//   decile means      run_demo.py:49-55       (dropna; groupby(date, decile).mean())
+//   long-short        run_demo.py:57-67
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/csmom.h"
+
+#define ABSENT_BITS 0x7FF4000000000001ULL
+#define ABSENT_MASK 0x7FF7FFFFFFFFFFFFULL
+
+__device__ __forceinline__ bool is_absent(double x) {
+  return (((uint64_t)__double_as_longlong(x)) & ABSENT_MASK) == ABSENT_BITS;
+}
+__device__ __forceinline__ double absent_val() { return __longlong_as_double((long long)ABSENT_BITS); }
+__device__ __forceinline__ double qnan() { return __longlong_as_double(0x7FF8000000000000LL); }
+__device__ __forceinline__ bool isnan_d(double x) { return x != x; }
+
+// =====================================================================================
+// Kernel A: month-end aggregation.  One thread per (month, VEC assets); a wave streams
+// 64*VEC*8 contiguous bytes per day row (1 KiB at VEC=2).  Days of a month are walked in
+// order so the Kahan volume sum matches pandas' group_sum bit for bit.
+// =====================================================================================
+template <int VEC, bool WITH_VOL>
+__global__ __launch_bounds__(256) void k_month_end(const double* __restrict__ P,
+                                                   const double* __restrict__ V,
+                                                   const int64_t* __restrict__ month_start,
+                                                   int64_t N, double* __restrict__ PM,
+                                                   double* __restrict__ VOL) {
+  const int m = blockIdx.y;
+  const int64_t a = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * VEC;
+  if (a >= N) return;
+  const int64_t d0 = month_start[m], d1 = month_start[m + 1];
+  double last[VEC];
+  bool anyp[VEC], anyv[VEC];
+  double s[VEC], c[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) {
+    last[k] = 0.0; anyp[k] = false; anyv[k] = false; s[k] = 0.0; c[k] = 0.0;
+  }
+  const double* p = P + d0 * N + a;
+  const double* v = WITH_VOL ? V + d0 * N + a : nullptr;
+  int64_t d = d0;
+  // 8-day batches keep 8 row loads in flight per lane before the dependent selects.
+  for (; d + 8 <= d1; d += 8) {
+    double x[8][VEC];
+    double y[WITH_VOL ? 8 : 1][VEC];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (VEC == 2) {
+        double2 t = *reinterpret_cast<const double2*>(p + j * N);
+        x[j][0] = t.x; x[j][VEC - 1] = t.y;
+        if (WITH_VOL) { double2 u = *reinterpret_cast<const double2*>(v + j * N); y[j][0] = u.x; y[j][VEC - 1] = u.y; }
+      } else {
+        x[j][0] = p[j * N];
+        if (WITH_VOL) y[j][0] = v[j * N];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const bool pr = !is_absent(x[j][k]);
+        const bool ok = pr && !isnan_d(x[j][k]);
+        anyp[k] |= pr;
+        anyv[k] |= ok;
+        last[k] = ok ? x[j][k] : last[k];
+        if (WITH_VOL && pr) {
+          double val = y[j][k];
+          val = isnan_d(val) ? 0.0 : val;
+          const double yy = val - c[k];
+          const double tt = s[k] + yy;
+          double cc = (tt - s[k]) - yy;
+          c[k] = isnan_d(cc) ? 0.0 : cc;
+          s[k] = tt;
+        }
+      }
+    }
+    p += 8 * N;
+    if (WITH_VOL) v += 8 * N;
+  }
+  for (; d < d1; ++d) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const double xv = p[k];
+      const bool pr = !is_absent(xv);
+      const bool ok = pr && !isnan_d(xv);
+      anyp[k] |= pr;
+      anyv[k] |= ok;
+      last[k] = ok ? xv : last[k];
+      if (WITH_VOL && pr) {
+        double val = v[k];
+        val = isnan_d(val) ? 0.0 : val;
+        const double yy = val - c[k];
+        const double tt = s[k] + yy;
+        double cc = (tt - s[k]) - yy;
+        c[k] = isnan_d(cc) ? 0.0 : cc;
+        s[k] = tt;
+      }
+    }
+    p += N;
+    if (WITH_VOL) v += N;
+  }
+  double out[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) out[k] = anyp[k] ? (anyv[k] ? last[k] : qnan()) : absent_val();
+  double* o = PM + (int64_t)m * N + a;
+  if (VEC == 2) {
+    *reinterpret_cast<double2*>(o) = make_double2(out[0], out[VEC - 1]);
+  } else {
+    o[0] = out[0];
+  }
+  if (WITH_VOL) {
+    double* w = VOL + (int64_t)m * N + a;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) w[k] = anyp[k] ? s[k] : 0.0;
+  }
+}
+
+// =====================================================================================
+// Kernel B: per-asset scan over months (present rows only).  One thread per asset; the
+// J+skip ret ring lives in LDS (slot-major, thread-fastest: conflict-free).  PM rows are
+// prefetched CHUNK months ahead so each wave keeps CHUNK*512 B in flight.
+// mom = (prod_{oldest..newest of the J oldest ring entries} fl(1+ret)) - 1, left to right.
+// =====================================================================================
+#define SCAN_THREADS 128
+#define SCAN_CHUNK 16
+
+__global__ __launch_bounds__(256) void k_momentum(
+    const double* __restrict__ PM, int T_m, int64_t N, int J, int skip, double* __restrict__ R,
+    double* __restrict__ M, double* __restrict__ NR, const double* __restrict__ carry,
+    const double* __restrict__ next_pm, double* __restrict__ carry_out) {
+  extern __shared__ __attribute__((aligned(16))) double ring_lds[];
+  const int W = J + skip;
+  const int tid = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + tid;
+  const bool live = a < N;
+  const int RS = blockDim.x;           // ring stride (slot-major, thread-fastest)
+  double* ring = ring_lds + tid;       // ring[k * RS]
+  double pff, psff;
+  if (live && carry) {
+    for (int k = 0; k < W; ++k) ring[k * RS] = carry[(int64_t)k * N + a];
+    pff = carry[(int64_t)W * N + a];
+    psff = carry[(int64_t)(W + 1) * N + a];
+  } else {
+    for (int k = 0; k < W; ++k) ring[k * RS] = qnan();
+    pff = qnan();
+    psff = qnan();
+  }
+  if (!live) return;
+  int head = 0;     // index of the oldest ring entry
+  int prev = -1;    // month of the pending ranked row (its next_ret waits for the next row)
+  const double NaN = qnan();
+  for (int m0 = 0; m0 < T_m; m0 += SCAN_CHUNK) {
+    double buf[SCAN_CHUNK];
+#pragma unroll
+    for (int j = 0; j < SCAN_CHUNK; ++j)
+      buf[j] = (m0 + j < T_m) ? PM[(int64_t)(m0 + j) * N + a] : absent_val();
+#pragma unroll
+    for (int j = 0; j < SCAN_CHUNK; ++j) {
+      const int m = m0 + j;
+      if (m >= T_m) break;
+      const double x = buf[j];
+      const int64_t o = (int64_t)m * N + a;
+      if (is_absent(x)) {
+        if (R) R[o] = NaN;
+        M[o] = NaN;
+        NR[o] = NaN;
+        continue;
+      }
+      const bool xv = !isnan_d(x);
+      const double pnew = xv ? x : pff;
+      const double ret = pnew / pff - 1.0;
+      pff = pnew;
+      // push: overwrite the oldest, advance head
+      ring[head * RS] = 1.0 + ret;
+      head = (head + 1 == W) ? 0 : head + 1;
+      double acc = ring[head * RS];
+      int idx = head;
+      for (int k = 1; k < J; ++k) {
+        idx = (idx + 1 == W) ? 0 : idx + 1;
+        acc = acc * ring[idx * RS];
+      }
+      const double mom = acc - 1.0;
+      const bool ranked = !isnan_d(mom);
+      const double ps_new = xv ? x : psff;
+      if (prev >= 0) NR[(int64_t)prev * N + a] = ps_new / psff - 1.0;
+      if (ranked) {
+        psff = ps_new;
+        prev = m;
+      } else {
+        NR[o] = NaN;
+        prev = -1;
+      }
+      if (R) R[o] = ret;
+      M[o] = mom;
+    }
+  }
+  if (prev >= 0) {
+    double nr = NaN;
+    if (next_pm) {
+      const double x = next_pm[a];
+      if (!is_absent(x)) {
+        const double ps_new = isnan_d(x) ? psff : x;
+        nr = ps_new / psff - 1.0;
+      }
+    }
+    NR[(int64_t)prev * N + a] = nr;
+  }
+  if (carry_out) {
+    int idx = head;
+    for (int k = 0; k < W; ++k) {  // carry rows hold the ring's factors fl(1+ret), oldest first
+      carry_out[(int64_t)k * N + a] = ring[idx * RS];
+      idx = (idx + 1 == W) ? 0 : idx + 1;
+    }
+    carry_out[(int64_t)W * N + a] = pff;
+    carry_out[(int64_t)(W + 1) * N + a] = psff;
+  }
+}
+
+// =====================================================================================
+// Kernel C: per-date qcut labels + fused equal-weight decile means (K = 1).
+// One workgroup per date.  Exact order statistics by bucket-select:
+//   pass 1  count / min / max of the ranked values
+//   pass 2  4096-bucket histogram, linear in value over [min, max] (monotone bucketing)
+//   (rare)  oversized target buckets are refined in key space (order-preserving u64 keys)
+//   pass 3  gather the target buckets' members into LDS, bitonic sort, read ranks
+//   pass 4  edges (NumPy lerp) -> dedupe -> labels; accumulate next_ret per label
+// =====================================================================================
+#define DEC_THREADS 512
+#define HB 4096
+#define CAP 4096
+#define MAXQ 21  // n_bins + 1 <= 21
+#define MAXT 42  // distinct target ranks (2 per interior quantile + min + max)
+
+struct QTab {
+  double q[MAXQ];
+};
+
+__device__ __forceinline__ uint64_t dkey(double x) {
+  const uint64_t b = (uint64_t)__double_as_longlong(x + 0.0);  // -0.0 -> +0.0
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double dval(uint64_t k) {
+  const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
+  return __longlong_as_double((long long)b);
+}
+
+struct Slot {
+  uint64_t klo, khi;  // key interval (inclusive) inside value bucket b0
+  int b0;
+  int count;          // members
+  int off;            // candidate offset
+  int resolved;       // all members share one key -> value known
+  double value;
+};
+
+struct DecShared {
+  uint32_t hist[HB];
+  double cand[CAP];
+  Slot slots[MAXT];
+  int64_t trank[MAXT];  // target ranks (sorted, distinct)
+  int64_t tres[MAXT];   // residual rank inside its slot
+  int tslot[MAXT];
+  double tval[MAXT];
+  int nslot, ntgt, total;
+  double vmin, vmax, scale;
+  uint64_t kmin_r, kmax_r;
+  double bins[MAXQ];
+  int nbins;
+  int64_t n;
+  int fill[MAXT];
+  Slot slots2[MAXT];
+  int remap[MAXT];
+  double e[MAXQ], u[MAXQ];
+  // reduction scratch
+  double red_d[DEC_THREADS / 64][2];
+  unsigned long long red_k[DEC_THREADS / 64][2];
+  int64_t red_n[DEC_THREADS / 64];
+};
+
+__device__ __forceinline__ int vbucket(double x, double lo, double scale) {
+  if (scale == 0.0) return 0;
+  const double f = (x - lo) * scale;
+  const int b = (int)f;
+  return b < HB ? b : HB - 1;
+}
+
+template <bool V2, typename F>
+__device__ __forceinline__ void for_row(const double* __restrict__ row, int64_t N, F&& f) {
+  if (V2) {
+    for (int64_t i = 2 * (int64_t)threadIdx.x; i < N; i += 2 * DEC_THREADS) {
+      const double2 t = *reinterpret_cast<const double2*>(row + i);
+      f(i, t.x);
+      f(i + 1, t.y);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < N; i += DEC_THREADS) f(i, row[i]);
+  }
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+// Exclusive scan of S.hist in place; returns nothing (hist[b] becomes prefix).
+__device__ void block_exclusive_scan_hist(uint32_t* hist) {
+  __shared__ uint32_t part[DEC_THREADS];
+  const int tid = threadIdx.x;
+  const int per = HB / DEC_THREADS;  // 8
+  uint32_t loc[HB / DEC_THREADS];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < per; ++j) { loc[j] = hist[tid * per + j]; s += loc[j]; }
+  part[tid] = s;
+  __syncthreads();
+  // Hillis-Steele over DEC_THREADS partials
+  for (int off = 1; off < DEC_THREADS; off <<= 1) {
+    uint32_t v = (tid >= off) ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - s;
+#pragma unroll
+  for (int j = 0; j < per; ++j) { hist[tid * per + j] = run; run += loc[j]; }
+  __syncthreads();
+}
+
+// member test for a slot (value bucket b0 and key interval)
+__device__ __forceinline__ bool slot_member(const Slot& s, int b, uint64_t k) {
+  return b == s.b0 && k >= s.klo && k <= s.khi;
+}
+
+template <int NB, bool V2>
+__global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restrict__ Mx,
+                                                         const double* __restrict__ NRx,
+                                                         int64_t N, int n_bins, QTab qt,
+                                                         int8_t* __restrict__ L,
+                                                         double* __restrict__ EW,
+                                                         int32_t* __restrict__ CNT,
+                                                         int32_t* __restrict__ NV) {
+  __shared__ DecShared S;
+  const int t = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const double* row = Mx + (int64_t)t * N;
+  const double* nrow = NRx ? NRx + (int64_t)t * N : nullptr;
+  int8_t* lrow = L + (int64_t)t * N;
+
+  // ---------------- pass 1: count / min / max
+  {
+    int64_t cnt = 0;
+    double lo = INFINITY, hi = -INFINITY;
+    for_row<V2>(row, N, [&](int64_t, double x) {
+      if (!isnan_d(x)) { ++cnt; lo = fmin(lo, x); hi = fmax(hi, x); }
+    });
+    for (int o = 32; o > 0; o >>= 1) {
+      cnt += __shfl_down(cnt, o, 64);
+      lo = fmin(lo, __shfl_down(lo, o, 64));
+      hi = fmax(hi, __shfl_down(hi, o, 64));
+    }
+    if (lane == 0) { S.red_n[wid] = cnt; S.red_d[wid][0] = lo; S.red_d[wid][1] = hi; }
+    __syncthreads();
+    if (tid == 0) {
+      int64_t c = 0; double l = INFINITY, h = -INFINITY;
+      for (int w = 0; w < DEC_THREADS / 64; ++w) { c += S.red_n[w]; l = fmin(l, S.red_d[w][0]); h = fmax(h, S.red_d[w][1]); }
+      S.n = c; S.vmin = l; S.vmax = h;
+      const double rng = h - l;
+      S.scale = (c > 0 && rng > 0.0 && rng <= 1.0e300) ? (double)HB / rng : 0.0;
+    }
+    __syncthreads();
+  }
+  const int64_t n = S.n;
+  if (NV && tid == 0) NV[t] = (int32_t)n;
+  const bool degenerate = (n == 0) || !(S.vmin < S.vmax);
+
+  if (!degenerate) {
+    // ---------------- target ranks
+    if (tid == 0) {
+      int nt = 0;
+      for (int k = 0; k <= n_bins; ++k) {
+        const double v = (double)(n - 1) * qt.q[k];
+        if (v >= (double)(n - 1)) {
+          S.trank[nt++] = n - 1;
+          continue;
+        }
+        const double p = floor(v);
+        const int64_t pi = (int64_t)p;
+        S.trank[nt++] = pi;
+        if (v - p != 0.0) S.trank[nt++] = pi + 1;
+      }
+      // sort + dedupe (tiny)
+      for (int i = 1; i < nt; ++i) {
+        int64_t x = S.trank[i]; int j = i - 1;
+        while (j >= 0 && S.trank[j] > x) { S.trank[j + 1] = S.trank[j]; --j; }
+        S.trank[j + 1] = x;
+      }
+      int u = 0;
+      for (int i = 0; i < nt; ++i) if (u == 0 || S.trank[u - 1] != S.trank[i]) S.trank[u++] = S.trank[i];
+      S.ntgt = u;
+    }
+    for (int b = tid; b < HB; b += DEC_THREADS) S.hist[b] = 0;
+    __syncthreads();
+    // ---------------- pass 2: value-bucket histogram
+    {
+      const double lo = S.vmin, sc = S.scale;
+      for_row<V2>(row, N, [&](int64_t, double x) {
+        if (!isnan_d(x)) atomicAdd(&S.hist[vbucket(x, lo, sc)], 1u);
+      });
+    }
+    __syncthreads();
+    // counts are needed after the scan: keep a copy of target-bucket counts via prefix diff
+    block_exclusive_scan_hist(S.hist);
+    if (tid < S.ntgt) {
+      const int64_t r = S.trank[tid];
+      // last bucket b with prefix[b] <= r
+      int lo = 0, hi = HB - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int64_t)S.hist[mid] <= r) lo = mid; else hi = mid - 1;
+      }
+      S.tslot[tid] = lo;  // temporarily: bucket id
+      S.tres[tid] = r - (int64_t)S.hist[lo];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      // build slots from distinct buckets (targets are sorted, so buckets are sorted)
+      int ns = 0;
+      for (int i = 0; i < S.ntgt; ++i) {
+        const int b = S.tslot[i];
+        if (ns == 0 || S.slots[ns - 1].b0 != b) {
+          Slot& s = S.slots[ns++];
+          s.b0 = b; s.klo = 0; s.khi = ~0ULL; s.resolved = 0; s.value = 0.0;
+          const uint32_t next = (b + 1 < HB) ? S.hist[b + 1] : (uint32_t)n;
+          s.count = (int)(next - S.hist[b]);
+        }
+        S.tslot[i] = ns - 1;
+      }
+      S.nslot = ns;
+      int tot = 0;
+      for (int i = 0; i < ns; ++i) tot += S.slots[i].count;
+      S.total = tot;
+    }
+    __syncthreads();
+
+    // ---------------- (rare) key-space refinement of the largest slot until all fit
+    while (S.total > CAP) {
+      __shared__ int rs;
+      if (tid == 0) {
+        int best = -1;
+        for (int i = 0; i < S.nslot; ++i)
+          if (!S.slots[i].resolved && (best < 0 || S.slots[i].count > S.slots[best].count)) best = i;
+        rs = best;
+      }
+      __syncthreads();
+      const Slot sl = S.slots[rs];
+      const double lo = S.vmin, sc = S.scale;
+      // key min / max of the members
+      unsigned long long kl = ~0ULL, kh = 0ULL;
+      for_row<V2>(row, N, [&](int64_t, double x) {
+        if (!isnan_d(x)) {
+          const uint64_t k = dkey(x);
+          if (slot_member(sl, vbucket(x, lo, sc), k)) { kl = k < kl ? k : kl; kh = k > kh ? k : kh; }
+        }
+      });
+      for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long a2 = __shfl_down(kl, o, 64), b2 = __shfl_down(kh, o, 64);
+        kl = a2 < kl ? a2 : kl; kh = b2 > kh ? b2 : kh;
+      }
+      if (lane == 0) { S.red_k[wid][0] = kl; S.red_k[wid][1] = kh; }
+      for (int b = tid; b < HB; b += DEC_THREADS) S.hist[b] = 0;
+      __syncthreads();
+      if (tid == 0) {
+        unsigned long long l2 = ~0ULL, h2 = 0ULL;
+        for (int w = 0; w < DEC_THREADS / 64; ++w) { l2 = S.red_k[w][0] < l2 ? S.red_k[w][0] : l2; h2 = S.red_k[w][1] > h2 ? S.red_k[w][1] : h2; }
+        S.kmin_r = l2; S.kmax_r = h2;
+      }
+      __syncthreads();
+      const uint64_t kmin = S.kmin_r, kmax = S.kmax_r;
+      if (kmin == kmax) {
+        if (tid == 0) {
+          Slot& s = S.slots[rs];
+          s.resolved = 1; s.value = dval(kmin); s.klo = kmin; s.khi = kmax;
+          S.total -= s.count;
+        }
+        __syncthreads();
+        continue;
+      }
+      const uint64_t range = kmax - kmin;
+      const int bits = 64 - __clzll((long long)range);
+      const int shift = bits > 12 ? bits - 12 : 0;
+      for_row<V2>(row, N, [&](int64_t, double x) {
+        if (!isnan_d(x)) {
+          const uint64_t k = dkey(x);
+          if (slot_member(sl, vbucket(x, lo, sc), k)) atomicAdd(&S.hist[(k - kmin) >> shift], 1u);
+        }
+      });
+      __syncthreads();
+      if (tid == 0) {
+        // split slot rs by the sub-buckets of its targets; rebuild the slot list in order
+        Slot old = S.slots[rs];
+        Slot* ns_list = S.slots2;
+        int nn = 0;
+        int* remap = S.remap;
+        for (int i = 0; i < S.nslot; ++i) remap[i] = -1;
+        for (int i = 0; i < S.nslot; ++i) {
+          if (i != rs) { ns_list[nn] = S.slots[i]; remap[i] = nn++; continue; }
+          // targets of this slot (contiguous in target order)
+          for (int ti = 0; ti < S.ntgt; ++ti) {
+            if (S.tslot[ti] != rs) continue;
+            int64_t r = S.tres[ti];
+            int j = 0;
+            int64_t acc = 0;
+            while (acc + (int64_t)S.hist[j] <= r) { acc += S.hist[j]; ++j; }
+            const uint64_t klo = kmin + ((uint64_t)j << shift);
+            uint64_t khi = klo + (((uint64_t)1 << shift) - 1);
+            if (khi > kmax || khi < klo) khi = kmax;
+            if (nn == 0 || ns_list[nn - 1].b0 != old.b0 || ns_list[nn - 1].klo != klo) {
+              Slot& s = ns_list[nn++];
+              s = old; s.klo = klo; s.khi = khi; s.count = (int)S.hist[j]; s.resolved = 0;
+            }
+            S.tres[ti] = r - acc;
+            S.tslot[ti] = -(nn - 1) - 2;  // mark as remapped (new index encoded)
+          }
+        }
+        for (int ti = 0; ti < S.ntgt; ++ti) {
+          if (S.tslot[ti] <= -2) S.tslot[ti] = -S.tslot[ti] - 2;
+          else S.tslot[ti] = remap[S.tslot[ti]];
+        }
+        int tot = 0;
+        for (int i = 0; i < nn; ++i) { S.slots[i] = ns_list[i]; if (!ns_list[i].resolved) tot += ns_list[i].count; }
+        S.nslot = nn;
+        S.total = tot;
+      }
+      __syncthreads();
+    }
+
+    // ---------------- pass 3: gather candidates of unresolved slots
+    if (tid == 0) {
+      int off = 0;
+      for (int i = 0; i < S.nslot; ++i) {
+        S.slots[i].off = off;
+        S.fill[i] = 0;
+        if (!S.slots[i].resolved) off += S.slots[i].count;
+      }
+      S.total = off;
+    }
+    // bucket -> first slot index map (reuses hist)
+    for (int b = tid; b < HB; b += DEC_THREADS) S.hist[b] = 0xFFFFFFFFu;
+    __syncthreads();
+    if (tid == 0)
+      for (int i = S.nslot - 1; i >= 0; --i) S.hist[S.slots[i].b0] = (uint32_t)i;
+    __syncthreads();
+    {
+      const double lo = S.vmin, sc = S.scale;
+      const int nsl = S.nslot;
+      for_row<V2>(row, N, [&](int64_t, double x) {
+        if (isnan_d(x)) return;
+        const int b = vbucket(x, lo, sc);
+        uint32_t si = S.hist[b];
+        if (si == 0xFFFFFFFFu) return;
+        const uint64_t k = dkey(x);
+        for (int i = (int)si; i < nsl && S.slots[i].b0 == b; ++i) {
+          const Slot& s = S.slots[i];
+          if (k >= s.klo && k <= s.khi) {
+            if (!s.resolved) {
+              const int pos = atomicAdd(&S.fill[i], 1);
+              S.cand[s.off + pos] = x;
+            }
+            break;
+          }
+        }
+      });
+    }
+    __syncthreads();
+    // ---------------- bitonic sort of the candidates (slot ranges are value-ordered)
+    {
+      const int tot = S.total;
+      int P2 = 1;
+      while (P2 < tot) P2 <<= 1;
+      for (int i = tot + tid; i < P2; i += DEC_THREADS) S.cand[i] = INFINITY;
+      __syncthreads();
+      for (int k = 2; k <= P2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = tid; i < P2; i += DEC_THREADS) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const double x = S.cand[i], y = S.cand[ixj];
+              const bool up = (i & k) == 0;
+              if ((x > y) == up) { S.cand[i] = y; S.cand[ixj] = x; }
+            }
+          }
+          __syncthreads();
+        }
+      }
+    }
+    if (tid < S.ntgt) {
+      const Slot& s = S.slots[S.tslot[tid]];
+      S.tval[tid] = s.resolved ? s.value : S.cand[s.off + S.tres[tid]];
+    }
+    __syncthreads();
+    // ---------------- edges (NumPy _lerp) and duplicates='drop'
+    if (tid == 0) {
+      auto order_stat = [&](int64_t r) -> double {
+        int lo2 = 0, hi2 = S.ntgt - 1;
+        while (lo2 < hi2) { const int mid = (lo2 + hi2) >> 1; if (S.trank[mid] < r) lo2 = mid + 1; else hi2 = mid; }
+        return S.tval[lo2];
+      };
+      double* e = S.e;
+      for (int k = 0; k <= n_bins; ++k) {
+        const double v = (double)(n - 1) * qt.q[k];
+        if (v >= (double)(n - 1)) { e[k] = S.vmax; continue; }
+        const double p = floor(v);
+        const double g = v - p;
+        const int64_t pi = (int64_t)p;
+        const double a = order_stat(pi);
+        const double b = (g != 0.0) ? order_stat(pi + 1) : a;
+        const double d = b - a;
+        e[k] = (g >= 0.5) ? (b - d * (1.0 - g)) : (a + d * g);
+      }
+      double* u = S.u;
+      int nu = 0;
+      for (int k = 0; k <= n_bins; ++k) {
+        bool seen = false;
+        for (int j = 0; j < nu; ++j) seen |= (u[j] == e[k]);
+        if (!seen) u[nu++] = e[k];
+      }
+      const int ne = n_bins + 1;
+      if (nu < ne && ne != 2) { for (int j = 0; j < nu; ++j) S.bins[j] = u[j]; S.nbins = nu; }
+      else { for (int j = 0; j < ne; ++j) S.bins[j] = e[j]; S.nbins = ne; }
+    }
+    __syncthreads();
+  } else {
+    if (tid == 0) S.nbins = 0;
+    __syncthreads();
+  }
+
+  // ---------------- pass 4: labels + equal-weight accumulation (double-double per label)
+  const int nb = S.nbins;
+  double bins[MAXQ];
+#pragma unroll
+  for (int j = 0; j < MAXQ; ++j) bins[j] = (j < nb) ? S.bins[j] : 0.0;
+  constexpr int NBA = NB > 0 ? NB : 1;
+  double hs[NBA], ls[NBA];
+  int cn[NBA];
+#pragma unroll
+  for (int d = 0; d < NBA; ++d) { hs[d] = 0.0; ls[d] = 0.0; cn[d] = 0; }
+  auto label_of = [&](double x) -> int {
+    if (nb == 0 || isnan_d(x)) return -1;
+    int ids = 0;
+#pragma unroll
+    for (int j = 0; j < MAXQ; ++j) ids += (j < nb && bins[j] < x) ? 1 : 0;
+    if (x == bins[0]) ids = 1;
+    return (ids == 0 || ids == nb) ? -1 : ids - 1;
+  };
+  auto accumulate = [&](int lab, double r) {
+    if (NB > 0 && lab >= 0 && !isnan_d(r)) {
+#pragma unroll
+      for (int d = 0; d < NB; ++d) {
+        if (lab == d) {
+          const double s = hs[d] + r;
+          const double bb = s - hs[d];
+          const double err = (hs[d] - (s - bb)) + (r - bb);
+          hs[d] = s; ls[d] += err; cn[d] += 1;
+        }
+      }
+    }
+  };
+  if (V2) {
+    for (int64_t i = 2 * (int64_t)tid; i < N; i += 2 * DEC_THREADS) {
+      const double2 x = *reinterpret_cast<const double2*>(row + i);
+      const int l0 = label_of(x.x), l1 = label_of(x.y);
+      char2 lv; lv.x = (char)l0; lv.y = (char)l1;
+      *reinterpret_cast<char2*>(lrow + i) = lv;
+      if (NB > 0 && nrow && (l0 >= 0 || l1 >= 0)) {
+        const double2 r = *reinterpret_cast<const double2*>(nrow + i);
+        accumulate(l0, r.x);
+        accumulate(l1, r.y);
+      }
+    }
+  } else {
+    for (int64_t i = tid; i < N; i += DEC_THREADS) {
+      const int l0 = label_of(row[i]);
+      lrow[i] = (int8_t)l0;
+      if (NB > 0 && nrow && l0 >= 0) accumulate(l0, nrow[i]);
+    }
+  }
+  if (NB > 0 && nrow && EW) {
+    // deterministic block reduction: wave shfl_down tree, then waves in order
+    __shared__ double wh[DEC_THREADS / 64][NB > 0 ? NB : 1], wl[DEC_THREADS / 64][NB > 0 ? NB : 1];
+    __shared__ int wc[DEC_THREADS / 64][NB > 0 ? NB : 1];
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+      double h = hs[d], l = ls[d];
+      int c = cn[d];
+      for (int o = 32; o > 0; o >>= 1) {
+        const double h2 = __shfl_down(h, o, 64), l2 = __shfl_down(l, o, 64);
+        const int c2 = __shfl_down(c, o, 64);
+        const double s = h + h2;
+        const double bb = s - h;
+        const double err = (h - (s - bb)) + (h2 - bb);
+        h = s; l = (l + l2) + err; c += c2;
+      }
+      if (lane == 0) { wh[wid][d] = h; wl[wid][d] = l; wc[wid][d] = c; }
+    }
+    __syncthreads();
+    if (tid < NB) {
+      const int d = tid;
+      double h = 0.0, l = 0.0;
+      int c = 0;
+      for (int w = 0; w < DEC_THREADS / 64; ++w) {
+        const double h2 = wh[w][d];
+        const double s = h + h2;
+        const double bb = s - h;
+        const double err = (h - (s - bb)) + (h2 - bb);
+        h = s; l = (l + wl[w][d]) + err; c += wc[w][d];
+      }
+      const double sum = h + l;
+      EW[(int64_t)t * NB + d] = c > 0 ? sum / (double)c : qnan();
+      if (CNT) CNT[(int64_t)t * NB + d] = c;
+    }
+  }
+}
+
+// =====================================================================================
+// Kernel E: long-short series (one workgroup; T_m * n_bins is tiny).
+// =====================================================================================
+__global__ __launch_bounds__(256) void k_long_short(const double* __restrict__ EW,
+                                                    const int32_t* __restrict__ CNT, int T_m,
+                                                    int nb, double* __restrict__ LS) {
+  __shared__ int has_lo, has_hi;
+  if (threadIdx.x == 0) { has_lo = 0; has_hi = 0; }
+  __syncthreads();
+  for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
+    if (CNT[(int64_t)t * nb] > 0) atomicOr(&has_lo, 1);
+    if (CNT[(int64_t)t * nb + nb - 1] > 0) atomicOr(&has_hi, 1);
+  }
+  __syncthreads();
+  const bool both = has_lo && has_hi;
+  for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
+    const double* e = EW + (int64_t)t * nb;
+    const int32_t* c = CNT + (int64_t)t * nb;
+    bool any = false;
+    double mx = -INFINITY, mn = INFINITY;
+    for (int d = 0; d < nb; ++d) {
+      if (c[d] > 0) { any = true; mx = fmax(mx, e[d]); mn = fmin(mn, e[d]); }
+    }
+    double v = qnan();
+    if (any) v = both ? (e[nb - 1] - e[0]) : (mx - mn);
+    LS[t] = v;
+  }
+}
+
+// =====================================================================================
+// Date-shard exchange records (multi-GPU date sharding).
+// =====================================================================================
+#define SUM_SCALARS 6
+
+__global__ __launch_bounds__(256) void k_shard_summary(const double* __restrict__ PM, int T_m,
+                                                       int64_t N, int T, double* __restrict__ out) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  int64_t n = 0, fv = -1, lvi = -1;
+  double lv = qnan(), first = absent_val();
+  for (int m = 0; m < T_m; ++m) {
+    const double x = PM[(int64_t)m * N + a];
+    if (is_absent(x)) continue;
+    if (n == 0) first = x;
+    if (!isnan_d(x)) { if (fv < 0) fv = n; lvi = n; lv = x; }
+    ++n;
+  }
+  // tail: last T present rows, oldest first; head: last valid among rows [0, n-T)
+  const int k = (int)(n < T ? n : T);
+  int got = 0;
+  double head = qnan();
+  for (int j = 0; j < T - k; ++j) out[(int64_t)(SUM_SCALARS + j) * N + a] = absent_val();
+  int m = T_m - 1;
+  for (; m >= 0 && got < k; --m) {
+    const double x = PM[(int64_t)m * N + a];
+    if (is_absent(x)) continue;
+    out[(int64_t)(SUM_SCALARS + T - 1 - got) * N + a] = x;
+    ++got;
+  }
+  for (; m >= 0; --m) {
+    const double x = PM[(int64_t)m * N + a];
+    if (is_absent(x)) continue;
+    if (!isnan_d(x)) { head = x; break; }
+  }
+  out[0 * N + a] = (double)n;
+  out[1 * N + a] = (double)fv;
+  out[2 * N + a] = (double)lvi;
+  out[3 * N + a] = lv;
+  out[4 * N + a] = head;
+  out[5 * N + a] = first;
+}
+
+__global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ sm, int G, int g,
+                                                    int64_t N, int J, int skip,
+                                                    double* __restrict__ carry,
+                                                    double* __restrict__ next_pm) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  const int W = J + skip, T = W + 1, S = SUM_SCALARS + T;
+  auto at = [&](int h, int r) -> double { return sm[((int64_t)h * S + r) * N + a]; };
+  // next_pm: first present row after shard g
+  double npm = absent_val();
+  for (int h = g + 1; h < G; ++h) if (at(h, 0) > 0.0) { npm = at(h, 5); break; }
+  next_pm[a] = npm;
+  const double NaN = qnan();
+  // locate the oldest of the last T present rows of shards < g
+  int nv = 0, src_h = -1, src_j = -1;
+  for (int h = g - 1; h >= 0 && nv < T; --h) {
+    const int k = (int)fmin(at(h, 0), (double)T);
+    const int take = k < T - nv ? k : T - nv;
+    if (take > 0) { nv += take; src_h = h; src_j = T - take; }
+  }
+  double pff_before = NaN;
+  if (nv > 0) {
+    const int k0 = (int)fmin(at(src_h, 0), (double)T);
+    for (int j = src_j - 1; j > T - 1 - k0; --j) { const double x = at(src_h, SUM_SCALARS + j); if (!isnan_d(x)) { pff_before = x; break; } }
+    if (isnan_d(pff_before)) pff_before = at(src_h, 4);
+    if (isnan_d(pff_before))
+      for (int h = src_h - 1; h >= 0; --h) if (!isnan_d(at(h, 3))) { pff_before = at(h, 3); break; }
+  }
+  // replay oldest -> newest; the newest W rets become the ring (as factors fl(1+ret))
+  double pff = pff_before;
+  for (int k = 0; k < W; ++k) carry[(int64_t)k * N + a] = NaN;
+  int c = 0;
+  for (int h = src_h; h >= 0 && h < g; ++h) {
+    const int kh = (int)fmin(at(h, 0), (double)T);
+    for (int j = (h == src_h) ? src_j : T - kh; j < T; ++j, ++c) {
+      const double x = at(h, SUM_SCALARS + j);
+      const double nx = isnan_d(x) ? pff : x;
+      const double ret = nx / pff - 1.0;
+      pff = nx;
+      const int pos = c - (nv - W);
+      if (pos >= 0) carry[(int64_t)pos * N + a] = 1.0 + ret;
+    }
+  }
+  double lastv = NaN;
+  for (int h = g - 1; h >= 0; --h) if (!isnan_d(at(h, 3))) { lastv = at(h, 3); break; }
+  carry[(int64_t)W * N + a] = lastv;
+  double psff = NaN;
+  int64_t off = 0, f = -1;
+  for (int h = 0; h < g; ++h) {
+    if (f < 0 && at(h, 1) >= 0.0) f = off + (int64_t)at(h, 1);
+    off += (int64_t)at(h, 0);
+  }
+  if (f >= 0) {
+    int64_t offh = off;
+    for (int h = g - 1; h >= 0; --h) {
+      offh -= (int64_t)at(h, 0);
+      if (at(h, 2) >= 0.0) {
+        const int64_t li = offh + (int64_t)at(h, 2);
+        if (li >= f + J + skip) psff = at(h, 3);
+        break;
+      }
+    }
+  }
+  carry[(int64_t)(W + 1) * N + a] = psff;
+}
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+struct csm_ctx {
+  int device;
+  hipStream_t stream;
+  char err[512];
+};
+
+static int set_err(csm_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(c->err, sizeof(c->err), fmt, ap);
+    va_end(ap);
+  }
+  return code;
+}
+
+#define HIP_CHECK(ctx, call)                                                               \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return set_err(ctx, CSM_E_HIP, "%s: %s", #call, hipGetErrorString(e_));              \
+  } while (0)
+
+#define LAUNCH_CHECK(ctx, name)                                                            \
+  do {                                                                                     \
+    hipError_t e_ = hipGetLastError();                                                     \
+    if (e_ != hipSuccess) return set_err(ctx, CSM_E_HIP, "%s launch: %s", name, hipGetErrorString(e_)); \
+  } while (0)
+
+static int prep(csm_ctx* c) {
+  if (!c) return CSM_E_INVAL;
+  c->err[0] = 0;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  return CSM_OK;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+extern "C" {
+
+int csm_abi_version(void) { return CSM_ABI_VERSION; }
+
+int csm_create(int device, csm_ctx** out) {
+  if (!out) return CSM_E_INVAL;
+  *out = nullptr;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return CSM_E_HIP;
+  if (hipSetDevice(device) != hipSuccess) return CSM_E_HIP;
+  csm_ctx* c = (csm_ctx*)calloc(1, sizeof(csm_ctx));
+  if (!c) return CSM_E_INVAL;
+  c->device = device;
+  c->stream = nullptr;
+  *out = c;
+  return CSM_OK;
+}
+
+int csm_destroy(csm_ctx* ctx) {
+  free(ctx);
+  return CSM_OK;
+}
+
+const char* csm_last_error(const csm_ctx* ctx) { return ctx ? ctx->err : "null context"; }
+
+int csm_set_stream(csm_ctx* ctx, void* stream) {
+  if (!ctx) return CSM_E_INVAL;
+  ctx->stream = (hipStream_t)stream;
+  return CSM_OK;
+}
+
+int csm_sync(csm_ctx* ctx) {
+  int r = prep(ctx);
+  if (r) return r;
+  HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return CSM_OK;
+}
+
+int csm_month_end(csm_ctx* ctx, const double* P, const double* V, int64_t T_d, int64_t N,
+                  const int64_t* month_start, int32_t T_m, double* PM, double* VOL) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !PM || N <= 0 || T_d < 0 || T_m < 0 || T_m > 65535)
+    return set_err(ctx, CSM_E_INVAL, "csm_month_end: bad arguments (N=%lld T_d=%lld T_m=%d)",
+                   (long long)N, (long long)T_d, T_m);
+  if ((V == nullptr) != (VOL == nullptr))
+    return set_err(ctx, CSM_E_INVAL, "csm_month_end: V and VOL must both be given or both NULL");
+  if (T_m == 0) return CSM_OK;
+  const bool v2 = (N % 2 == 0) && aligned16(P) && aligned16(PM) && (!V || aligned16(V));
+  const int vec = v2 ? 2 : 1;
+  dim3 grid((unsigned)((N + 256LL * vec - 1) / (256LL * vec)), (unsigned)T_m);
+  if (v2) {
+    if (V) hipLaunchKernelGGL((k_month_end<2, true>), grid, dim3(256), 0, ctx->stream, P, V, month_start, N, PM, VOL);
+    else hipLaunchKernelGGL((k_month_end<2, false>), grid, dim3(256), 0, ctx->stream, P, V, month_start, N, PM, VOL);
+  } else {
+    if (V) hipLaunchKernelGGL((k_month_end<1, true>), grid, dim3(256), 0, ctx->stream, P, V, month_start, N, PM, VOL);
+    else hipLaunchKernelGGL((k_month_end<1, false>), grid, dim3(256), 0, ctx->stream, P, V, month_start, N, PM, VOL);
+  }
+  LAUNCH_CHECK(ctx, "k_month_end");
+  return CSM_OK;
+}
+
+int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                 double* R, double* M, double* NR, const double* carry, const double* next_pm,
+                 double* carry_out) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!PM || !M || !NR || N <= 0 || T_m < 0 || J < 1 || skip < 0 || J + skip > 256)
+    return set_err(ctx, CSM_E_INVAL, "csm_momentum: bad arguments (N=%lld T_m=%d J=%d skip=%d)",
+                   (long long)N, T_m, J, skip);
+  const int W = J + skip;
+  const int tpb = W <= 64 ? SCAN_THREADS : 64;  // ring = W * tpb doubles of LDS (<= 128 KiB)
+  const size_t lds = (size_t)W * tpb * sizeof(double);
+  const unsigned blocks = (unsigned)((N + tpb - 1) / tpb);
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_momentum,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_momentum, dim3(blocks), dim3(tpb), lds, ctx->stream, PM, T_m, N, J,
+                     skip, R, M, NR, carry, next_pm, carry_out);
+  LAUNCH_CHECK(ctx, "k_momentum");
+  return CSM_OK;
+}
+
+}  // extern "C"
+
+template <int NB>
+static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
+                           int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
+                           int32_t* CNT, int32_t* NV) {
+  if (v2) hipLaunchKernelGGL((k_deciles<NB, true>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV);
+  else hipLaunchKernelGGL((k_deciles<NB, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV);
+}
+
+extern "C" {
+
+int csm_deciles(csm_ctx* ctx, const double* M, const double* NR, int32_t T_m, int64_t N,
+                int32_t n_bins, const double* qtable, int8_t* L, double* EW, int32_t* CNT,
+                int32_t* NV) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!M || !L || !qtable || N <= 0 || T_m < 0 || n_bins < 1 || n_bins > MAXQ - 1 || N > 0x7FFFFFFFLL)
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles: bad arguments (N=%lld T_m=%d n_bins=%d)",
+                   (long long)N, T_m, n_bins);
+  if (NR && (!EW || !CNT))
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles: EW and CNT are required when NR is given");
+  if (T_m == 0) return CSM_OK;
+  QTab q;
+  for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
+  const bool v2 = (N % 2 == 0) && aligned16(M) && (!NR || aligned16(NR)) && (((uintptr_t)L & 1u) == 0);
+  if (!NR) {
+    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV);
+  } else {
+    switch (n_bins) {
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
+      default:
+        return set_err(ctx, CSM_E_INVAL, "csm_deciles: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", n_bins);
+    }
+  }
+  LAUNCH_CHECK(ctx, "k_deciles");
+  return CSM_OK;
+}
+
+int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T_m,
+                   int32_t n_bins, double* LS) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!EW || !CNT || !LS || T_m < 0 || n_bins < 1)
+    return set_err(ctx, CSM_E_INVAL, "csm_long_short: bad arguments");
+  if (T_m == 0) return CSM_OK;
+  hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
+  LAUNCH_CHECK(ctx, "k_long_short");
+  return CSM_OK;
+}
+
+int csm_shard_summary(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                      int32_t skip, double* out) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!PM || !out || N <= 0 || T_m < 0 || J < 1 || skip < 0 || J + skip > 256)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_summary: bad arguments");
+  const unsigned blocks = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(k_shard_summary, dim3(blocks), dim3(256), 0, ctx->stream, PM, T_m, N,
+                     J + skip + 1, out);
+  LAUNCH_CHECK(ctx, "k_shard_summary");
+  return CSM_OK;
+}
+
+int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, int64_t N,
+                   int32_t J, int32_t skip, double* carry, double* next_pm) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!summaries || !carry || !next_pm || N <= 0 || G < 1 || g < 0 || g >= G || J < 1 ||
+      skip < 0 || J + skip > 256)
+    return set_err(ctx, CSM_E_INVAL, "csm_fold_carry: bad arguments");
+  const unsigned blocks = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(k_fold_carry, dim3(blocks), dim3(256), 0, ctx->stream, summaries, G, g, N, J,
+                     skip, carry, next_pm);
+  LAUNCH_CHECK(ctx, "k_fold_carry");
+  return CSM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+"""Date-sharded multi-GPU pipeline: one process per GPU, torch.distributed over RCCL/xGMI.
+
+Each rank owns a contiguous range of whole calendar months of the daily panel (month-end
+aggregation is month-local, so no daily halo is exchanged).  The per-asset scan needs the
+state the earlier months leave behind (ret window, ffilled price, subset-ffilled price) and
+the first month price after the shard (next_ret of the shard's last ranked row).  Both are
+rebuilt exactly from one all-gather of prefix-independent per-asset shard summaries
+([S][N] f64, S = 6 + J + skip + 1).  After ranking and the per-date decile means, a second
+all-gather of the per-date [T_m_local][n_bins] mean/count rows gives every rank the full
+series; the long-short needs panel-wide column existence (run_demo.py:60-65).
+
+Two collectives per pass; no collective touches daily data.  The stage implementation is
+injected: `Engine` on the GPU (the product), anything with the same methods elsewhere (the
+CPU tests drive this orchestration with gloo and the oracle).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+def month_partition(T_m: int, G: int):
+    """Contiguous month ranges, earlier ranks take the remainder."""
+    base, rem = divmod(T_m, G)
+    out, m0 = [], 0
+    for g in range(G):
+        m1 = m0 + base + (1 if g < rem else 0)
+        out.append((m0, m1))
+        m0 = m1
+    return out
+
+
+def all_gather_stack(x: torch.Tensor, group=None) -> torch.Tensor:
+    """[G, *x.shape] all-gather; RCCL gets the single-buffer form, gloo the list form."""
+    G = dist.get_world_size(group)
+    if G == 1:
+        return x.unsqueeze(0)
+    out = torch.empty((G,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out.view(-1), x.contiguous().view(-1), group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), x.contiguous(), group=group)
+    return out
+
+
+@dataclass
+class ShardResult:
+    M: torch.Tensor      # [T_m_local][N] mom_J of this rank's months
+    NR: torch.Tensor     # [T_m_local][N] next_ret
+    L: torch.Tensor      # [T_m_local][N] labels
+    EW: torch.Tensor     # [T_m_total][n_bins] all ranks' decile means (rank order)
+    CNT: torch.Tensor    # [T_m_total][n_bins]
+    LS: torch.Tensor     # [T_m_total] long-short, NaN = dropped
+
+
+class DateShardPipeline:
+    """Runs one pass of the hot path on this rank's month range.
+
+    stages: object with month_end, shard_summary, fold_carry, momentum, deciles, long_short
+    (the `Engine` method signatures).  months_per_rank: local month counts of all ranks
+    (fixed for a run, so no size exchange happens per pass).
+    """
+
+    def __init__(self, stages, months_per_rank, J=12, skip=1, n_bins=10, group=None):
+        self.st = stages
+        self.months = list(months_per_rank)
+        self.J, self.skip, self.n_bins = J, skip, n_bins
+        self.group = group
+        self.G = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if len(self.months) != self.G:
+            raise ValueError(f"months_per_rank has {len(self.months)} entries for {self.G} ranks")
+        self.Tmax = max(self.months)
+
+    def run(self, P_local, month_start_local) -> ShardResult:
+        st, J, s, nb = self.st, self.J, self.skip, self.n_bins
+        PM, _ = st.month_end(P_local, month_start_local)
+        T_m, N = PM.shape
+        if T_m != self.months[self.rank]:
+            raise ValueError(f"rank {self.rank}: {T_m} months, partition says {self.months[self.rank]}")
+        summary = st.shard_summary(PM, J, s)
+        if self.G > 1:
+            summaries = all_gather_stack(summary, self.group)          # collective 1
+            carry, next_pm = st.fold_carry(summaries, self.rank, J, s)
+        else:
+            carry, next_pm = None, None
+        _, M, NR = st.momentum(PM, J, s, carry=carry, next_pm=next_pm)
+        L, EW, CNT, _ = st.deciles(M, NR, nb)
+        if self.G > 1:
+            pad_ew = torch.full((self.Tmax, nb), float("nan"), dtype=EW.dtype, device=EW.device)
+            pad_cnt = torch.zeros((self.Tmax, nb), dtype=CNT.dtype, device=CNT.device)
+            pad_ew[:T_m] = EW
+            pad_cnt[:T_m] = CNT
+            # one collective for both: counts ride as exact float64
+            packed = torch.cat([pad_ew, pad_cnt.to(EW.dtype)], dim=1)
+            allp = all_gather_stack(packed, self.group)                 # collective 2
+            ews = [allp[g, :self.months[g], :nb] for g in range(self.G)]
+            cns = [allp[g, :self.months[g], nb:] for g in range(self.G)]
+            EW = torch.cat(ews, 0).contiguous()
+            CNT = torch.cat(cns, 0).to(torch.int32).contiguous()
+        LS = st.long_short(EW, CNT)
+        return ShardResult(M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS)
+
+
+def virtual_shards(stages, P, month_start_host, G, J=12, skip=1, n_bins=10):
+    """Run the G-shard decomposition sequentially on ONE device (no collectives): the same
+    summary / fold / scan kernels as DateShardPipeline, for single-GPU verification that a
+    G-GPU run equals the 1-GPU run bit for bit.  Returns concatenated (M, NR, L, EW, CNT, LS)."""
+    import numpy as np
+
+    ms = np.asarray(month_start_host, dtype=np.int64)
+    T_m = len(ms) - 1
+    dev = P.device
+    parts = month_partition(T_m, G)
+    PMs = []
+    for (m0, m1) in parts:
+        d0, d1 = ms[m0], ms[m1]
+        msl = torch.from_numpy(ms[m0:m1 + 1] - d0).to(dev)
+        PM, _ = stages.month_end(P[d0:d1].contiguous(), msl)
+        PMs.append(PM)
+    summaries = torch.stack([stages.shard_summary(PM, J, skip) for PM in PMs])
+    Ms, NRs, Ls, EWs, CNTs = [], [], [], [], []
+    for g, PM in enumerate(PMs):
+        carry, next_pm = stages.fold_carry(summaries, g, J, skip)
+        _, M, NR = stages.momentum(PM, J, skip, carry=carry, next_pm=next_pm)
+        L, EW, CNT, _ = stages.deciles(M, NR, n_bins)
+        Ms.append(M); NRs.append(NR); Ls.append(L); EWs.append(EW); CNTs.append(CNT)
+    EW = torch.cat(EWs).contiguous()
+    CNT = torch.cat(CNTs).contiguous()
+    LS = stages.long_short(EW, CNT)
+    return torch.cat(Ms), torch.cat(NRs), torch.cat(Ls), EW, CNT, LS

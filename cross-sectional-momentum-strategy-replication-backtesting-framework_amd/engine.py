@@ -1,0 +1,202 @@
+"""Device engine: the momentum hot path on dense HBM-resident panels.
+
+`Engine` owns one csm context per device and launches on torch's current HIP stream, so
+torch events, graphs and allocations compose with it.  Tensors are torch ROCm tensors:
+  P[T_d][N] f64 daily prices (ABSENT payload = no row, NaN = missing price),
+  month_start[T_m+1] int64, everything else as in include/csmom.h.
+
+Reference mapping (file:line):
+  month_end   -> src/features.py:34-39      momentum   -> src/features.py:44-52, run_demo.py:48
+  deciles     -> run_demo.py:18-29,46,49-55  long_short -> run_demo.py:57-67
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ._lib import ABSENT_BITS, check, load_library
+
+QTABLE_CACHE: dict[int, np.ndarray] = {}
+
+
+def quantile_table(n_bins: int) -> np.ndarray:
+    """qcut's quantile grid as NumPy's percentile sees it ((linspace*100)/100)."""
+    q = QTABLE_CACHE.get(n_bins)
+    if q is None:
+        q = np.ascontiguousarray((np.linspace(0.0, 1.0, n_bins + 1) * 100.0) / 100.0)
+        QTABLE_CACHE[n_bins] = q
+    return q
+
+
+def absent_tensor(shape, device) -> torch.Tensor:
+    return torch.full(shape, ABSENT_BITS, dtype=torch.int64, device=device).view(torch.float64)
+
+
+def is_absent(x: torch.Tensor) -> torch.Tensor:
+    b = x.contiguous().view(torch.int64)
+    return (b & 0x7FF7FFFFFFFFFFFF) == ABSENT_BITS
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _need(t: torch.Tensor, name: str, dtype, shape, device):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name} must live on {device}, got {t.device}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+@dataclass
+class PipelineOut:
+    PM: torch.Tensor
+    M: torch.Tensor
+    NR: torch.Tensor
+    L: torch.Tensor
+    EW: torch.Tensor
+    CNT: torch.Tensor
+    LS: torch.Tensor
+    R: torch.Tensor | None = None
+    VOL: torch.Tensor | None = None
+    NV: torch.Tensor | None = None
+
+
+class Engine:
+    """Signal (J, skip) -> per-date n_bins labels -> equal-weight long-short, on one GPU."""
+
+    def __init__(self, device: int | str | torch.device = 0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("csmom.Engine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        st = self.lib.csm_create(self.device.index, ctypes.byref(h))
+        if st != 0:
+            raise RuntimeError(f"csm_create(device={self.device.index}) failed with {st}")
+        self.ctx = h
+
+    def __del__(self):
+        lib = getattr(self, "lib", None)
+        if lib is not None and getattr(self, "ctx", None):
+            lib.csm_destroy(self.ctx)
+            self.ctx = None
+
+    # ------------------------------------------------------------------ plumbing
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device)
+        self.lib.csm_set_stream(self.ctx, ctypes.c_void_p(s.cuda_stream))
+
+    def _call(self, name, *args):
+        self._bind_stream()
+        check(self.lib, self.ctx, getattr(self.lib, name)(self.ctx, *args), name)
+
+    def empty(self, shape, dtype=torch.float64):
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    # ------------------------------------------------------------------ stages
+    def month_end(self, P, month_start, V=None, PM=None, VOL=None):
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        PM = self.empty((T_m, N)) if PM is None else PM
+        _need(PM, "PM", torch.float64, (T_m, N), self.device)
+        if V is not None:
+            _need(V, "V", torch.float64, (T_d, N), self.device)
+            VOL = self.empty((T_m, N)) if VOL is None else VOL
+            _need(VOL, "VOL", torch.float64, (T_m, N), self.device)
+        else:
+            VOL = None
+        self._call("csm_month_end", _ptr(P), _ptr(V), T_d, N, _ptr(month_start), T_m,
+                   _ptr(PM), _ptr(VOL))
+        return PM, VOL
+
+    def momentum(self, PM, J=12, skip=1, with_ret=False, carry=None, next_pm=None,
+                 carry_out=None, out=None):
+        T_m, N = PM.shape
+        _need(PM, "PM", torch.float64, (T_m, N), self.device)
+        W = J + skip
+        if carry is not None:
+            _need(carry, "carry", torch.float64, (W + 2, N), self.device)
+        if next_pm is not None:
+            _need(next_pm, "next_pm", torch.float64, (N,), self.device)
+        if carry_out is not None:
+            _need(carry_out, "carry_out", torch.float64, (W + 2, N), self.device)
+        if out is None:
+            R = self.empty((T_m, N)) if with_ret else None
+            M = self.empty((T_m, N))
+            NR = self.empty((T_m, N))
+        else:
+            R, M, NR = out
+        self._call("csm_momentum", _ptr(PM), T_m, N, int(J), int(skip), _ptr(R), _ptr(M),
+                   _ptr(NR), _ptr(carry), _ptr(next_pm), _ptr(carry_out))
+        return R, M, NR
+
+    def deciles(self, M, NR=None, n_bins=10, out=None, with_nv=False):
+        T_m, N = M.shape
+        _need(M, "M", torch.float64, (T_m, N), self.device)
+        if NR is not None:
+            _need(NR, "NR", torch.float64, (T_m, N), self.device)
+        if out is None:
+            L = self.empty((T_m, N), torch.int8)
+            EW = self.empty((T_m, n_bins)) if NR is not None else None
+            CNT = self.empty((T_m, n_bins), torch.int32) if NR is not None else None
+            NV = self.empty((T_m,), torch.int32) if with_nv else None
+        else:
+            L, EW, CNT, NV = out
+        q = quantile_table(n_bins)
+        self._call("csm_deciles", _ptr(M), _ptr(NR), T_m, N, int(n_bins),
+                   q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV))
+        return L, EW, CNT, NV
+
+    def long_short(self, EW, CNT, LS=None):
+        T_m, nb = EW.shape
+        _need(EW, "EW", torch.float64, (T_m, nb), self.device)
+        _need(CNT, "CNT", torch.int32, (T_m, nb), self.device)
+        LS = self.empty((T_m,)) if LS is None else LS
+        self._call("csm_long_short", _ptr(EW), _ptr(CNT), T_m, nb, _ptr(LS))
+        return LS
+
+    def shard_summary(self, PM, J, skip, out=None):
+        T_m, N = PM.shape
+        _need(PM, "PM", torch.float64, (T_m, N), self.device)
+        S = 6 + J + skip + 1
+        out = self.empty((S, N)) if out is None else out
+        _need(out, "summary", torch.float64, (S, N), self.device)
+        self._call("csm_shard_summary", _ptr(PM), T_m, N, int(J), int(skip), _ptr(out))
+        return out
+
+    def fold_carry(self, summaries, g, J, skip, carry=None, next_pm=None):
+        G, S, N = summaries.shape
+        if S != 6 + J + skip + 1:
+            raise ValueError(f"summaries have {S} rows, expected {6 + J + skip + 1}")
+        _need(summaries, "summaries", torch.float64, (G, S, N), self.device)
+        carry = self.empty((J + skip + 2, N)) if carry is None else carry
+        next_pm = self.empty((N,)) if next_pm is None else next_pm
+        self._call("csm_fold_carry", _ptr(summaries), G, int(g), N, int(J), int(skip),
+                   _ptr(carry), _ptr(next_pm))
+        return carry, next_pm
+
+    def sync(self):
+        self._call("csm_sync")
+
+    # ------------------------------------------------------------------ pipeline
+    def run(self, P, month_start, J=12, skip=1, n_bins=10, V=None, with_ret=False):
+        """One full pass: month-end -> signal -> labels + EW decile means -> long-short."""
+        PM, VOL = self.month_end(P, month_start, V)
+        R, M, NR = self.momentum(PM, J, skip, with_ret=with_ret)
+        L, EW, CNT, NV = self.deciles(M, NR, n_bins, with_nv=True)
+        LS = self.long_short(EW, CNT)
+        return PipelineOut(PM=PM, M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS, R=R, VOL=VOL, NV=NV)

@@ -1,0 +1,96 @@
+"""Seeded synthetic daily panels generated directly in HBM (bench inputs; 8 GB at C4).
+
+Same conventions as SURVEY.md 8(d): log-returns N(mu_a, sigma_a), mu_a ~ N(3e-4, 2e-4),
+sigma_a ~ U(0.01, 0.04), P0 = 100, business-day calendar; masking mix of 5 % late
+listings, 5 % early delistings, 1 % NaN days, 0.2 % absent (asset, month) rows and 0.1 %
+all-NaN months.  Data generation is plumbing (torch ops), never part of a timed pass.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ._lib import ABSENT_BITS
+from .panel import month_offsets
+
+NAN_BITS = 0x7FF8000000000000
+
+
+@dataclass
+class DevicePanel:
+    P: torch.Tensor              # [T_d][N] float64 in HBM
+    month_start: torch.Tensor    # [T_m+1] int64 in HBM
+    month_start_host: np.ndarray
+    days: pd.DatetimeIndex
+    month_end: pd.DatetimeIndex
+
+    @property
+    def shape(self):
+        return tuple(self.P.shape)
+
+
+def bday_calendar(start: str, periods: int):
+    days = pd.bdate_range(start, periods=periods)
+    ms, mend = month_offsets(days)
+    return days, ms, mend
+
+
+def shard_calendar(start: str, periods_total: int, G: int, rank: int):
+    """Whole-month date shard `rank` of a G-way split of bdate_range(start, periods_total)."""
+    days, ms, mend = bday_calendar(start, periods_total)
+    T_m = len(ms) - 1
+    base, rem = divmod(T_m, G)
+    m0 = rank * base + min(rank, rem)
+    m1 = m0 + base + (1 if rank < rem else 0)
+    d0, d1 = ms[m0], ms[m1]
+    months = [base + (1 if g < rem else 0) for g in range(G)]
+    return days[d0:d1], (ms[m0:m1 + 1] - d0).astype(np.int64), mend[m0:m1], months
+
+
+def make_device_panel(N: int, days: pd.DatetimeIndex, month_start: np.ndarray, seed: int,
+                      device, late=0.05, delist=0.05, nan_day=0.01, absent_month=0.002,
+                      nan_month=0.001, block_days: int = 512) -> DevicePanel:
+    device = torch.device(device)
+    T_d = len(days)
+    T_m = len(month_start) - 1
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    f64 = dict(dtype=torch.float64, device=device)
+    mu = torch.randn(N, generator=g, **f64) * 2e-4 + 3e-4
+    sig = torch.rand(N, generator=g, **f64) * 0.03 + 0.01
+    list_day = torch.where(torch.rand(N, generator=g, **f64) < late,
+                           torch.randint(1, max(2, T_d // 2), (N,), generator=g, device=device),
+                           torch.zeros(N, dtype=torch.int64, device=device))
+    delist_day = torch.where(torch.rand(N, generator=g, **f64) < delist,
+                             torch.randint(max(1, T_d // 2), max(2, T_d), (N,), generator=g,
+                                           device=device),
+                             torch.full((N,), T_d, dtype=torch.int64, device=device))
+    am = torch.rand(T_m, N, generator=g, **f64) < absent_month      # absent (month, asset)
+    nm = torch.rand(T_m, N, generator=g, **f64) < nan_month         # all-NaN (month, asset)
+    day_month = torch.from_numpy(
+        np.repeat(np.arange(T_m), np.diff(month_start)).astype(np.int64)).to(device)
+    P = torch.empty(T_d, N, **f64)
+    run = torch.zeros(N, **f64)
+    absent = torch.tensor(ABSENT_BITS, dtype=torch.int64, device=device)
+    qnan = torch.tensor(NAN_BITS, dtype=torch.int64, device=device)
+    for d0 in range(0, T_d, block_days):
+        d1 = min(T_d, d0 + block_days)
+        lr = torch.randn(d1 - d0, N, generator=g, **f64) * sig + mu
+        c = torch.cumsum(lr, 0) + run
+        run = c[-1].clone()
+        blk = (100.0 * torch.exp(c)).view(torch.int64)
+        dd = torch.arange(d0, d1, device=device)[:, None]
+        dm = day_month[d0:d1]
+        gone = (dd < list_day[None, :]) | (dd >= delist_day[None, :]) | am[dm]
+        nanc = (torch.rand(d1 - d0, N, generator=g, **f64) < nan_day) | nm[dm]
+        blk = torch.where(nanc, qnan, blk)
+        blk = torch.where(gone, absent, blk)
+        P[d0:d1] = blk.view(torch.float64)
+        del lr, c, blk, gone, nanc
+    ms_dev = torch.from_numpy(np.ascontiguousarray(month_start, dtype=np.int64)).to(device)
+    mend = (days[month_start[:-1]] + pd.offsets.MonthEnd(0)) if T_m else pd.DatetimeIndex([])
+    return DevicePanel(P=P, month_start=ms_dev, month_start_host=np.asarray(month_start),
+                       days=days, month_end=pd.DatetimeIndex(mend))

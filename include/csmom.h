@@ -1,0 +1,126 @@
+/*
+ * csmom.h -- C ABI of libcsmom.so, the MI355X (gfx950) engine for the cross-sectional
+ * momentum backtest hot path of
+ * AkshayJha22/Cross-Sectional-Momentum-Strategy-Replication-Backtesting-Framework.
+ *
+ * The reference has no FFI: its boundary is plain Python functions on pandas objects
+ * (SURVEY.md section 8(b)).  Each entry point below replaces the arithmetic of one of
+ * those functions; the Python layer in the package keeps the reference's signatures and
+ * calls these through ctypes.
+ *
+ * Conventions
+ *   - Every array argument is a DEVICE pointer (hipMalloc / torch ROCm tensor) unless it
+ *     is documented as a host pointer.  Buffers are caller-owned.
+ *   - Dense row-major [T][N] layouts, assets fastest, float64 throughout.
+ *   - A cell with no daily row ("absent") holds the NaN payload CSM_ABSENT_BITS; a present
+ *     row with a missing price holds an ordinary NaN.
+ *   - Calls are asynchronous on the context's stream (csm_set_stream); csm_sync waits.
+ *   - Every call returns CSM_OK (0) or a negative status; csm_last_error() describes it.
+ *   - A context is not thread-safe; separate contexts may be used concurrently.
+ */
+#ifndef CSMOM_H
+#define CSMOM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CSM_ABI_VERSION 1
+#define CSM_ABSENT_BITS 0x7FF4000000000001ULL
+
+#define CSM_OK 0
+#define CSM_E_INVAL (-1)   /* bad argument (null pointer, size, unsupported parameter) */
+#define CSM_E_HIP (-2)     /* HIP runtime / launch failure */
+
+typedef struct csm_ctx csm_ctx;
+
+int csm_abi_version(void);
+
+/* Create a context bound to HIP device `device` (stream = the null stream). */
+int csm_create(int device, csm_ctx** out);
+int csm_destroy(csm_ctx* ctx);
+const char* csm_last_error(const csm_ctx* ctx);
+/* Launch subsequent work on `stream` (a hipStream_t; NULL = the null stream). */
+int csm_set_stream(csm_ctx* ctx, void* stream);
+int csm_sync(csm_ctx* ctx);
+
+/*
+ * Month-end aggregation.  Replaces the `groupby(['ticker', Grouper(freq='ME')])
+ * .agg(adj_close=last, monthly_volume=sum)` of src/features.py:34-39.
+ *   P[T_d][N]        daily adj_close (ABSENT / NaN encoded)
+ *   V[T_d][N]        daily volume, nullable (NaN counts as 0, features.py:31)
+ *   month_start[T_m+1] int64 day offsets of each month (device)
+ *   PM[T_m][N]       out: last non-NaN price; NaN if the month has rows but no price;
+ *                    ABSENT if it has no row
+ *   VOL[T_m][N]      out, nullable: pandas-Kahan sum of volume over present days
+ */
+int csm_month_end(csm_ctx* ctx, const double* P, const double* V, int64_t T_d, int64_t N,
+                  const int64_t* month_start, int32_t T_m, double* PM, double* VOL);
+
+/*
+ * ret_1m / mom_J / next_ret scan over present rows of each asset.  Replaces
+ * src/features.py:44-52 (pct_change with ffill; shift(skip).rolling(J).apply(prod))
+ * and run_demo.py:48 (next-row return within the ranked subset).
+ *   PM[T_m][N]   month prices from csm_month_end
+ *   R, M, NR     out [T_m][N]; R nullable.  NaN where undefined or absent.
+ *   carry        nullable [(J+skip)+2][N]: inherited scan state for a date shard
+ *                (rows 0..J+skip-1: ring of factors fl(1+ret), oldest first;
+ *                row J+skip: pff (last valid price); row J+skip+1: psff)
+ *   next_pm      nullable [N]: month price of the first present row after the panel
+ *                (ABSENT if none)
+ *   carry_out    nullable [(J+skip)+2][N]: scan state after the panel
+ * J >= 1, skip >= 0, J + skip <= 256.
+ */
+int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                 int32_t skip, double* R, double* M, double* NR, const double* carry,
+                 const double* next_pm, double* carry_out);
+
+/*
+ * Per-date qcut labels, fused with the equal-weight decile means.  Replaces
+ * run_demo.py:18-29 (assign_deciles_per_date via pd.qcut(duplicates='drop')),
+ * run_demo.py:46 (groupby('date').transform) and run_demo.py:49-55 (dropna +
+ * groupby(['date','decile']).next_ret.mean()).
+ *   M[T_m][N]     signal (NaN = not ranked)
+ *   NR[T_m][N]    nullable: next-row returns; when NULL, EW/CNT are not produced
+ *   qtable        HOST pointer, n_bins+1 quantile levels as NumPy's percentile sees them
+ *                 ((linspace(0,1,n+1)*100)/100)
+ *   L[T_m][N]     out int8 labels, -1 = NaN
+ *   EW[T_m][n_bins]  out, nullable: mean next_ret per (date, label), NaN if empty
+ *   CNT[T_m][n_bins] out, nullable: row counts per (date, label)
+ *   NV[T_m]       out, nullable: ranked rows per date
+ * n_bins in {2,3,4,5,10,20} (any n_bins in [1,20] when NR == NULL).
+ */
+int csm_deciles(csm_ctx* ctx, const double* M, const double* NR, int32_t T_m, int64_t N,
+                int32_t n_bins, const double* qtable, int8_t* L, double* EW, int32_t* CNT,
+                int32_t* NV);
+
+/*
+ * Long-short series.  Replaces run_demo.py:57-67: top minus bottom label mean when both
+ * columns occur anywhere in the panel, else per-date max minus min; NaN = dropped date.
+ *   EW, CNT [T_m][n_bins] from csm_deciles;  LS[T_m] out.
+ */
+int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T_m,
+                   int32_t n_bins, double* LS);
+
+/*
+ * Date-shard summary of a shard's month prices (prefix-independent), [S][N] float64 with
+ * S = 6 + J + skip + 1 (layout in DESIGN.md / oracle shard_summary).  No reference
+ * counterpart: it is the exchange record of the multi-GPU date sharding.
+ */
+int csm_shard_summary(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                      int32_t skip, double* out);
+
+/*
+ * Fold the all-gathered summaries [G][S][N] into shard g's inherited scan state
+ * (carry [(J+skip)+2][N]) and next_pm[N], bit-exactly equal to an unsharded scan.
+ */
+int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, int64_t N,
+                   int32_t J, int32_t skip, double* carry, double* next_pm);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CSMOM_H */

@@ -1,0 +1,128 @@
+"""GPU: date-shard decomposition == unsharded (bit for bit) and the drop-in API on real data."""
+import io
+import contextlib
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from conftest import bits_equal, load_golden, max_rel
+from oracle import csmom_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _up(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
+
+
+@pytest.mark.parametrize("J,skip", [(12, 1), (3, 0), (9, 2)])
+@pytest.mark.parametrize("G", [2, 3, 5, 8])
+def test_virtual_shards_equal_unsharded(engine, J, skip, G):
+    import csmom
+    from csmom.distributed import virtual_shards
+    z = load_golden("edge")
+    P, ms = _up(z["P"]), z["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), J, skip, 10)
+    M, NR, L, EW, CNT, LS = virtual_shards(engine, P, ms, G, J, skip, 10)
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L)
+    assert torch.equal(CNT, out.CNT)
+    assert bits_equal(EW.cpu().numpy(), out.EW.cpu().numpy())
+    assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+
+
+def test_summary_and_fold_match_oracle(engine):
+    z = load_golden("edge")
+    J, skip = 12, 1
+    PM = O.month_end(z["P"], z["month_start"])[0]
+    parts = O.month_ranges(PM.shape[0], 4)
+    sums = np.stack([O.shard_summary(PM[a:b], J, skip) for a, b in parts])
+    gs = torch.stack([engine.shard_summary(_up(PM[a:b]), J, skip) for a, b in parts])
+    assert bits_equal(gs.cpu().numpy(), sums)
+    for g in range(4):
+        st, npm = O.fold_carry(sums, g, J, skip)
+        carry, next_pm = engine.fold_carry(gs, g, J, skip)
+        c = carry.cpu().numpy()
+        assert bits_equal(c[:J + skip], 1.0 + st.ring), g
+        assert bits_equal(c[J + skip], st.pff), g
+        assert bits_equal(c[J + skip + 1], st.psff), g
+        assert bits_equal(next_pm.cpu().numpy(), npm), g
+
+
+def test_carry_out_chains(engine):
+    """Running the scan in two chunks with carry_out -> carry equals one scan."""
+    z = load_golden("longwin")
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    J, skip = 24, 1
+    _, M, NR = engine.momentum(PM, J, skip)
+    cut = PM.shape[0] // 2
+    co = torch.empty((J + skip + 2, PM.shape[1]), dtype=torch.float64, device="cuda:0")
+    _, M1, _ = engine.momentum(PM[:cut].contiguous(), J, skip, carry_out=co)
+    _, M2, _ = engine.momentum(PM[cut:].contiguous(), J, skip, carry=co)
+    assert bits_equal(torch.cat([M1, M2]).cpu().numpy(), M.cpu().numpy())
+
+
+def _real_long():
+    z = load_golden("real_data")
+    P, V = z["P"], z["V"]
+    days = pd.DatetimeIndex(z["day_ns"])
+    tick = z["tickers"]
+    pres = ~O.is_absent(P)
+    dd, aa = np.nonzero(pres.T)[1], np.nonzero(pres.T)[0]
+    return pd.DataFrame({"date": days[dd], "ticker": tick[aa], "adj_close": P[dd, aa],
+                         "volume": V[dd, aa]}), z
+
+
+def test_compute_monthly_momentum_frame(engine):
+    import csmom
+    df, z = _real_long()
+    out = csmom.compute_monthly_momentum_from_daily(df, 12, 1)
+    assert list(out.columns) == ["ticker", "date", "adj_close", "monthly_volume", "ret_1m", "mom_J"]
+    tix = {t: i for i, t in enumerate(z["tickers"])}
+    mix = {d: i for i, d in enumerate(pd.DatetimeIndex(z["month_end_ns"]))}
+    a = out["ticker"].map(tix).to_numpy()
+    m = out["date"].map(mix).to_numpy()
+    assert len(out) == int(z["J12s1_present"].sum())
+    assert bits_equal(out["adj_close"].to_numpy(), z["J12s1_PM"][m, a])
+    assert bits_equal(out["ret_1m"].to_numpy(), z["J12s1_R"][m, a])
+    assert bits_equal(out["mom_J"].to_numpy(), z["J12s1_M"][m, a])
+    assert bits_equal(out["monthly_volume"].to_numpy(), z["J12s1_VOL"][m, a])
+
+
+def test_monthly_replication_prints_reference_numbers(engine, tmp_path):
+    import csmom
+    df, z = _real_long()
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        res = csmom.monthly_replication(df, {}, plot_path=str(tmp_path / "cum.png"))
+    assert len(res.mom_ret) == 70
+    assert abs(res.mean - float(z["J12s1_mean"])) <= 1e-10 * abs(float(z["J12s1_mean"]))
+    assert abs(res.sharpe - float(z["J12s1_sharpe"])) <= 1e-10 * abs(float(z["J12s1_sharpe"]))
+    assert max_rel(res.cum.to_numpy(), z["J12s1_cum"]) <= 1e-10
+    assert (tmp_path / "cum.png").exists()
+    printed = str(z["printed"])
+    assert buf.getvalue().splitlines()[0].split(":")[0] == printed.splitlines()[0].split(":")[0]
+
+
+def test_assign_deciles_per_date_api(engine):
+    import csmom
+    d = load_golden("deciles")
+    v, o, lab = d["values"], d["offsets"], d["labels"]
+    for i in range(0, len(o) - 1, 97):
+        x = pd.Series(v[o[i]:o[i + 1]], index=np.arange(o[i + 1] - o[i]) * 3)
+        got = csmom.assign_deciles_per_date(x, n=10)
+        ref = lab[o[i]:o[i + 1]]
+        assert np.array_equal(got.to_numpy(dtype=np.float64), ref, equal_nan=True)
+        assert got.index.equals(x.index)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    import csmom
+    from csmom import _lib
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setenv("CSMOM_LIB", str(tmp_path / "nope.so"))
+    with pytest.raises(csmom.CsmUnavailable):
+        csmom.Engine(0)
