@@ -1,0 +1,60 @@
+"""The C ABI library builds for gfx950, loads here (no GPU) and exports what include/csmom.h
+declares; argument validation and GPU-less failure paths return status codes."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def header_symbols():
+    txt = (ROOT / "include" / "csmom.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(csm_\w+)\(", txt, re.M)))
+
+
+def test_header_declares_expected_api():
+    syms = header_symbols()
+    for s in ("csm_create", "csm_month_end", "csm_momentum", "csm_deciles", "csm_long_short",
+              "csm_shard_summary", "csm_fold_carry", "csm_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    import csmom
+    lib = csmom.load_library()
+    raw = ctypes.CDLL(str(csmom.lib_path()))
+    for s in header_symbols():
+        assert hasattr(raw, s), s
+    assert lib.csm_abi_version() == 1
+
+
+def test_null_context_is_inval():
+    import csmom
+    lib = csmom.load_library()
+    assert lib.csm_month_end(None, None, None, 0, 0, None, 0, None, None) == -1
+    assert lib.csm_momentum(None, None, 0, 0, 12, 1, None, None, None, None, None, None) == -1
+    assert lib.csm_deciles(None, None, None, 0, 0, 10, None, None, None, None, None) == -1
+    assert lib.csm_sync(None) == -1
+    assert lib.csm_last_error(None) == b"null context"
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import csmom
+    lib = csmom.load_library()
+    h = ctypes.c_void_p()
+    assert lib.csm_create(0, ctypes.byref(h)) != 0
+    assert not h.value
+
+
+def test_engine_requires_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import csmom
+    with pytest.raises(RuntimeError):
+        csmom.Engine(0)
