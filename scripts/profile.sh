@@ -1,0 +1,19 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py's dominant kernels.  Kernel trace + stats in one run; HBM
+# counters in separate --pmc passes (FETCH_SIZE and WRITE_SIZE cannot share a pass).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG="${1:-r01}"
+CFG="${2:-c4}"
+OUT="gpurun_out/prof_${TAG}_${CFG}"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+BENCH="bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.log" 2>&1
+rc=$?; tail -2 "$OUT/trace.log"; [ $rc -eq 0 ] || { echo "FATAL trace rc=$rc"; exit $rc; }
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1
+rc=$?; tail -1 "$OUT/pmc_fetch.log"; [ $rc -eq 0 ] || { echo "FATAL fetch rc=$rc"; exit $rc; }
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
+rc=$?; tail -1 "$OUT/pmc_write.log"; [ $rc -eq 0 ] || { echo "FATAL write rc=$rc"; exit $rc; }
+find "$OUT" -name "*.csv" | head -20
+echo "profile done"
