@@ -99,12 +99,15 @@ def main():
     pipe = DateShardPipeline(eng, months, J, skip, nb) if world > 1 else None
 
     # preallocated outputs: the timed loop performs no allocation
-    PM = eng.empty((T_m, N))
+    max_days = int(np.diff(ms_host).max())
+    fused = eng.use_fused(panel.P, None, max_days)
+    PM = None if fused else eng.empty((T_m, N))
     M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
     L = eng.empty((T_m, N), torch.int8)
     EW, CNT = eng.empty((T_m, nb)), eng.empty((T_m, nb), torch.int32)
     LS = eng.empty((T_m,))
-    stage_names = ["month_end", "scan", "deciles", "long_short"]
+    stage_names = (["signal(k_signal)", "deciles(k_deciles)", "long_short"] if fused else
+                   ["month_end(k_month_end)", "scan(k_momentum)", "deciles(k_deciles)", "long_short"])
     nst = len(stage_names) + 1
     step_events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst)]
                    for _ in range(args.steps)]
@@ -114,15 +117,22 @@ def main():
         if pipe is not None:
             r = pipe.run(panel.P, panel.month_start)
             return r.LS
-        ev[0].record()
-        eng.month_end(panel.P, panel.month_start, PM=PM)
-        ev[1].record()
-        eng.momentum(PM, J, skip, out=(None, M, NR))
-        ev[2].record()
+        i = 0
+        ev[i].record()
+        if fused:
+            eng.signal(panel.P, panel.month_start, max_days, J, skip, out=(None, None, M, NR))
+        else:
+            eng.month_end(panel.P, panel.month_start, PM=PM)
+            i += 1
+            ev[i].record()
+            eng.momentum(PM, J, skip, out=(None, M, NR))
+        i += 1
+        ev[i].record()
         eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
-        ev[3].record()
+        i += 1
+        ev[i].record()
         eng.long_short(EW, CNT, LS)
-        ev[4].record()
+        ev[i + 1].record()
         return LS
 
     for _ in range(args.warmup):
@@ -183,10 +193,15 @@ def main():
         roofline = None
         if world == 1:
             me_ms = stage_ms[0] / args.steps
-            alg_me = 8.0 * N * T_d + 8.0 * N * T_m          # read P once, write PM once
+            if fused:
+                kname = "k_signal"
+                alg_me = 8.0 * N * T_d + 16.0 * N * T_m       # read P once, write mom + next_ret
+            else:
+                kname = "k_month_end"
+                alg_me = 8.0 * N * T_d + 8.0 * N * T_m          # read P once, write PM once
             achieved = alg_me / (me_ms * 1e-3) / 1e9
             traffic = None
-            pmc = ROOT / "profiles" / "pmc_month_end.json"
+            pmc = ROOT / "profiles" / f"pmc_{kname}.json"
             if pmc.exists():
                 try:
                     pj = json.loads(pmc.read_text())
@@ -194,7 +209,7 @@ def main():
                         traffic = pj.get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
-            roofline = dict(bound="hbm", kernel="k_month_end", achieved=round(achieved, 1),
+            roofline = dict(bound="hbm", kernel=kname, achieved=round(achieved, 1),
                             peak=HBM_PEAK_GBS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
                             traffic=traffic, algorithmic_bytes_per_launch=alg_me,
                             avg_launch_ms=round(me_ms, 4))

@@ -20,7 +20,7 @@ ABSENT_BITS = 0x7FF4000000000001
 EXPORTS = (
     "csm_abi_version", "csm_create", "csm_destroy", "csm_last_error", "csm_set_stream",
     "csm_sync", "csm_month_end", "csm_momentum", "csm_deciles", "csm_long_short",
-    "csm_shard_summary", "csm_fold_carry",
+    "csm_shard_summary", "csm_fold_carry", "csm_signal",
 )
 
 
@@ -55,6 +55,8 @@ def _declare(lib):
         "csm_sync": (ctypes.c_int, [_p]),
         "csm_month_end": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i32, _p, _p]),
         "csm_momentum": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p]),
+        "csm_signal": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
+                                      _p, _p, _p]),
         "csm_deciles": (ctypes.c_int, [_p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
         "csm_long_short": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p]),
         "csm_shard_summary": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p]),

@@ -134,10 +134,104 @@ __global__ __launch_bounds__(256) void k_month_end(const double* __restrict__ P,
 }
 
 // =====================================================================================
-// Kernel B: per-asset scan over months (present rows only).  One thread per asset; the
-// J+skip ret ring lives in LDS (slot-major, thread-fastest: conflict-free).  PM rows are
-// prefetched CHUNK months ahead so each wave keeps CHUNK*512 B in flight.
-// mom = (prod_{oldest..newest of the J oldest ring entries} fl(1+ret)) - 1, left to right.
+// Per-asset scan state and one present-row step (shared by k_momentum and k_signal).
+// The J+skip ring of factors fl(1+ret) lives in LDS, slot-major with a per-lane column
+// (stride RS doubles), so a wave's ring accesses are conflict-free.
+// mom = (prod over the J oldest ring entries of fl(1+ret), left to right) - 1.
+// =====================================================================================
+struct ScanLane {
+  double pff;   // last valid month price (features.py:44 grouped ffill)
+  double psff;  // last valid price among ranked rows (run_demo.py:48 subset ffill)
+  int head;     // index of the oldest ring entry
+  int prev;     // month of the pending ranked row (its next_ret waits for the next row)
+};
+
+__device__ __forceinline__ void scan_init(ScanLane& s, double* ring, int RS, int W,
+                                          const double* __restrict__ carry, int64_t N,
+                                          int64_t a, bool live) {
+  if (live && carry) {
+    for (int k = 0; k < W; ++k) ring[k * RS] = carry[(int64_t)k * N + a];
+    s.pff = carry[(int64_t)W * N + a];
+    s.psff = carry[(int64_t)(W + 1) * N + a];
+  } else {
+    for (int k = 0; k < W; ++k) ring[k * RS] = qnan();
+    s.pff = qnan();
+    s.psff = qnan();
+  }
+  s.head = 0;
+  s.prev = -1;
+}
+
+// Consumes month m's price x of asset a; returns mom (NaN when absent / undefined).
+__device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double* ring, int RS,
+                                            int W, int J, int64_t N, int64_t a,
+                                            double* __restrict__ R, double* __restrict__ M,
+                                            double* __restrict__ NR) {
+  const double NaN = qnan();
+  const int64_t o = (int64_t)m * N + a;
+  if (is_absent(x)) {
+    if (R) R[o] = NaN;
+    M[o] = NaN;
+    NR[o] = NaN;
+    return NaN;
+  }
+  const bool xv = !isnan_d(x);
+  const double pnew = xv ? x : s.pff;
+  const double ret = pnew / s.pff - 1.0;
+  s.pff = pnew;
+  ring[s.head * RS] = 1.0 + ret;          // push: overwrite the oldest, advance head
+  s.head = (s.head + 1 == W) ? 0 : s.head + 1;
+  double acc = ring[s.head * RS];
+  int idx = s.head;
+  for (int k = 1; k < J; ++k) {
+    idx = (idx + 1 == W) ? 0 : idx + 1;
+    acc = acc * ring[idx * RS];
+  }
+  const double mom = acc - 1.0;
+  const bool ranked = !isnan_d(mom);
+  const double ps_new = xv ? x : s.psff;
+  if (s.prev >= 0) NR[(int64_t)s.prev * N + a] = ps_new / s.psff - 1.0;
+  if (ranked) {
+    s.psff = ps_new;
+    s.prev = m;
+  } else {
+    NR[o] = NaN;
+    s.prev = -1;
+  }
+  if (R) R[o] = ret;
+  M[o] = mom;
+  return mom;
+}
+
+__device__ __forceinline__ void scan_finish(ScanLane& s, double* ring, int RS, int W, int64_t N,
+                                            int64_t a, double* __restrict__ NR,
+                                            const double* __restrict__ next_pm,
+                                            double* __restrict__ carry_out) {
+  if (s.prev >= 0) {
+    double nr = qnan();
+    if (next_pm) {
+      const double x = next_pm[a];
+      if (!is_absent(x)) {
+        const double ps_new = isnan_d(x) ? s.psff : x;
+        nr = ps_new / s.psff - 1.0;
+      }
+    }
+    NR[(int64_t)s.prev * N + a] = nr;
+  }
+  if (carry_out) {
+    int idx = s.head;
+    for (int k = 0; k < W; ++k) {  // carry rows hold the ring's factors, oldest first
+      carry_out[(int64_t)k * N + a] = ring[idx * RS];
+      idx = (idx + 1 == W) ? 0 : idx + 1;
+    }
+    carry_out[(int64_t)W * N + a] = s.pff;
+    carry_out[(int64_t)(W + 1) * N + a] = s.psff;
+  }
+}
+
+// =====================================================================================
+// Kernel B: per-asset scan over month prices (present rows only).  One thread per asset;
+// PM rows prefetched SCAN_CHUNK months ahead (SCAN_CHUNK * 512 B in flight per wave).
 // =====================================================================================
 #define SCAN_THREADS 128
 #define SCAN_CHUNK 16
@@ -151,22 +245,11 @@ __global__ __launch_bounds__(256) void k_momentum(
   const int tid = threadIdx.x;
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + tid;
   const bool live = a < N;
-  const int RS = blockDim.x;           // ring stride (slot-major, thread-fastest)
-  double* ring = ring_lds + tid;       // ring[k * RS]
-  double pff, psff;
-  if (live && carry) {
-    for (int k = 0; k < W; ++k) ring[k * RS] = carry[(int64_t)k * N + a];
-    pff = carry[(int64_t)W * N + a];
-    psff = carry[(int64_t)(W + 1) * N + a];
-  } else {
-    for (int k = 0; k < W; ++k) ring[k * RS] = qnan();
-    pff = qnan();
-    psff = qnan();
-  }
+  const int RS = blockDim.x;
+  double* ring = ring_lds + tid;
+  ScanLane s;
+  scan_init(s, ring, RS, W, carry, N, a, live);
   if (!live) return;
-  int head = 0;     // index of the oldest ring entry
-  int prev = -1;    // month of the pending ranked row (its next_ret waits for the next row)
-  const double NaN = qnan();
   for (int m0 = 0; m0 < T_m; m0 += SCAN_CHUNK) {
     double buf[SCAN_CHUNK];
 #pragma unroll
@@ -176,61 +259,83 @@ __global__ __launch_bounds__(256) void k_momentum(
     for (int j = 0; j < SCAN_CHUNK; ++j) {
       const int m = m0 + j;
       if (m >= T_m) break;
-      const double x = buf[j];
-      const int64_t o = (int64_t)m * N + a;
-      if (is_absent(x)) {
-        if (R) R[o] = NaN;
-        M[o] = NaN;
-        NR[o] = NaN;
-        continue;
-      }
-      const bool xv = !isnan_d(x);
-      const double pnew = xv ? x : pff;
-      const double ret = pnew / pff - 1.0;
-      pff = pnew;
-      // push: overwrite the oldest, advance head
-      ring[head * RS] = 1.0 + ret;
-      head = (head + 1 == W) ? 0 : head + 1;
-      double acc = ring[head * RS];
-      int idx = head;
-      for (int k = 1; k < J; ++k) {
-        idx = (idx + 1 == W) ? 0 : idx + 1;
-        acc = acc * ring[idx * RS];
-      }
-      const double mom = acc - 1.0;
-      const bool ranked = !isnan_d(mom);
-      const double ps_new = xv ? x : psff;
-      if (prev >= 0) NR[(int64_t)prev * N + a] = ps_new / psff - 1.0;
-      if (ranked) {
-        psff = ps_new;
-        prev = m;
-      } else {
-        NR[o] = NaN;
-        prev = -1;
-      }
-      if (R) R[o] = ret;
-      M[o] = mom;
+      scan_step(s, buf[j], m, ring, RS, W, J, N, a, R, M, NR);
     }
   }
-  if (prev >= 0) {
-    double nr = NaN;
-    if (next_pm) {
-      const double x = next_pm[a];
-      if (!is_absent(x)) {
-        const double ps_new = isnan_d(x) ? psff : x;
-        nr = ps_new / psff - 1.0;
-      }
+  scan_finish(s, ring, RS, W, N, a, NR, next_pm, carry_out);
+}
+
+// =====================================================================================
+// Kernel AB (fused): month-end aggregation + scan in one stream over the daily panel, for
+// large N.  One wave per block, two assets per lane (16-B row loads, 1 KiB per wave-
+// instruction).  While month m is reduced and scanned, all MAXD day rows of month m+1 are
+// already in flight (register double buffer).  Months shorter than MAXD re-load their last
+// row into the spare slots: those loads hit L1/L2 (no extra HBM bytes), keep the load count
+// fixed so vmcnt waits stay counted, and do not change "last non-NaN" / "any present".
+// The month prices never round-trip through HBM unless PM is requested.
+// =====================================================================================
+template <int MAXD>
+__global__ __launch_bounds__(64) void k_signal(
+    const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
+    int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
+    double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
+    double* __restrict__ carry_out) {
+  extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][128]
+  const int W = J + skip;
+  const int tid = threadIdx.x;
+  const int64_t a0 = ((int64_t)blockIdx.x * 64 + tid) * 2;
+  const bool live = a0 < N;
+  double* ring0 = ring_lds + 2 * tid;
+  double* ring1 = ring0 + 1;
+  const int RS = 128;
+  ScanLane s0, s1;
+  scan_init(s0, ring0, RS, W, carry, N, a0, live);
+  scan_init(s1, ring1, RS, W, carry, N, a0 + 1, live);
+  const double* base = P + (live ? a0 : 0);
+  // Loads are issued unconditionally (months past the end re-load the last month: cache
+  // hits) so every wait is a counted vmcnt; only the processing is guarded.
+  auto load_month = [&](double2 (&buf)[MAXD], int mm) {
+    mm = mm < T_m ? mm : T_m - 1;
+    const int64_t f0 = month_start[mm], nn = month_start[mm + 1] - f0;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k)
+      buf[k] = *reinterpret_cast<const double2*>(base + (f0 + (k < nn ? k : nn - 1)) * N);
+  };
+  auto process = [&](const double2 (&X)[MAXD], int m) {
+    double last0 = 0.0, last1 = 0.0;
+    bool p0 = false, p1 = false, v0 = false, v1 = false;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+      const double x0 = X[k].x, x1 = X[k].y;
+      const bool q0 = !is_absent(x0), q1 = !is_absent(x1);
+      const bool ok0 = q0 && !isnan_d(x0), ok1 = q1 && !isnan_d(x1);
+      p0 |= q0; p1 |= q1; v0 |= ok0; v1 |= ok1;
+      last0 = ok0 ? x0 : last0;
+      last1 = ok1 ? x1 : last1;
     }
-    NR[(int64_t)prev * N + a] = nr;
+    const double pm0 = p0 ? (v0 ? last0 : qnan()) : absent_val();
+    const double pm1 = p1 ? (v1 ? last1 : qnan()) : absent_val();
+    if (live) {
+      if (PMo) *reinterpret_cast<double2*>(PMo + (int64_t)m * N + a0) = make_double2(pm0, pm1);
+      scan_step(s0, pm0, m, ring0, RS, W, J, N, a0, R, M, NR);
+      scan_step(s1, pm1, m, ring1, RS, W, J, N, a0 + 1, R, M, NR);
+    }
+  };
+  // three register buffers: months m+1 and m+2 stay in flight while month m is reduced
+  double2 A[MAXD], B[MAXD], C[MAXD];
+  load_month(A, 0);
+  load_month(B, 1);
+  for (int m = 0; m < T_m; m += 3) {
+    load_month(C, m + 2);
+    process(A, m);
+    load_month(A, m + 3);
+    if (m + 1 < T_m) process(B, m + 1);
+    load_month(B, m + 4);
+    if (m + 2 < T_m) process(C, m + 2);
   }
-  if (carry_out) {
-    int idx = head;
-    for (int k = 0; k < W; ++k) {  // carry rows hold the ring's factors fl(1+ret), oldest first
-      carry_out[(int64_t)k * N + a] = ring[idx * RS];
-      idx = (idx + 1 == W) ? 0 : idx + 1;
-    }
-    carry_out[(int64_t)W * N + a] = pff;
-    carry_out[(int64_t)(W + 1) * N + a] = psff;
+  if (live) {
+    scan_finish(s0, ring0, RS, W, N, a0, NR, next_pm, carry_out);
+    scan_finish(s1, ring1, RS, W, N, a0 + 1, NR, next_pm, carry_out);
   }
 }
 
@@ -295,23 +400,47 @@ struct DecShared {
   int64_t red_n[DEC_THREADS / 64];
 };
 
+// Monotone non-decreasing in x for any lo / scale (values outside [lo, lo + HB/scale)
+// clamp into the end buckets), so bucket order never contradicts value order.
 __device__ __forceinline__ int vbucket(double x, double lo, double scale) {
   if (scale == 0.0) return 0;
   const double f = (x - lo) * scale;
-  const int b = (int)f;
-  return b < HB ? b : HB - 1;
+  if (!(f > 0.0)) return 0;
+  if (f >= (double)HB) return HB - 1;
+  return (int)f;
 }
 
+// Row sweep with ROW_U independent 16-B (or 8-B) loads issued per lane before use, so a
+// 512-thread block keeps ROW_U KiB x 8 waves in flight.
+#define ROW_U 8
 template <bool V2, typename F>
 __device__ __forceinline__ void for_row(const double* __restrict__ row, int64_t N, F&& f) {
   if (V2) {
-    for (int64_t i = 2 * (int64_t)threadIdx.x; i < N; i += 2 * DEC_THREADS) {
+    const int64_t step = 2 * DEC_THREADS;
+    int64_t i = 2 * (int64_t)threadIdx.x;
+    for (; i + (ROW_U - 1) * step < N; i += ROW_U * step) {
+      double2 v[ROW_U];
+#pragma unroll
+      for (int u = 0; u < ROW_U; ++u) v[u] = *reinterpret_cast<const double2*>(row + i + u * step);
+#pragma unroll
+      for (int u = 0; u < ROW_U; ++u) { f(i + u * step, v[u].x); f(i + u * step + 1, v[u].y); }
+    }
+    for (; i < N; i += step) {
       const double2 t = *reinterpret_cast<const double2*>(row + i);
       f(i, t.x);
       f(i + 1, t.y);
     }
   } else {
-    for (int64_t i = threadIdx.x; i < N; i += DEC_THREADS) f(i, row[i]);
+    const int64_t step = DEC_THREADS;
+    int64_t i = threadIdx.x;
+    for (; i + (ROW_U - 1) * step < N; i += ROW_U * step) {
+      double v[ROW_U];
+#pragma unroll
+      for (int u = 0; u < ROW_U; ++u) v[u] = row[i + u * step];
+#pragma unroll
+      for (int u = 0; u < ROW_U; ++u) f(i + u * step, v[u]);
+    }
+    for (; i < N; i += step) f(i, row[i]);
   }
 }
 
@@ -350,7 +479,7 @@ __device__ __forceinline__ bool slot_member(const Slot& s, int b, uint64_t k) {
 }
 
 template <int NB, bool V2>
-__global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restrict__ Mx,
+__global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __restrict__ Mx,
                                                          const double* __restrict__ NRx,
                                                          int64_t N, int n_bins, QTab qt,
                                                          int8_t* __restrict__ L,
@@ -365,12 +494,66 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
   const double* nrow = NRx ? NRx + (int64_t)t * N : nullptr;
   int8_t* lrow = L + (int64_t)t * N;
 
-  // ---------------- pass 1: count / min / max
+  // ---------------- pass 0: robust bucketing range from a coalesced sample.
+  // The histogram below is monotone for ANY [lo, hi] (values outside clamp into the end
+  // buckets), so lo/hi need not be the exact extremes: a 0.2 %..99.8 % range of a sample
+  // keeps heavy momentum tails from squeezing the bulk into a few buckets.  The exact
+  // count / min / max come out of the histogram pass itself.
+  {
+    if (tid == 0) S.total = 0;
+    __syncthreads();
+    constexpr int SCH = 32;  // 32 chunks x 64 consecutive assets
+    const int64_t chunk = 64;
+    for (int c = tid >> 6; c < SCH; c += DEC_THREADS / 64) {
+      const int64_t start = (N <= SCH * chunk) ? (int64_t)c * chunk
+                                               : ((int64_t)c * (N - chunk)) / (SCH - 1);
+      const int64_t i = start + (tid & 63);
+      if (i < N) {
+        const double x = row[i];
+        if (!isnan_d(x)) S.cand[atomicAdd(&S.total, 1)] = x;
+      }
+    }
+    __syncthreads();
+    const int ns = S.total;
+    int P2 = 1;
+    while (P2 < ns) P2 <<= 1;
+    for (int i = ns + tid; i < P2; i += DEC_THREADS) S.cand[i] = INFINITY;
+    __syncthreads();
+    for (int k = 2; k <= P2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < P2; i += DEC_THREADS) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const double x = S.cand[i], y = S.cand[ixj];
+            if ((x > y) == ((i & k) == 0)) { S.cand[i] = y; S.cand[ixj] = x; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (tid == 0) {
+      double lo = 0.0, hi = 0.0;
+      if (ns >= 2) {
+        lo = S.cand[(ns * 2) / 1000];
+        hi = S.cand[ns - 1 - (ns * 2) / 1000];
+      }
+      const double rng = hi - lo;
+      S.vmin = lo;
+      S.scale = (rng > 0.0 && rng <= 1.0e300) ? (double)HB / rng : 0.0;
+    }
+    for (int b2 = tid; b2 < HB; b2 += DEC_THREADS) S.hist[b2] = 0;
+    __syncthreads();
+  }
+  // ---------------- pass 1: value-bucket histogram + exact count / min / max
+  const double blo = S.vmin, bscale = S.scale;
   {
     int64_t cnt = 0;
     double lo = INFINITY, hi = -INFINITY;
     for_row<V2>(row, N, [&](int64_t, double x) {
-      if (!isnan_d(x)) { ++cnt; lo = fmin(lo, x); hi = fmax(hi, x); }
+      if (!isnan_d(x)) {
+        ++cnt; lo = fmin(lo, x); hi = fmax(hi, x);
+        atomicAdd(&S.hist[vbucket(x, blo, bscale)], 1u);
+      }
     });
     for (int o = 32; o > 0; o >>= 1) {
       cnt += __shfl_down(cnt, o, 64);
@@ -383,8 +566,6 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
       int64_t c = 0; double l = INFINITY, h = -INFINITY;
       for (int w = 0; w < DEC_THREADS / 64; ++w) { c += S.red_n[w]; l = fmin(l, S.red_d[w][0]); h = fmax(h, S.red_d[w][1]); }
       S.n = c; S.vmin = l; S.vmax = h;
-      const double rng = h - l;
-      S.scale = (c > 0 && rng > 0.0 && rng <= 1.0e300) ? (double)HB / rng : 0.0;
     }
     __syncthreads();
   }
@@ -393,19 +574,16 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
   const bool degenerate = (n == 0) || !(S.vmin < S.vmax);
 
   if (!degenerate) {
-    // ---------------- target ranks
+    // ---------------- target ranks (interior order statistics; min / max are known)
     if (tid == 0) {
       int nt = 0;
       for (int k = 0; k <= n_bins; ++k) {
         const double v = (double)(n - 1) * qt.q[k];
-        if (v >= (double)(n - 1)) {
-          S.trank[nt++] = n - 1;
-          continue;
-        }
+        if (v >= (double)(n - 1)) continue;  // edge = max
         const double p = floor(v);
         const int64_t pi = (int64_t)p;
-        S.trank[nt++] = pi;
-        if (v - p != 0.0) S.trank[nt++] = pi + 1;
+        if (pi > 0) S.trank[nt++] = pi;
+        if (v - p != 0.0 && pi + 1 < n - 1) S.trank[nt++] = pi + 1;
       }
       // sort + dedupe (tiny)
       for (int i = 1; i < nt; ++i) {
@@ -416,15 +594,6 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
       int u = 0;
       for (int i = 0; i < nt; ++i) if (u == 0 || S.trank[u - 1] != S.trank[i]) S.trank[u++] = S.trank[i];
       S.ntgt = u;
-    }
-    for (int b = tid; b < HB; b += DEC_THREADS) S.hist[b] = 0;
-    __syncthreads();
-    // ---------------- pass 2: value-bucket histogram
-    {
-      const double lo = S.vmin, sc = S.scale;
-      for_row<V2>(row, N, [&](int64_t, double x) {
-        if (!isnan_d(x)) atomicAdd(&S.hist[vbucket(x, lo, sc)], 1u);
-      });
     }
     __syncthreads();
     // counts are needed after the scan: keep a copy of target-bucket counts via prefix diff
@@ -472,7 +641,7 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
       }
       __syncthreads();
       const Slot sl = S.slots[rs];
-      const double lo = S.vmin, sc = S.scale;
+      const double lo = blo, sc = bscale;
       // key min / max of the members
       unsigned long long kl = ~0ULL, kh = 0ULL;
       for_row<V2>(row, N, [&](int64_t, double x) {
@@ -570,7 +739,7 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
       for (int i = S.nslot - 1; i >= 0; --i) S.hist[S.slots[i].b0] = (uint32_t)i;
     __syncthreads();
     {
-      const double lo = S.vmin, sc = S.scale;
+      const double lo = blo, sc = bscale;
       const int nsl = S.nslot;
       for_row<V2>(row, N, [&](int64_t, double x) {
         if (isnan_d(x)) return;
@@ -620,6 +789,8 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
     // ---------------- edges (NumPy _lerp) and duplicates='drop'
     if (tid == 0) {
       auto order_stat = [&](int64_t r) -> double {
+        if (r <= 0) return S.vmin;
+        if (r >= n - 1) return S.vmax;
         int lo2 = 0, hi2 = S.ntgt - 1;
         while (lo2 < hi2) { const int mid = (lo2 + hi2) >> 1; if (S.trank[mid] < r) lo2 = mid + 1; else hi2 = mid; }
         return S.tval[lo2];
@@ -655,9 +826,7 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
 
   // ---------------- pass 4: labels + equal-weight accumulation (double-double per label)
   const int nb = S.nbins;
-  double bins[MAXQ];
-#pragma unroll
-  for (int j = 0; j < MAXQ; ++j) bins[j] = (j < nb) ? S.bins[j] : 0.0;
+  const double* bins = S.bins;  // LDS, every lane reads the same word: broadcast
   constexpr int NBA = NB > 0 ? NB : 1;
   double hs[NBA], ls[NBA];
   int cn[NBA];
@@ -666,8 +835,7 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
   auto label_of = [&](double x) -> int {
     if (nb == 0 || isnan_d(x)) return -1;
     int ids = 0;
-#pragma unroll
-    for (int j = 0; j < MAXQ; ++j) ids += (j < nb && bins[j] < x) ? 1 : 0;
+    for (int j = 0; j < nb; ++j) ids += (bins[j] < x) ? 1 : 0;
     if (x == bins[0]) ids = 1;
     return (ids == 0 || ids == nb) ? -1 : ids - 1;
   };
@@ -685,7 +853,26 @@ __global__ __launch_bounds__(DEC_THREADS) void k_deciles(const double* __restric
     }
   };
   if (V2) {
-    for (int64_t i = 2 * (int64_t)tid; i < N; i += 2 * DEC_THREADS) {
+    const int64_t step = 2 * DEC_THREADS;
+    int64_t i = 2 * (int64_t)tid;
+    constexpr int LU = 4;
+    for (; i + (LU - 1) * step < N; i += LU * step) {
+      double2 x[LU], r[LU];
+#pragma unroll
+      for (int u = 0; u < LU; ++u) x[u] = *reinterpret_cast<const double2*>(row + i + u * step);
+      if (NB > 0 && nrow) {
+#pragma unroll
+        for (int u = 0; u < LU; ++u) r[u] = *reinterpret_cast<const double2*>(nrow + i + u * step);
+      }
+#pragma unroll
+      for (int u = 0; u < LU; ++u) {
+        const int l0 = label_of(x[u].x), l1 = label_of(x[u].y);
+        char2 lv; lv.x = (char)l0; lv.y = (char)l1;
+        *reinterpret_cast<char2*>(lrow + i + u * step) = lv;
+        if (NB > 0 && nrow) { accumulate(l0, r[u].x); accumulate(l1, r[u].y); }
+      }
+    }
+    for (; i < N; i += step) {
       const double2 x = *reinterpret_cast<const double2*>(row + i);
       const int l0 = label_of(x.x), l1 = label_of(x.y);
       char2 lv; lv.x = (char)l0; lv.y = (char)l1;
@@ -999,6 +1186,43 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
   hipLaunchKernelGGL(k_momentum, dim3(blocks), dim3(tpb), lds, ctx->stream, PM, T_m, N, J,
                      skip, R, M, NR, carry, next_pm, carry_out);
   LAUNCH_CHECK(ctx, "k_momentum");
+  return CSM_OK;
+}
+
+int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
+               int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
+               double* M, double* NR, const double* carry, const double* next_pm,
+               double* carry_out) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !M || !NR || N <= 0 || T_d < 0 || T_m < 0 || J < 1 || skip < 0 ||
+      J + skip > 256 || max_month_days < 1)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal: bad arguments (N=%lld T_m=%d J=%d skip=%d)",
+                   (long long)N, T_m, J, skip);
+  if (N % 2 != 0 || !aligned16(P) || (PM && !aligned16(PM)))
+    return set_err(ctx, CSM_E_INVAL, "csm_signal: needs even N and 16-byte aligned P/PM "
+                   "(use csm_month_end + csm_momentum otherwise)");
+  if (max_month_days > 32)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal: months longer than 32 days are not supported "
+                   "(use csm_month_end + csm_momentum)");
+  if (T_m == 0) return CSM_OK;
+  const int W = J + skip;
+  const size_t lds = (size_t)W * 128 * sizeof(double);
+  const unsigned blocks = (unsigned)((N / 2 + 63) / 64);
+  if (max_month_days <= 24) {
+    if (lds > 65536)
+      HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_signal<24>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_signal<24>, dim3(blocks), dim3(64), lds, ctx->stream, P, month_start,
+                       T_m, N, J, skip, PM, R, M, NR, carry, next_pm, carry_out);
+  } else {
+    if (lds > 65536)
+      HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_signal<32>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_signal<32>, dim3(blocks), dim3(64), lds, ctx->stream, P, month_start,
+                       T_m, N, J, skip, PM, R, M, NR, carry, next_pm, carry_out);
+  }
+  LAUNCH_CHECK(ctx, "k_signal");
   return CSM_OK;
 }
 

@@ -20,6 +20,7 @@ import torch
 from ._lib import ABSENT_BITS, check, load_library
 
 QTABLE_CACHE: dict[int, np.ndarray] = {}
+FUSED_MIN_N = 32768  # below this the fused kernel has too few waves to fill 256 CUs
 
 
 def quantile_table(n_bins: int) -> np.ndarray:
@@ -144,6 +145,30 @@ class Engine:
                    _ptr(NR), _ptr(carry), _ptr(next_pm), _ptr(carry_out))
         return R, M, NR
 
+    def signal(self, P, month_start, max_month_days, J=12, skip=1, with_pm=False,
+               with_ret=False, carry=None, next_pm=None, carry_out=None, out=None):
+        """Fused month-end + scan (csm_signal): one pass over the daily panel, no PM round
+        trip.  Needs even N and months of <= 32 days."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        W = J + skip
+        for t, nm, shp in ((carry, "carry", (W + 2, N)), (next_pm, "next_pm", (N,)),
+                           (carry_out, "carry_out", (W + 2, N))):
+            if t is not None:
+                _need(t, nm, torch.float64, shp, self.device)
+        if out is None:
+            PM = self.empty((T_m, N)) if with_pm else None
+            R = self.empty((T_m, N)) if with_ret else None
+            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
+        else:
+            PM, R, M, NR = out
+        self._call("csm_signal", _ptr(P), T_d, N, _ptr(month_start), T_m, int(max_month_days),
+                   int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR), _ptr(carry),
+                   _ptr(next_pm), _ptr(carry_out))
+        return PM, R, M, NR
+
     def deciles(self, M, NR=None, n_bins=10, out=None, with_nv=False):
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)
@@ -193,10 +218,27 @@ class Engine:
         self._call("csm_sync")
 
     # ------------------------------------------------------------------ pipeline
-    def run(self, P, month_start, J=12, skip=1, n_bins=10, V=None, with_ret=False):
-        """One full pass: month-end -> signal -> labels + EW decile means -> long-short."""
-        PM, VOL = self.month_end(P, month_start, V)
-        R, M, NR = self.momentum(PM, J, skip, with_ret=with_ret)
+    def use_fused(self, P, V=None, max_month_days=None) -> bool:
+        T_d, N = P.shape
+        return (V is None and N % 2 == 0 and N >= FUSED_MIN_N and P.data_ptr() % 16 == 0
+                and max_month_days is not None and max_month_days <= 32)
+
+    def run(self, P, month_start, J=12, skip=1, n_bins=10, V=None, with_ret=False,
+            max_month_days=None, fused=None):
+        """One full pass: month-end -> signal -> labels + EW decile means -> long-short.
+        Large panels take the fused month-end + scan kernel (no PM round trip)."""
+        T_m, N = month_start.numel() - 1, P.shape[1]
+        if max_month_days is None and T_m > 0:
+            max_month_days = int((month_start[1:] - month_start[:-1]).max().item())
+        if fused is None:
+            fused = self.use_fused(P, V, max_month_days)
+        if fused:
+            PM, R, M, NR = self.signal(P, month_start, max_month_days, J, skip, with_pm=True,
+                                       with_ret=with_ret)
+            VOL = None
+        else:
+            PM, VOL = self.month_end(P, month_start, V)
+            R, M, NR = self.momentum(PM, J, skip, with_ret=with_ret)
         L, EW, CNT, NV = self.deciles(M, NR, n_bins, with_nv=True)
         LS = self.long_short(EW, CNT)
         return PipelineOut(PM=PM, M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS, R=R, VOL=VOL, NV=NV)

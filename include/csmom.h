@@ -78,6 +78,17 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
                  const double* next_pm, double* carry_out);
 
 /*
+ * Fused month-end aggregation + scan in one pass over the daily panel (csm_month_end then
+ * csm_momentum without the PM round trip).  Same outputs and carry contract as
+ * csm_momentum; PM and R nullable; no volume.  Needs even N, 16-B aligned P, and
+ * max_month_days (HOST value: the longest month in days) <= 32.
+ */
+int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
+               int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, double* PM,
+               double* R, double* M, double* NR, const double* carry, const double* next_pm,
+               double* carry_out);
+
+/*
  * Per-date qcut labels, fused with the equal-weight decile means.  Replaces
  * run_demo.py:18-29 (assign_deciles_per_date via pd.qcut(duplicates='drop')),
  * run_demo.py:46 (groupby('date').transform) and run_demo.py:49-55 (dropna +

@@ -162,3 +162,55 @@ def test_odd_n_scalar_path(engine):
         assert bits_equal(getattr(out, k).cpu().numpy(), ref[k]), k
     assert np.array_equal(out.L.cpu().numpy(), ref["L"])
     assert max_rel(out.LS.cpu().numpy(), ref["LS"]) <= REL
+
+
+@pytest.mark.parametrize("name", ["edge", "longwin", "c1"])
+def test_fused_signal_matches_fixtures(engine, name):
+    """k_signal (fused month-end + scan) against the reference fixtures, with and without
+    the unfused two-kernel path."""
+    z = load_golden(name)
+    P = _up(z["P"])
+    ms_h = z["month_start"].astype(np.int64)
+    ms = _up(ms_h)
+    maxd = int(np.diff(ms_h).max())
+    for tag in golden_tags(z):
+        J, s = parse_tag(tag)
+        out = engine.run(P, ms, J, s, 10, with_ret=True, max_month_days=maxd, fused=True)
+        ref = engine.run(P, ms, J, s, 10, with_ret=True, max_month_days=maxd, fused=False)
+        for k in ("PM", "R", "M", "NR", "EW", "LS"):
+            assert bits_equal(getattr(out, k).cpu().numpy(), getattr(ref, k).cpu().numpy()), (tag, k)
+        assert torch.equal(out.L, ref.L) and torch.equal(out.CNT, ref.CNT) and torch.equal(out.NV, ref.NV)
+        assert np.array_equal(out.L.cpu().numpy(), z[f"{tag}_L"]), tag
+        if "PM" in z.files:
+            assert bits_equal(out.M.cpu().numpy(), z[f"{tag}_M"]), tag
+            assert bits_equal(out.NR.cpu().numpy(), z[f"{tag}_NR"]), tag
+
+
+def test_fused_signal_large_panel_vs_oracle(engine):
+    """C2-sized daily panel (5,000 x 6,522 business days): fused path vs the oracle at full
+    size -- bit-exact mom/next_ret/labels, EW/LS within 1e-10."""
+    from oracle.synth_np import make_panel
+    pan = make_panel(5000, 6522, seed=2, start="2000-01-03", with_volume=False)
+    ms_h = pan["month_start"]
+    P = _up(pan["P"])
+    out = engine.run(P, _up(ms_h), 12, 1, 10, max_month_days=int(np.diff(ms_h).max()), fused=True)
+    ref = O.pipeline(pan["P"], ms_h, 12, 1, 10)
+    assert bits_equal(out.PM.cpu().numpy(), ref["PM"])
+    assert bits_equal(out.M.cpu().numpy(), ref["M"])
+    assert bits_equal(out.NR.cpu().numpy(), ref["NR"])
+    assert np.array_equal(out.L.cpu().numpy(), ref["L"])
+    assert np.array_equal(out.CNT.cpu().numpy(), ref["CNT"])
+    assert max_rel(out.EW.cpu().numpy(), ref["EW"]) <= REL
+    assert max_rel(out.LS.cpu().numpy(), ref["LS"]) <= REL
+
+
+def test_fused_rejects_bad_layouts(engine):
+    import csmom
+    P = torch.zeros((10, 7), dtype=torch.float64, device="cuda:0")
+    ms = torch.tensor([0, 5, 10], dtype=torch.int64, device="cuda:0")
+    with pytest.raises(csmom.CsmError):
+        engine.signal(P, ms, 5)          # odd N
+    P2 = torch.zeros((40, 8), dtype=torch.float64, device="cuda:0")
+    ms2 = torch.tensor([0, 40], dtype=torch.int64, device="cuda:0")
+    with pytest.raises(csmom.CsmError):
+        engine.signal(P2, ms2, 40)       # month longer than 32 days

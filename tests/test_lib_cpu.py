@@ -11,12 +11,13 @@ ROOT = Path(__file__).resolve().parents[1]
 
 def header_symbols():
     txt = (ROOT / "include" / "csmom.h").read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(csm_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(csm_\w+)\(", txt, re.M)))
 
 
 def test_header_declares_expected_api():
     syms = header_symbols()
-    for s in ("csm_create", "csm_month_end", "csm_momentum", "csm_deciles", "csm_long_short",
+    for s in ("csm_create", "csm_month_end", "csm_momentum", "csm_signal", "csm_deciles",
+              "csm_long_short",
               "csm_shard_summary", "csm_fold_carry", "csm_last_error"):
         assert s in syms
 
@@ -35,6 +36,8 @@ def test_null_context_is_inval():
     lib = csmom.load_library()
     assert lib.csm_month_end(None, None, None, 0, 0, None, 0, None, None) == -1
     assert lib.csm_momentum(None, None, 0, 0, 12, 1, None, None, None, None, None, None) == -1
+    assert lib.csm_signal(None, None, 0, 0, None, 0, 23, 12, 1, None, None, None, None, None,
+                          None, None) == -1
     assert lib.csm_deciles(None, None, None, 0, 0, 10, None, None, None, None, None) == -1
     assert lib.csm_sync(None) == -1
     assert lib.csm_last_error(None) == b"null context"
