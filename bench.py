@@ -106,8 +106,14 @@ def main():
     L = eng.empty((T_m, N), torch.int8)
     EW, CNT = eng.empty((T_m, nb)), eng.empty((T_m, nb), torch.int32)
     LS = eng.empty((T_m,))
+    chunks = 1 if fused else eng.default_chunks(T_m, N, J, skip)
+    ws = None
+    if chunks > 1:
+        nbytes = int(eng.lib.csm_momentum_chunked_workspace(T_m, N, J, skip, chunks))
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    scan_name = f"scan(k_momentum_chunked x{chunks})" if chunks > 1 else "scan(k_momentum)"
     stage_names = (["signal(k_signal)", "deciles(k_deciles)", "long_short"] if fused else
-                   ["month_end(k_month_end)", "scan(k_momentum)", "deciles(k_deciles)", "long_short"])
+                   ["month_end(k_month_end)", scan_name, "deciles(k_deciles)", "long_short"])
     nst = len(stage_names) + 1
     step_events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst)]
                    for _ in range(args.steps)]
@@ -125,7 +131,10 @@ def main():
             eng.month_end(panel.P, panel.month_start, PM=PM)
             i += 1
             ev[i].record()
-            eng.momentum(PM, J, skip, out=(None, M, NR))
+            if chunks > 1:
+                eng.momentum_chunked(PM, J, skip, chunks=chunks, out=(None, M, NR), workspace=ws)
+            else:
+                eng.momentum(PM, J, skip, out=(None, M, NR))
         i += 1
         ev[i].record()
         eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
@@ -228,6 +237,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic seeded GBM panel generated in HBM (late listings, delistings, "
                     "NaN days, absent and all-NaN months)",
+            "engine_path": ("fused k_signal" if fused else
+                            f"k_month_end + scan ({chunks} month chunks)"),
             "config": {"workload": cfg["name"] if args.assets is None and args.days is None
                        else f"custom: {N} assets x {T_d} bdays per GPU",
                        "assets": N, "bdays_per_gpu": T_d, "months_per_gpu": T_m, "J": J,

@@ -20,7 +20,8 @@ ABSENT_BITS = 0x7FF4000000000001
 EXPORTS = (
     "csm_abi_version", "csm_create", "csm_destroy", "csm_last_error", "csm_set_stream",
     "csm_sync", "csm_month_end", "csm_momentum", "csm_deciles", "csm_long_short",
-    "csm_shard_summary", "csm_fold_carry", "csm_signal",
+    "csm_shard_summary", "csm_fold_carry", "csm_signal", "csm_momentum_chunked",
+    "csm_momentum_chunked_workspace", "csm_tune",
 )
 
 
@@ -48,6 +49,7 @@ _i64 = ctypes.c_int64
 def _declare(lib):
     sig = {
         "csm_abi_version": (ctypes.c_int, []),
+        "csm_tune": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
         "csm_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
         "csm_destroy": (ctypes.c_int, [_p]),
         "csm_last_error": (ctypes.c_char_p, [_p]),
@@ -57,6 +59,9 @@ def _declare(lib):
         "csm_momentum": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p]),
         "csm_signal": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
                                       _p, _p, _p]),
+        "csm_momentum_chunked": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _i32, _p, _p, _p,
+                                                _p, _p]),
+        "csm_momentum_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),
         "csm_deciles": (ctypes.c_int, [_p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
         "csm_long_short": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p]),
         "csm_shard_summary": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p]),

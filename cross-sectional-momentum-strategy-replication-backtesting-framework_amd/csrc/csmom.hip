@@ -229,6 +229,14 @@ __device__ __forceinline__ void scan_finish(ScanLane& s, double* ring, int RS, i
   }
 }
 
+// Month range of chunk g when T_m months are split into G contiguous chunks (earlier
+// chunks take the remainder) -- the same split as distributed.month_partition.
+__device__ __forceinline__ void chunk_range(int T_m, int G, int g, int& m0, int& m1) {
+  const int base = T_m / G, rem = T_m % G;
+  m0 = g * base + (g < rem ? g : rem);
+  m1 = m0 + base + (g < rem ? 1 : 0);
+}
+
 // =====================================================================================
 // Kernel B: per-asset scan over month prices (present rows only).  One thread per asset;
 // PM rows prefetched SCAN_CHUNK months ahead (SCAN_CHUNK * 512 B in flight per wave).
@@ -236,11 +244,42 @@ __device__ __forceinline__ void scan_finish(ScanLane& s, double* ring, int RS, i
 #define SCAN_THREADS 128
 #define SCAN_CHUNK 16
 
+__device__ __forceinline__ void momentum_body(
+    double* ring_lds, const double* __restrict__ PM, int T_m, int64_t N, int J, int skip,
+    double* __restrict__ R, double* __restrict__ M, double* __restrict__ NR,
+    const double* __restrict__ carry, const double* __restrict__ next_pm,
+    double* __restrict__ carry_out);
+
 __global__ __launch_bounds__(256) void k_momentum(
     const double* __restrict__ PM, int T_m, int64_t N, int J, int skip, double* __restrict__ R,
     double* __restrict__ M, double* __restrict__ NR, const double* __restrict__ carry,
     const double* __restrict__ next_pm, double* __restrict__ carry_out) {
   extern __shared__ __attribute__((aligned(16))) double ring_lds[];
+  momentum_body(ring_lds, PM, T_m, N, J, skip, R, M, NR, carry, next_pm, carry_out);
+}
+
+// Time-chunked scan (small N): chunk blockIdx.y scans its month range from the carry that
+// k_fold_carry rebuilt for it -- C x more waves in flight, same results bit for bit.
+__global__ __launch_bounds__(256) void k_momentum_chunked(
+    const double* __restrict__ PM, int T_m, int G, int64_t N, int J, int skip,
+    double* __restrict__ R, double* __restrict__ M, double* __restrict__ NR,
+    const double* __restrict__ carry, const double* __restrict__ next_pm) {
+  extern __shared__ __attribute__((aligned(16))) double ring_lds[];
+  const int g = blockIdx.y;
+  int m0, m1;
+  chunk_range(T_m, G, g, m0, m1);
+  const int W = J + skip;
+  const int64_t off = (int64_t)m0 * N;
+  momentum_body(ring_lds, PM + off, m1 - m0, N, J, skip, R ? R + off : nullptr, M + off,
+                NR + off, g > 0 ? carry + (int64_t)g * (W + 2) * N : nullptr,
+                next_pm + (int64_t)g * N, nullptr);
+}
+
+__device__ __forceinline__ void momentum_body(
+    double* ring_lds, const double* __restrict__ PM, int T_m, int64_t N, int J, int skip,
+    double* __restrict__ R, double* __restrict__ M, double* __restrict__ NR,
+    const double* __restrict__ carry, const double* __restrict__ next_pm,
+    double* __restrict__ carry_out) {
   const int W = J + skip;
   const int tid = threadIdx.x;
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + tid;
@@ -268,74 +307,107 @@ __global__ __launch_bounds__(256) void k_momentum(
 // =====================================================================================
 // Kernel AB (fused): month-end aggregation + scan in one stream over the daily panel, for
 // large N.  One wave per block, two assets per lane (16-B row loads, 1 KiB per wave-
-// instruction).  While month m is reduced and scanned, all MAXD day rows of month m+1 are
-// already in flight (register double buffer).  Months shorter than MAXD re-load their last
+// instruction).  While month m is reduced and scanned, the MAXD day rows of months m+1..m+3
+// are already in flight (four register buffers).  Months shorter than MAXD re-load their last
 // row into the spare slots: those loads hit L1/L2 (no extra HBM bytes), keep the load count
 // fixed so vmcnt waits stay counted, and do not change "last non-NaN" / "any present".
 // The month prices never round-trip through HBM unless PM is requested.
 // =====================================================================================
-template <int MAXD>
+// VEC assets per lane (VEC = 2: 16-B row loads, 1 KiB per wave-instruction; VEC = 1: twice
+// the waves, 8-B loads), NBUF month buffers (NBUF - 1 months in flight).
+template <int VEC> struct RowT;
+template <> struct RowT<1> { typedef double T; };
+template <> struct RowT<2> { typedef double2 T; };
+__device__ __forceinline__ double comp(double v, int) { return v; }
+__device__ __forceinline__ double comp(double2 v, int k) { return k == 0 ? v.x : v.y; }
+
+template <int MAXD, int VEC, int NBUF>
 __global__ __launch_bounds__(64) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
     double* __restrict__ carry_out) {
-  extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][128]
+  typedef typename RowT<VEC>::T VT;
+  extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC]
   const int W = J + skip;
   const int tid = threadIdx.x;
-  const int64_t a0 = ((int64_t)blockIdx.x * 64 + tid) * 2;
+  const int64_t a0 = ((int64_t)blockIdx.x * 64 + tid) * VEC;
   const bool live = a0 < N;
-  double* ring0 = ring_lds + 2 * tid;
-  double* ring1 = ring0 + 1;
-  const int RS = 128;
-  ScanLane s0, s1;
-  scan_init(s0, ring0, RS, W, carry, N, a0, live);
-  scan_init(s1, ring1, RS, W, carry, N, a0 + 1, live);
+  const int RS = 64 * VEC;
+  ScanLane sl[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, carry, N, a0 + k, live);
   const double* base = P + (live ? a0 : 0);
   // Loads are issued unconditionally (months past the end re-load the last month: cache
   // hits) so every wait is a counted vmcnt; only the processing is guarded.
-  auto load_month = [&](double2 (&buf)[MAXD], int mm) {
+  auto load_month = [&](VT (&buf)[MAXD], int mm) {
     mm = mm < T_m ? mm : T_m - 1;
     const int64_t f0 = month_start[mm], nn = month_start[mm + 1] - f0;
 #pragma unroll
     for (int k = 0; k < MAXD; ++k)
-      buf[k] = *reinterpret_cast<const double2*>(base + (f0 + (k < nn ? k : nn - 1)) * N);
+      buf[k] = *reinterpret_cast<const VT*>(base + (f0 + (k < nn ? k : nn - 1)) * N);
   };
-  auto process = [&](const double2 (&X)[MAXD], int m) {
-    double last0 = 0.0, last1 = 0.0;
-    bool p0 = false, p1 = false, v0 = false, v1 = false;
+  auto process = [&](const VT (&X)[MAXD], int m) {
+    double pm[VEC];
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k) {
-      const double x0 = X[k].x, x1 = X[k].y;
-      const bool q0 = !is_absent(x0), q1 = !is_absent(x1);
-      const bool ok0 = q0 && !isnan_d(x0), ok1 = q1 && !isnan_d(x1);
-      p0 |= q0; p1 |= q1; v0 |= ok0; v1 |= ok1;
-      last0 = ok0 ? x0 : last0;
-      last1 = ok1 ? x1 : last1;
+    for (int c = 0; c < VEC; ++c) {
+      double last = 0.0;
+      bool p = false, v = false;
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k) {
+        const double x = comp(X[k], c);
+        const bool ok = x == x;  // a valid price (ABSENT and missing are NaN)
+        p |= !is_absent(x);
+        v |= ok;
+        last = ok ? x : last;
+      }
+      pm[c] = p ? (v ? last : qnan()) : absent_val();
     }
-    const double pm0 = p0 ? (v0 ? last0 : qnan()) : absent_val();
-    const double pm1 = p1 ? (v1 ? last1 : qnan()) : absent_val();
     if (live) {
-      if (PMo) *reinterpret_cast<double2*>(PMo + (int64_t)m * N + a0) = make_double2(pm0, pm1);
-      scan_step(s0, pm0, m, ring0, RS, W, J, N, a0, R, M, NR);
-      scan_step(s1, pm1, m, ring1, RS, W, J, N, a0 + 1, R, M, NR);
+      if (PMo) {
+        if (VEC == 2) *reinterpret_cast<double2*>(PMo + (int64_t)m * N + a0) = make_double2(pm[0], pm[VEC - 1]);
+        else PMo[(int64_t)m * N + a0] = pm[0];
+      }
+#pragma unroll
+      for (int c = 0; c < VEC; ++c)
+        scan_step(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
     }
   };
-  // three register buffers: months m+1 and m+2 stay in flight while month m is reduced
-  double2 A[MAXD], B[MAXD], C[MAXD];
-  load_month(A, 0);
-  load_month(B, 1);
-  for (int m = 0; m < T_m; m += 3) {
-    load_month(C, m + 2);
-    process(A, m);
-    load_month(A, m + 3);
-    if (m + 1 < T_m) process(B, m + 1);
-    load_month(B, m + 4);
-    if (m + 2 < T_m) process(C, m + 2);
+  VT A[MAXD], B[MAXD], C[MAXD];
+  if (NBUF == 3) {
+    // months m+1, m+2 in flight while month m is reduced
+    load_month(A, 0);
+    load_month(B, 1);
+    for (int m = 0; m < T_m; m += 3) {
+      load_month(C, m + 2);
+      process(A, m);
+      load_month(A, m + 3);
+      if (m + 1 < T_m) process(B, m + 1);
+      load_month(B, m + 4);
+      if (m + 2 < T_m) process(C, m + 2);
+    }
+  } else {
+    // months m+1..m+3 in flight (the whole-history-per-wave pattern needs ~3 months in
+    // flight to approach the row-stream rate, see scripts/mb)
+    VT D[MAXD];
+    load_month(A, 0);
+    load_month(B, 1);
+    load_month(C, 2);
+    for (int m = 0; m < T_m; m += 4) {
+      load_month(D, m + 3);
+      process(A, m);
+      load_month(A, m + 4);
+      if (m + 1 < T_m) process(B, m + 1);
+      load_month(B, m + 5);
+      if (m + 2 < T_m) process(C, m + 2);
+      load_month(C, m + 6);
+      if (m + 3 < T_m) process(D, m + 3);
+    }
   }
   if (live) {
-    scan_finish(s0, ring0, RS, W, N, a0, NR, next_pm, carry_out);
-    scan_finish(s1, ring1, RS, W, N, a0 + 1, NR, next_pm, carry_out);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k)
+      scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm, carry_out);
   }
 }
 
@@ -393,6 +465,8 @@ struct DecShared {
   int fill[MAXT];
   Slot slots2[MAXT];
   int remap[MAXT];
+  int vbe[MAXQ];          // bucket of each bin edge
+  int8_t blab[HB];        // bucket -> label (-1 NaN label, -2 bucket holds an edge: compare exactly)
   double e[MAXQ], u[MAXQ];
   // reduction scratch
   double red_d[DEC_THREADS / 64][2];
@@ -401,12 +475,10 @@ struct DecShared {
 };
 
 // Monotone non-decreasing in x for any lo / scale (values outside [lo, lo + HB/scale)
-// clamp into the end buckets), so bucket order never contradicts value order.
+// clamp into the end buckets), so bucket order never contradicts value order.  Branch-free:
+// fmax/fmin clamp (NaN -> bucket 0; callers never count NaN), truncation = floor on [0, HB).
 __device__ __forceinline__ int vbucket(double x, double lo, double scale) {
-  if (scale == 0.0) return 0;
-  const double f = (x - lo) * scale;
-  if (!(f > 0.0)) return 0;
-  if (f >= (double)HB) return HB - 1;
+  const double f = fmin(fmax((x - lo) * scale, 0.0), (double)(HB - 1));
   return (int)f;
 }
 
@@ -485,7 +557,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
                                                          int8_t* __restrict__ L,
                                                          double* __restrict__ EW,
                                                          int32_t* __restrict__ CNT,
-                                                         int32_t* __restrict__ NV) {
+                                                         int32_t* __restrict__ NV, int ablate) {
   __shared__ DecShared S;
   const int t = blockIdx.x;
   const int tid = threadIdx.x;
@@ -550,10 +622,11 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     int64_t cnt = 0;
     double lo = INFINITY, hi = -INFINITY;
     for_row<V2>(row, N, [&](int64_t, double x) {
-      if (!isnan_d(x)) {
-        ++cnt; lo = fmin(lo, x); hi = fmax(hi, x);
-        atomicAdd(&S.hist[vbucket(x, blo, bscale)], 1u);
-      }
+      const bool ok = x == x;
+      cnt += ok ? 1 : 0;
+      lo = fmin(lo, x);  // fmin / fmax ignore a NaN operand
+      hi = fmax(hi, x);
+      atomicAdd(&S.hist[vbucket(x, blo, bscale)], ok ? 1u : 0u);
     });
     for (int o = 32; o > 0; o >>= 1) {
       cnt += __shfl_down(cnt, o, 64);
@@ -630,8 +703,10 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     }
     __syncthreads();
 
-    // ---------------- (rare) key-space refinement of the largest slot until all fit
-    while (S.total > CAP) {
+    // ---------------- (rare) key-space refinement of the largest slot until all fit.
+    // Each refinement shrinks a slot's key range >= 4096x (<= 6 per target before it is a
+    // single key), so the bound below is never reached on consistent state.
+    for (int guard = 0; S.total > CAP && guard < 8 * MAXT; ++guard) {
       __shared__ int rs;
       if (tid == 0) {
         int best = -1;
@@ -698,7 +773,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
             int64_t r = S.tres[ti];
             int j = 0;
             int64_t acc = 0;
-            while (acc + (int64_t)S.hist[j] <= r) { acc += S.hist[j]; ++j; }
+            while (j < HB - 1 && acc + (int64_t)S.hist[j] <= r) { acc += S.hist[j]; ++j; }
             const uint64_t klo = kmin + ((uint64_t)j << shift);
             uint64_t khi = klo + (((uint64_t)1 << shift) - 1);
             if (khi > kmax || khi < klo) khi = kmax;
@@ -738,14 +813,13 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     if (tid == 0)
       for (int i = S.nslot - 1; i >= 0; --i) S.hist[S.slots[i].b0] = (uint32_t)i;
     __syncthreads();
-    {
+    if (!(ablate & 2)) {
       const double lo = blo, sc = bscale;
       const int nsl = S.nslot;
       for_row<V2>(row, N, [&](int64_t, double x) {
-        if (isnan_d(x)) return;
+        const uint32_t si = S.hist[vbucket(x, lo, sc)];
+        if (si == 0xFFFFFFFFu || !(x == x)) return;  // common case: not a target bucket
         const int b = vbucket(x, lo, sc);
-        uint32_t si = S.hist[b];
-        if (si == 0xFFFFFFFFu) return;
         const uint64_t k = dkey(x);
         for (int i = (int)si; i < nsl && S.slots[i].b0 == b; ++i) {
           const Slot& s = S.slots[i];
@@ -819,12 +893,30 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
       else { for (int j = 0; j < ne; ++j) S.bins[j] = e[j]; S.nbins = ne; }
     }
     __syncthreads();
+    // bucket -> label table: a bucket holding no edge has one label for all its values
+    // (vbucket is monotone: vb(e) < vb(x) implies e < x, vb(e) > vb(x) implies e > x)
+    if (tid < S.nbins) S.vbe[tid] = vbucket(S.bins[tid], blo, bscale);
+    __syncthreads();
+    {
+      const int nbe = S.nbins;
+      for (int b2 = tid; b2 < HB; b2 += DEC_THREADS) {
+        int c = 0;
+        bool amb = false;
+        for (int j = 0; j < nbe; ++j) { const int vb = S.vbe[j]; c += vb < b2 ? 1 : 0; amb |= vb == b2; }
+        S.blab[b2] = (int8_t)(amb ? -2 : ((c == 0 || c == nbe) ? -1 : c - 1));
+      }
+    }
+    __syncthreads();
   } else {
     if (tid == 0) S.nbins = 0;
     __syncthreads();
   }
 
-  // ---------------- pass 4: labels + equal-weight accumulation (double-double per label)
+  // ---------------- pass 4: labels + equal-weight accumulation
+  // Labels come from the bucket table; only values in a bucket that holds an edge are
+  // compared against the edges.  Per lane the next_ret sums are plain fp64 (a few dozen
+  // terms per label), then combined across lanes and waves with a fixed-order
+  // double-double tree (deterministic; |error| ~ 1e-16 * sum |r|).
   const int nb = S.nbins;
   const double* bins = S.bins;  // LDS, every lane reads the same word: broadcast
   constexpr int NBA = NB > 0 ? NB : 1;
@@ -833,26 +925,28 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
 #pragma unroll
   for (int d = 0; d < NBA; ++d) { hs[d] = 0.0; ls[d] = 0.0; cn[d] = 0; }
   auto label_of = [&](double x) -> int {
-    if (nb == 0 || isnan_d(x)) return -1;
+    int lab = (nb == 0) ? -1 : (int)S.blab[vbucket(x, blo, bscale)];
+    lab = (x == x) ? lab : -1;
+    if (lab != -2) return lab;
     int ids = 0;
     for (int j = 0; j < nb; ++j) ids += (bins[j] < x) ? 1 : 0;
     if (x == bins[0]) ids = 1;
     return (ids == 0 || ids == nb) ? -1 : ids - 1;
   };
   auto accumulate = [&](int lab, double r) {
-    if (NB > 0 && lab >= 0 && !isnan_d(r)) {
+    if (NB > 0 && !(ablate & 1)) {
+      const bool ok = lab >= 0 && !isnan_d(r);
 #pragma unroll
       for (int d = 0; d < NB; ++d) {
-        if (lab == d) {
-          const double s = hs[d] + r;
-          const double bb = s - hs[d];
-          const double err = (hs[d] - (s - bb)) + (r - bb);
-          hs[d] = s; ls[d] += err; cn[d] += 1;
-        }
+        const bool h = ok && lab == d;
+        hs[d] += h ? r : 0.0;
+        cn[d] += h ? 1 : 0;
       }
     }
   };
-  if (V2) {
+  if (ablate & 4) {
+    // profiling ablation: no label pass
+  } else if (V2) {
     const int64_t step = 2 * DEC_THREADS;
     int64_t i = 2 * (int64_t)tid;
     constexpr int LU = 4;
@@ -999,17 +1093,70 @@ __global__ __launch_bounds__(256) void k_shard_summary(const double* __restrict_
   out[5 * N + a] = first;
 }
 
+__global__ __launch_bounds__(256) void k_shard_summary_chunked(const double* __restrict__ PM,
+                                                               int T_m, int64_t N, int T, int G,
+                                                               double* __restrict__ out) {
+  const int g = blockIdx.y;
+  int m0, m1;
+  chunk_range(T_m, G, g, m0, m1);
+  const int S = SUM_SCALARS + T;
+  // reuse the single-shard body through pointer offsets (grid.x covers the assets)
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  const double* pm = PM + (int64_t)m0 * N;
+  double* o = out + (int64_t)g * S * N;
+  const int tm = m1 - m0;
+  int64_t n = 0, fv = -1, lvi = -1;
+  double lv = qnan(), first = absent_val();
+  for (int m = 0; m < tm; ++m) {
+    const double x = pm[(int64_t)m * N + a];
+    if (is_absent(x)) continue;
+    if (n == 0) first = x;
+    if (!isnan_d(x)) { if (fv < 0) fv = n; lvi = n; lv = x; }
+    ++n;
+  }
+  const int k = (int)(n < T ? n : T);
+  int got = 0;
+  double head = qnan();
+  for (int j = 0; j < T - k; ++j) o[(int64_t)(SUM_SCALARS + j) * N + a] = absent_val();
+  int m = tm - 1;
+  for (; m >= 0 && got < k; --m) {
+    const double x = pm[(int64_t)m * N + a];
+    if (is_absent(x)) continue;
+    o[(int64_t)(SUM_SCALARS + T - 1 - got) * N + a] = x;
+    ++got;
+  }
+  for (; m >= 0; --m) {
+    const double x = pm[(int64_t)m * N + a];
+    if (is_absent(x)) continue;
+    if (!isnan_d(x)) { head = x; break; }
+  }
+  o[0 * N + a] = (double)n;
+  o[1 * N + a] = (double)fv;
+  o[2 * N + a] = (double)lvi;
+  o[3 * N + a] = lv;
+  o[4 * N + a] = head;
+  o[5 * N + a] = first;
+}
+
 __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ sm, int G, int g,
                                                     int64_t N, int J, int skip,
                                                     double* __restrict__ carry,
-                                                    double* __restrict__ next_pm) {
+                                                    double* __restrict__ next_pm,
+                                                    const double* __restrict__ tail_pm) {
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= N) return;
   const int W = J + skip, T = W + 1, S = SUM_SCALARS + T;
+  if (g < 0) {  // batched over all chunks: chunk blockIdx.y, outputs stacked per chunk
+    g = blockIdx.y;
+    carry += (int64_t)g * (W + 2) * N;
+    next_pm += (int64_t)g * N;
+  }
   auto at = [&](int h, int r) -> double { return sm[((int64_t)h * S + r) * N + a]; };
   // next_pm: first present row after shard g
-  double npm = absent_val();
+  double npm = (tail_pm && g == G - 1) ? tail_pm[a] : absent_val();
   for (int h = g + 1; h < G; ++h) if (at(h, 0) > 0.0) { npm = at(h, 5); break; }
+  if (tail_pm && g < G - 1 && is_absent(npm)) npm = tail_pm[a];
   next_pm[a] = npm;
   const double NaN = qnan();
   // locate the oldest of the last T present rows of shards < g
@@ -1068,6 +1215,11 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 // =====================================================================================
 // C ABI
 // =====================================================================================
+// Process-wide tuning knobs (csm_tune): kernel variants for A/B measurement in one process.
+static int g_tune_signal_vec = 2;   // k_signal assets per lane: 1 or 2
+static int g_tune_signal_nbuf = 3;  // k_signal month buffers: 3 or 4
+static int g_tune_dec_ablate = 0;   // k_deciles pass ablation bitmask (profiling only: wrong results)
+
 struct csm_ctx {
   int device;
   hipStream_t stream;
@@ -1109,6 +1261,14 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 extern "C" {
 
 int csm_abi_version(void) { return CSM_ABI_VERSION; }
+
+int csm_tune(const char* key, int value) {
+  if (!key) return CSM_E_INVAL;
+  if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
+  if (!strcmp(key, "signal_nbuf") && (value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
+  if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
+  return CSM_E_INVAL;
+}
 
 int csm_create(int device, csm_ctx** out) {
   if (!out) return CSM_E_INVAL;
@@ -1199,28 +1359,31 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
       J + skip > 256 || max_month_days < 1)
     return set_err(ctx, CSM_E_INVAL, "csm_signal: bad arguments (N=%lld T_m=%d J=%d skip=%d)",
                    (long long)N, T_m, J, skip);
-  if (N % 2 != 0 || !aligned16(P) || (PM && !aligned16(PM)))
-    return set_err(ctx, CSM_E_INVAL, "csm_signal: needs even N and 16-byte aligned P/PM "
-                   "(use csm_month_end + csm_momentum otherwise)");
   if (max_month_days > 32)
     return set_err(ctx, CSM_E_INVAL, "csm_signal: months longer than 32 days are not supported "
                    "(use csm_month_end + csm_momentum)");
   if (T_m == 0) return CSM_OK;
   const int W = J + skip;
-  const size_t lds = (size_t)W * 128 * sizeof(double);
-  const unsigned blocks = (unsigned)((N / 2 + 63) / 64);
-  if (max_month_days <= 24) {
-    if (lds > 65536)
-      HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_signal<24>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_signal<24>, dim3(blocks), dim3(64), lds, ctx->stream, P, month_start,
-                       T_m, N, J, skip, PM, R, M, NR, carry, next_pm, carry_out);
-  } else {
-    if (lds > 65536)
-      HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_signal<32>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_signal<32>, dim3(blocks), dim3(64), lds, ctx->stream, P, month_start,
-                       T_m, N, J, skip, PM, R, M, NR, carry, next_pm, carry_out);
+  const bool can2 = (N % 2 == 0) && aligned16(P) && (!PM || aligned16(PM));
+  const int vec = (g_tune_signal_vec == 1 || !can2) ? 1 : 2;
+  const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : 4;
+  const size_t lds = (size_t)W * 64 * vec * sizeof(double);
+  const unsigned blocks = (unsigned)((N / vec + 63) / 64);
+  const void* fn = nullptr;
+#define SIG(MD, V, NB) (const void*)k_signal<MD, V, NB>
+  if (max_month_days <= 24)
+    fn = vec == 2 ? (nbuf == 3 ? SIG(24, 2, 3) : SIG(24, 2, 4)) : (nbuf == 3 ? SIG(24, 1, 3) : SIG(24, 1, 4));
+  else
+    fn = vec == 2 ? (nbuf == 3 ? SIG(32, 2, 3) : SIG(32, 2, 4)) : (nbuf == 3 ? SIG(32, 1, 3) : SIG(32, 1, 4));
+#undef SIG
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  {
+    int T_m_ = T_m, J_ = J, skip_ = skip;
+    int64_t N_ = N;
+    void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
+                    (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out};
+    HIP_CHECK(ctx, hipLaunchKernel(fn, dim3(blocks), dim3(64), args, lds, ctx->stream));
   }
   LAUNCH_CHECK(ctx, "k_signal");
   return CSM_OK;
@@ -1232,8 +1395,9 @@ template <int NB>
 static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                            int32_t* CNT, int32_t* NV) {
-  if (v2) hipLaunchKernelGGL((k_deciles<NB, true>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV);
-  else hipLaunchKernelGGL((k_deciles<NB, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV);
+  const int ab = g_tune_dec_ablate;
+  if (v2) hipLaunchKernelGGL((k_deciles<NB, true>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab);
+  else hipLaunchKernelGGL((k_deciles<NB, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab);
 }
 
 extern "C" {
@@ -1304,8 +1468,50 @@ int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, 
     return set_err(ctx, CSM_E_INVAL, "csm_fold_carry: bad arguments");
   const unsigned blocks = (unsigned)((N + 255) / 256);
   hipLaunchKernelGGL(k_fold_carry, dim3(blocks), dim3(256), 0, ctx->stream, summaries, G, g, N, J,
-                     skip, carry, next_pm);
+                     skip, carry, next_pm, (const double*)nullptr);
   LAUNCH_CHECK(ctx, "k_fold_carry");
+  return CSM_OK;
+}
+
+int64_t csm_momentum_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                                       int32_t C) {
+  if (N <= 0 || C < 1 || J < 1 || skip < 0) return 0;
+  const int64_t S = SUM_SCALARS + J + skip + 1, W = J + skip;
+  (void)T_m;
+  return (int64_t)C * (S + (W + 2) + 1) * N * (int64_t)sizeof(double);
+}
+
+int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                         int32_t skip, int32_t C, double* R, double* M, double* NR,
+                         const double* next_pm, void* workspace) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!PM || !M || !NR || !workspace || N <= 0 || T_m < 0 || J < 1 || skip < 0 ||
+      J + skip > 256 || C < 1 || C > 65535)
+    return set_err(ctx, CSM_E_INVAL, "csm_momentum_chunked: bad arguments (N=%lld T_m=%d C=%d)",
+                   (long long)N, T_m, C);
+  if (T_m == 0) return CSM_OK;
+  if (C > T_m) C = T_m;
+  const int W = J + skip, T = W + 1, S = SUM_SCALARS + T;
+  double* sm = (double*)workspace;
+  double* carry = sm + (int64_t)C * S * N;
+  double* npm = carry + (int64_t)C * (W + 2) * N;
+  const unsigned bx = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(k_shard_summary_chunked, dim3(bx, C), dim3(256), 0, ctx->stream, PM, T_m, N,
+                     T, C, sm);
+  LAUNCH_CHECK(ctx, "k_shard_summary_chunked");
+  hipLaunchKernelGGL(k_fold_carry, dim3(bx, C), dim3(256), 0, ctx->stream, (const double*)sm, C,
+                     -1, N, J, skip, carry, npm, next_pm);
+  LAUNCH_CHECK(ctx, "k_fold_carry");
+  const int tpb = W <= 64 ? SCAN_THREADS : 64;
+  const size_t lds = (size_t)W * tpb * sizeof(double);
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_momentum_chunked,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_momentum_chunked, dim3((unsigned)((N + tpb - 1) / tpb), C), dim3(tpb), lds,
+                     ctx->stream, PM, T_m, C, N, J, skip, R, M, NR, (const double*)carry,
+                     (const double*)npm);
+  LAUNCH_CHECK(ctx, "k_momentum_chunked");
   return CSM_OK;
 }
 

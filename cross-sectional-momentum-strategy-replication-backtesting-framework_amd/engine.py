@@ -145,6 +145,35 @@ class Engine:
                    _ptr(NR), _ptr(carry), _ptr(next_pm), _ptr(carry_out))
         return R, M, NR
 
+    @staticmethod
+    def default_chunks(T_m, N, J=12, skip=1):
+        """Chunks for the time-chunked scan: enough (chunk, asset) lanes to fill the chip
+        (~2^17), chunks no shorter than ~2 windows."""
+        if T_m <= 0:
+            return 1
+        want = max(1, -(-131072 // max(N, 1)))
+        return int(max(1, min(want, T_m // max(2 * (J + skip + 1), 1), 256)))
+
+    def momentum_chunked(self, PM, J=12, skip=1, chunks=None, with_ret=False, next_pm=None,
+                         out=None, workspace=None):
+        """csm_momentum_chunked: the scan split into `chunks` concurrent month ranges."""
+        T_m, N = PM.shape
+        _need(PM, "PM", torch.float64, (T_m, N), self.device)
+        C = self.default_chunks(T_m, N, J, skip) if chunks is None else int(chunks)
+        if next_pm is not None:
+            _need(next_pm, "next_pm", torch.float64, (N,), self.device)
+        if out is None:
+            R = self.empty((T_m, N)) if with_ret else None
+            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
+        else:
+            R, M, NR = out
+        nbytes = int(self.lib.csm_momentum_chunked_workspace(T_m, N, int(J), int(skip), C))
+        if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
+            workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
+        self._call("csm_momentum_chunked", _ptr(PM), T_m, N, int(J), int(skip), C, _ptr(R),
+                   _ptr(M), _ptr(NR), _ptr(next_pm), _ptr(workspace))
+        return R, M, NR
+
     def signal(self, P, month_start, max_month_days, J=12, skip=1, with_pm=False,
                with_ret=False, carry=None, next_pm=None, carry_out=None, out=None):
         """Fused month-end + scan (csm_signal): one pass over the daily panel, no PM round
@@ -220,8 +249,8 @@ class Engine:
     # ------------------------------------------------------------------ pipeline
     def use_fused(self, P, V=None, max_month_days=None) -> bool:
         T_d, N = P.shape
-        return (V is None and N % 2 == 0 and N >= FUSED_MIN_N and P.data_ptr() % 16 == 0
-                and max_month_days is not None and max_month_days <= 32)
+        return (V is None and N >= FUSED_MIN_N and max_month_days is not None
+                and max_month_days <= 32)
 
     def run(self, P, month_start, J=12, skip=1, n_bins=10, V=None, with_ret=False,
             max_month_days=None, fused=None):
@@ -238,7 +267,10 @@ class Engine:
             VOL = None
         else:
             PM, VOL = self.month_end(P, month_start, V)
-            R, M, NR = self.momentum(PM, J, skip, with_ret=with_ret)
+            if self.default_chunks(T_m, N, J, skip) > 1:
+                R, M, NR = self.momentum_chunked(PM, J, skip, with_ret=with_ret)
+            else:
+                R, M, NR = self.momentum(PM, J, skip, with_ret=with_ret)
         L, EW, CNT, NV = self.deciles(M, NR, n_bins, with_nv=True)
         LS = self.long_short(EW, CNT)
         return PipelineOut(PM=PM, M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS, R=R, VOL=VOL, NV=NV)

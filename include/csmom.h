@@ -38,6 +38,12 @@ typedef struct csm_ctx csm_ctx;
 
 int csm_abi_version(void);
 
+/* Process-wide tuning knobs for A/B measurement: "signal_vec" (1|2 assets per lane in the
+ * fused kernel), "signal_nbuf" (3|4 month buffers), "dec_ablate" (profiling-only bitmask
+ * that SKIPS decile passes and so produces wrong results).  Returns CSM_E_INVAL for an
+ * unknown key or value. */
+int csm_tune(const char* key, int value);
+
 /* Create a context bound to HIP device `device` (stream = the null stream). */
 int csm_create(int device, csm_ctx** out);
 int csm_destroy(csm_ctx* ctx);
@@ -78,10 +84,23 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
                  const double* next_pm, double* carry_out);
 
 /*
+ * Time-chunked scan for panels with few assets: the months are split into C contiguous
+ * chunks that are scanned concurrently from exactly rebuilt boundary states (the date-shard
+ * summary/fold of csm_shard_summary / csm_fold_carry, inside one GPU).  Same outputs as
+ * csm_momentum (no carry input).  workspace: device buffer of
+ * csm_momentum_chunked_workspace(T_m, N, J, skip, C) bytes.
+ */
+int64_t csm_momentum_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                                       int32_t C);
+int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                         int32_t skip, int32_t C, double* R, double* M, double* NR,
+                         const double* next_pm, void* workspace);
+
+/*
  * Fused month-end aggregation + scan in one pass over the daily panel (csm_month_end then
  * csm_momentum without the PM round trip).  Same outputs and carry contract as
- * csm_momentum; PM and R nullable; no volume.  Needs even N, 16-B aligned P, and
- * max_month_days (HOST value: the longest month in days) <= 32.
+ * csm_momentum; PM and R nullable; no volume.  max_month_days (HOST value: the longest
+ * month in days) must be <= 32.  Even N with 16-B aligned P takes 16-B row loads.
  */
 int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
                int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, double* PM,

@@ -204,12 +204,37 @@ def test_fused_signal_large_panel_vs_oracle(engine):
     assert max_rel(out.LS.cpu().numpy(), ref["LS"]) <= REL
 
 
-def test_fused_rejects_bad_layouts(engine):
+def test_fused_odd_n_and_variants(engine):
+    """Odd N runs the fused kernel with one asset per lane; every (assets-per-lane, buffer
+    depth) variant gives the same bits."""
+    z = load_golden("edge")
+    P = z["P"][:, :-1]
+    ms_h = z["month_start"].astype(np.int64)
+    maxd = int(np.diff(ms_h).max())
+    ref = O.pipeline(P, ms_h, 12, 1, 10)
+    out = engine.run(_up(P), _up(ms_h), 12, 1, 10, max_month_days=maxd, fused=True)
+    for k in ("PM", "M", "NR"):
+        assert bits_equal(getattr(out, k).cpu().numpy(), ref[k]), k
+    assert np.array_equal(out.L.cpu().numpy(), ref["L"])
+    P2, ms2 = _up(z["P"]), _up(ms_h)
+    base = engine.signal(P2, ms2, maxd, 12, 1, with_pm=True)
+    lib = engine.lib
+    try:
+        for vec in (1, 2):
+            for nbuf in (3, 4):
+                assert lib.csm_tune(b"signal_vec", vec) == 0 and lib.csm_tune(b"signal_nbuf", nbuf) == 0
+                got = engine.signal(P2, ms2, maxd, 12, 1, with_pm=True)
+                for a, b in zip(got, base):
+                    if a is not None:
+                        assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (vec, nbuf)
+    finally:
+        lib.csm_tune(b"signal_vec", 2)
+        lib.csm_tune(b"signal_nbuf", 3)
+    assert lib.csm_tune(b"nope", 1) != 0
+
+
+def test_fused_rejects_long_months(engine):
     import csmom
-    P = torch.zeros((10, 7), dtype=torch.float64, device="cuda:0")
-    ms = torch.tensor([0, 5, 10], dtype=torch.int64, device="cuda:0")
-    with pytest.raises(csmom.CsmError):
-        engine.signal(P, ms, 5)          # odd N
     P2 = torch.zeros((40, 8), dtype=torch.float64, device="cuda:0")
     ms2 = torch.tensor([0, 40], dtype=torch.int64, device="cuda:0")
     with pytest.raises(csmom.CsmError):

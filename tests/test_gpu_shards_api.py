@@ -126,3 +126,28 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setenv("CSMOM_LIB", str(tmp_path / "nope.so"))
     with pytest.raises(csmom.CsmUnavailable):
         csmom.Engine(0)
+
+
+@pytest.mark.parametrize("name,J,skip", [("edge", 12, 1), ("edge", 3, 0), ("longwin", 24, 1),
+                                         ("c1", 12, 1)])
+@pytest.mark.parametrize("C", [2, 3, 7, 16])
+def test_chunked_scan_equals_single_scan(engine, name, J, skip, C):
+    z = load_golden(name)
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    R, M, NR = engine.momentum(PM, J, skip, with_ret=True)
+    Rc, Mc, NRc = engine.momentum_chunked(PM, J, skip, chunks=C, with_ret=True)
+    assert bits_equal(Rc.cpu().numpy(), R.cpu().numpy())
+    assert bits_equal(Mc.cpu().numpy(), M.cpu().numpy())
+    assert bits_equal(NRc.cpu().numpy(), NR.cpu().numpy())
+
+
+def test_chunked_scan_with_tail_next_pm(engine):
+    """next_pm (the price after the panel) reaches the pending row of the last chunk and of
+    assets absent from all later chunks."""
+    z = load_golden("edge")
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    npm = PM[-1].clone()
+    _, M, NR = engine.momentum(PM[:-1].contiguous(), 12, 1, next_pm=npm)
+    _, Mc, NRc = engine.momentum_chunked(PM[:-1].contiguous(), 12, 1, chunks=5, next_pm=npm)
+    assert bits_equal(NRc.cpu().numpy(), NR.cpu().numpy())
+    assert bits_equal(Mc.cpu().numpy(), M.cpu().numpy())
