@@ -21,7 +21,8 @@ EXPORTS = (
     "csm_abi_version", "csm_create", "csm_destroy", "csm_last_error", "csm_set_stream",
     "csm_sync", "csm_month_end", "csm_momentum", "csm_deciles", "csm_long_short",
     "csm_shard_summary", "csm_fold_carry", "csm_signal", "csm_momentum_chunked",
-    "csm_momentum_chunked_workspace", "csm_tune",
+    "csm_momentum_chunked_workspace", "csm_tune", "csm_signal_tiled", "csm_tile_panel",
+    "csm_tiled_size",
 )
 
 
@@ -59,6 +60,10 @@ def _declare(lib):
         "csm_momentum": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p]),
         "csm_signal": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
                                       _p, _p, _p]),
+        "csm_signal_tiled": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p,
+                                            _p, _p, _p, _p, _p]),
+        "csm_tiled_size": (ctypes.c_int64, [_i64, _i64]),
+        "csm_tile_panel": (ctypes.c_int, [_p, _p, _i64, _i64, _p]),
         "csm_momentum_chunked": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _i32, _p, _p, _p,
                                                 _p, _p]),
         "csm_momentum_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),

@@ -133,6 +133,41 @@ __global__ __launch_bounds__(256) void k_month_end(const double* __restrict__ P,
   }
 }
 
+// Kernel A' (one-shot month-end): one thread per (two assets, month) issues all MAXD day-row
+// loads of its month at once (rows past the month's end re-load its last row: cache hits that
+// change neither "last non-NaN" nor "any present"), reduces and exits.  The grid sweeps the
+// panel in address order, the access pattern of the fastest read microbenchmark (scripts/mb).
+template <int MAXD>
+__global__ __launch_bounds__(256) void k_month_end_rows(const double* __restrict__ P,
+                                                        const int64_t* __restrict__ month_start,
+                                                        int64_t N, double* __restrict__ PM) {
+  const int m = blockIdx.y;
+  const int64_t a = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (a >= N) return;
+  const int64_t f0 = month_start[m], nn = month_start[m + 1] - f0;
+  const double* p = P + f0 * N + a;
+  double2 X[MAXD];
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k)
+    X[k] = *reinterpret_cast<const double2*>(p + (int64_t)(k < nn ? k : nn - 1) * N);
+  double pm[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    double last = 0.0;
+    bool pr = false, v = false;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+      const double x = c == 0 ? X[k].x : X[k].y;
+      const bool ok = x == x;
+      pr |= !is_absent(x);
+      v |= ok;
+      last = ok ? x : last;
+    }
+    pm[c] = pr ? (v ? last : qnan()) : absent_val();
+  }
+  *reinterpret_cast<double2*>(PM + (int64_t)m * N + a) = make_double2(pm[0], pm[1]);
+}
+
 // =====================================================================================
 // Per-asset scan state and one present-row step (shared by k_momentum and k_signal).
 // The J+skip ring of factors fl(1+ret) lives in LDS, slot-major with a per-lane column
@@ -162,7 +197,16 @@ __device__ __forceinline__ void scan_init(ScanLane& s, double* ring, int RS, int
   s.prev = -1;
 }
 
+// Output stores of the scan: ST = 0 plain, 1 nontemporal (the monthly panels are consumed by
+// the next kernel from HBM anyway), 2 none (profiling ablation only: results are discarded).
+template <int ST>
+__device__ __forceinline__ void st_out(double* p, double v) {
+  if (ST == 0) *p = v;
+  else if (ST == 1) __builtin_nontemporal_store(v, p);
+}
+
 // Consumes month m's price x of asset a; returns mom (NaN when absent / undefined).
+template <int ST = 0>
 __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double* ring, int RS,
                                             int W, int J, int64_t N, int64_t a,
                                             double* __restrict__ R, double* __restrict__ M,
@@ -170,9 +214,9 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
   const double NaN = qnan();
   const int64_t o = (int64_t)m * N + a;
   if (is_absent(x)) {
-    if (R) R[o] = NaN;
-    M[o] = NaN;
-    NR[o] = NaN;
+    if (R) st_out<ST>(R + o, NaN);
+    st_out<ST>(M + o, NaN);
+    st_out<ST>(NR + o, NaN);
     return NaN;
   }
   const bool xv = !isnan_d(x);
@@ -190,16 +234,17 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
   const double mom = acc - 1.0;
   const bool ranked = !isnan_d(mom);
   const double ps_new = xv ? x : s.psff;
-  if (s.prev >= 0) NR[(int64_t)s.prev * N + a] = ps_new / s.psff - 1.0;
+  if (s.prev >= 0) st_out<ST>(NR + (int64_t)s.prev * N + a, ps_new / s.psff - 1.0);
   if (ranked) {
     s.psff = ps_new;
     s.prev = m;
   } else {
-    NR[o] = NaN;
+    st_out<ST>(NR + o, NaN);
     s.prev = -1;
   }
-  if (R) R[o] = ret;
-  M[o] = mom;
+  if (R) st_out<ST>(R + o, ret);
+  st_out<ST>(M + o, mom);
+  if (ST == 2 && mom == 1234.5678) M[o] = mom;  // keeps the ablated scan's work alive
   return mom;
 }
 
@@ -321,23 +366,31 @@ template <> struct RowT<2> { typedef double2 T; };
 __device__ __forceinline__ double comp(double v, int) { return v; }
 __device__ __forceinline__ double comp(double2 v, int k) { return k == 0 ? v.x : v.y; }
 
-template <int MAXD, int VEC, int NBUF>
-__global__ __launch_bounds__(64) void k_signal(
+// TILED: P is the asset-tiled panel [ceil(N/128)][T_d][128] (csm_tile_panel) and the wave's
+// 128 assets (VEC = 2) are one tile, so its whole history is one contiguous T_d KiB stream;
+// otherwise P is row-major [T_d][N] and consecutive day rows of a wave are N * 8 B apart.
+// BW > 1 (row-major only): BW waves cover 64 * VEC * BW adjacent assets and meet at a
+// barrier every NBUF months, so a workgroup's day-row reads stay BW KiB contiguous in time.
+template <int MAXD, int VEC, int NBUF, bool TILED = false, int ST = 0, int BW = 1>
+__global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out) {
+    double* __restrict__ carry_out, int64_t T_d) {
+  static_assert(!TILED || BW == 1, "tiled panels are read one tile per wave");
   typedef typename RowT<VEC>::T VT;
-  extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC]
+  extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC * BW]
   const int W = J + skip;
   const int tid = threadIdx.x;
-  const int64_t a0 = ((int64_t)blockIdx.x * 64 + tid) * VEC;
+  const int64_t a0 = ((int64_t)blockIdx.x * 64 * BW + tid) * VEC;
   const bool live = a0 < N;
-  const int RS = 64 * VEC;
+  const int RS = 64 * VEC * BW;
   ScanLane sl[VEC];
 #pragma unroll
   for (int k = 0; k < VEC; ++k) scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, carry, N, a0 + k, live);
-  const double* base = P + (live ? a0 : 0);
+  const double* base = TILED ? P + (int64_t)blockIdx.x * T_d * (64 * VEC) + VEC * tid
+                             : P + (live ? a0 : 0);
+  const int64_t rstride = TILED ? 64 * VEC : N;
   // Loads are issued unconditionally (months past the end re-load the last month: cache
   // hits) so every wait is a counted vmcnt; only the processing is guarded.
   auto load_month = [&](VT (&buf)[MAXD], int mm) {
@@ -345,7 +398,7 @@ __global__ __launch_bounds__(64) void k_signal(
     const int64_t f0 = month_start[mm], nn = month_start[mm + 1] - f0;
 #pragma unroll
     for (int k = 0; k < MAXD; ++k)
-      buf[k] = *reinterpret_cast<const VT*>(base + (f0 + (k < nn ? k : nn - 1)) * N);
+      buf[k] = *reinterpret_cast<const VT*>(base + (f0 + (k < nn ? k : nn - 1)) * rstride);
   };
   auto process = [&](const VT (&X)[MAXD], int m) {
     double pm[VEC];
@@ -370,7 +423,7 @@ __global__ __launch_bounds__(64) void k_signal(
       }
 #pragma unroll
       for (int c = 0; c < VEC; ++c)
-        scan_step(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
+        scan_step<ST>(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
     }
   };
   VT A[MAXD], B[MAXD], C[MAXD];
@@ -395,6 +448,7 @@ __global__ __launch_bounds__(64) void k_signal(
     load_month(C, 2);
     for (int m = 0; m < T_m; m += 4) {
       load_month(D, m + 3);
+      if (BW > 1) __syncthreads();
       process(A, m);
       load_month(A, m + 4);
       if (m + 1 < T_m) process(B, m + 1);
@@ -409,6 +463,110 @@ __global__ __launch_bounds__(64) void k_signal(
     for (int k = 0; k < VEC; ++k)
       scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm, carry_out);
   }
+}
+
+// =====================================================================================
+// Kernel AB' (fused, multi-wave): the same month-end + scan as k_signal, with the month
+// reductions spread over NW waves.  A workgroup owns 128 assets (two per lane for the 16-B
+// row loads).  Months go round-robin to the waves: in batch b, wave w reduces month
+// b*NW + w for all 128 assets and parks the month prices in LDS; after one barrier every
+// wave scans its 128/NW assets through the batch's NW months in order.  The next batch's
+// day rows (NB = 2: the next two batches') are in flight during the barrier and the scan,
+// so one workgroup keeps NW..2*NW months of loads outstanding and the sequential scan is
+// spread over NW SIMDs instead of one.  Results are bit-identical to k_signal.
+// =====================================================================================
+// Every workgroup must be resident at once (each lives for the whole kernel): 782 x NW waves
+// at C4 on 1024 SIMDs, so NW = 4 asks for <= 128 VGPRs (4 waves per SIMD).
+template <int MAXD, int NW, int NB>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 4 && NB == 1 ? 4 : 2)))
+void k_signal_mw(
+    const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
+    int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
+    double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
+    double* __restrict__ carry_out) {
+  constexpr int TA = 128;           // assets per workgroup
+  constexpr int SA = TA / NW;       // assets each wave scans
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* pmb = lds;                // [2][NW][TA] month prices, double-buffered by batch parity
+  double* ring = lds + 2 * NW * TA; // [W][TA] scan rings
+  const int W = J + skip;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * TA;
+  // reduction role: lane covers assets t0 + 2*lane, +1
+  const int64_t ar = t0 + 2 * lane;
+  const bool rlive = ar < N;        // N even: both assets live together
+  const double* base = P + (rlive ? ar : 0);
+  // scan role: lane < SA covers asset t0 + w*SA + lane
+  const int ci = w * SA + lane;
+  const int64_t as = t0 + ci;
+  const bool slive = lane < SA && as < N;
+  ScanLane sl;
+  if (lane < SA) scan_init(sl, ring + ci, TA, W, carry, N, as, slive);  // lanes >= SA own no column
+  const int nbatch = (T_m + NW - 1) / NW;
+  auto load_month = [&](double2 (&buf)[MAXD], int mm) {
+    mm = mm < T_m ? mm : T_m - 1;
+    const int64_t f0 = month_start[mm], nn = month_start[mm + 1] - f0;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k)
+      buf[k] = *reinterpret_cast<const double2*>(base + (f0 + (k < nn ? k : nn - 1)) * N);
+  };
+  auto reduce_park = [&](const double2 (&X)[MAXD], int m, double* dst) {
+    double pm[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      double last = 0.0;
+      bool p = false, v = false;
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k) {
+        const double x = c == 0 ? X[k].x : X[k].y;
+        const bool ok = x == x;
+        p |= !is_absent(x);
+        v |= ok;
+        last = ok ? x : last;
+      }
+      pm[c] = p ? (v ? last : qnan()) : absent_val();
+    }
+    *reinterpret_cast<double2*>(dst + 2 * lane) = make_double2(pm[0], pm[1]);
+    if (PMo && rlive && m < T_m)
+      *reinterpret_cast<double2*>(PMo + (int64_t)m * N + ar) = make_double2(pm[0], pm[1]);
+  };
+  auto scan_batch = [&](int b) {
+    const double* src = pmb + (b & 1) * NW * TA;
+    if (slive) {
+      for (int j = 0; j < NW; ++j) {
+        const int m = b * NW + j;
+        if (m >= T_m) break;
+        scan_step(sl, src[j * TA + ci], m, ring + ci, TA, W, J, N, as, R, M, NR);
+      }
+    }
+  };
+  double2 A[MAXD];
+  if (NB == 1) {
+    load_month(A, w);
+    for (int b = 0; b < nbatch; ++b) {
+      reduce_park(A, b * NW + w, pmb + (b & 1) * NW * TA + w * TA);
+      load_month(A, (b + 1) * NW + w);
+      __syncthreads();
+      scan_batch(b);
+    }
+  } else {
+    double2 B[MAXD];
+    load_month(A, w);
+    load_month(B, NW + w);
+    for (int b = 0; b < nbatch; b += 2) {
+      reduce_park(A, b * NW + w, pmb + w * TA);
+      load_month(A, (b + 2) * NW + w);
+      __syncthreads();
+      scan_batch(b);
+      if (b + 1 < nbatch) {
+        reduce_park(B, (b + 1) * NW + w, pmb + NW * TA + w * TA);
+        load_month(B, (b + 3) * NW + w);
+        __syncthreads();
+        scan_batch(b + 1);
+      }
+    }
+  }
+  if (slive) scan_finish(sl, ring + ci, TA, W, N, as, NR, next_pm, carry_out);
 }
 
 // =====================================================================================
@@ -472,6 +630,9 @@ struct DecShared {
   double red_d[DEC_THREADS / 64][2];
   unsigned long long red_k[DEC_THREADS / 64][2];
   int64_t red_n[DEC_THREADS / 64];
+  int red_n2[DEC_THREADS / 64][2];
+  int tpre[MAXT + 1];   // prefix of unresolved member counts over the targets
+  int sel_count;        // 1: counting selection, 0: bitonic sort
 };
 
 // Monotone non-decreasing in x for any lo / scale (values outside [lo, lo + HB/scale)
@@ -521,25 +682,51 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
-// Exclusive scan of S.hist in place; returns nothing (hist[b] becomes prefix).
+// Block-wide (min, max) and (sum, sum) over DEC_THREADS; every thread gets the results.
+// Two barriers each (the scratch is reusable on return).
+__device__ __forceinline__ void block_minmax(double mn, double mx, double& gmn, double& gmx,
+                                             double (*scr)[2]) {
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fmin(mn, __shfl_down(mn, o, 64));
+    mx = fmax(mx, __shfl_down(mx, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) { scr[threadIdx.x >> 6][0] = mn; scr[threadIdx.x >> 6][1] = mx; }
+  __syncthreads();
+  gmn = INFINITY; gmx = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < DEC_THREADS / 64; ++w) { gmn = fmin(gmn, scr[w][0]); gmx = fmax(gmx, scr[w][1]); }
+  __syncthreads();
+}
+__device__ __forceinline__ void block_sum2(int a, int b, int& ga, int& gb, int (*scr)[2]) {
+  for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
+  if ((threadIdx.x & 63) == 0) { scr[threadIdx.x >> 6][0] = a; scr[threadIdx.x >> 6][1] = b; }
+  __syncthreads();
+  ga = 0; gb = 0;
+#pragma unroll
+  for (int w = 0; w < DEC_THREADS / 64; ++w) { ga += scr[w][0]; gb += scr[w][1]; }
+  __syncthreads();
+}
+
+// Exclusive scan of hist[HB] in place (hist[b] becomes the count of buckets < b): per-thread
+// sums of 8 consecutive buckets, a wave scan by shuffles, then the wave totals.  Two barriers.
 __device__ void block_exclusive_scan_hist(uint32_t* hist) {
-  __shared__ uint32_t part[DEC_THREADS];
-  const int tid = threadIdx.x;
-  const int per = HB / DEC_THREADS;  // 8
-  uint32_t loc[HB / DEC_THREADS];
+  __shared__ uint32_t wtot[DEC_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int per = HB / DEC_THREADS;  // 8
+  uint32_t loc[per];
   uint32_t s = 0;
 #pragma unroll
   for (int j = 0; j < per; ++j) { loc[j] = hist[tid * per + j]; s += loc[j]; }
-  part[tid] = s;
-  __syncthreads();
-  // Hillis-Steele over DEC_THREADS partials
-  for (int off = 1; off < DEC_THREADS; off <<= 1) {
-    uint32_t v = (tid >= off) ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
+  uint32_t inc = s;  // inclusive wave scan
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
   }
-  uint32_t run = part[tid] - s;
+  if (lane == 63) wtot[wid] = inc;
+  __syncthreads();
+  uint32_t run = inc - s;
+  for (int w = 0; w < wid; ++w) run += wtot[w];
 #pragma unroll
   for (int j = 0; j < per; ++j) { hist[tid * per + j] = run; run += loc[j]; }
   __syncthreads();
@@ -572,43 +759,49 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
   // keeps heavy momentum tails from squeezing the bulk into a few buckets.  The exact
   // count / min / max come out of the histogram pass itself.
   {
-    if (tid == 0) S.total = 0;
-    __syncthreads();
-    constexpr int SCH = 32;  // 32 chunks x 64 consecutive assets
-    const int64_t chunk = 64;
-    for (int c = tid >> 6; c < SCH; c += DEC_THREADS / 64) {
-      const int64_t start = (N <= SCH * chunk) ? (int64_t)c * chunk
-                                               : ((int64_t)c * (N - chunk)) / (SCH - 1);
-      const int64_t i = start + (tid & 63);
-      if (i < N) {
-        const double x = row[i];
-        if (!isnan_d(x)) S.cand[atomicAdd(&S.total, 1)] = x;
-      }
+    // 32 chunks x 64 consecutive assets, 4 samples per thread held in registers.  The
+    // (ns * 2 / 1000)-th smallest and largest samples are found by extracting the distinct
+    // minima / maxima in rounds (each round takes every copy of a value): <= 5 rounds of two
+    // block reductions instead of sorting the sample.
+    constexpr int SCH = 32, PER = SCH * 64 / DEC_THREADS;
+    double xs[PER];
+    int nloc = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int c = (tid >> 6) + k * (DEC_THREADS / 64);
+      const int64_t start = (N <= SCH * 64) ? (int64_t)c * 64 : ((int64_t)c * (N - 64)) / (SCH - 1);
+      const int64_t i = start + lane;
+      xs[k] = (i < N) ? row[i] : qnan();
+      nloc += (xs[k] == xs[k]) ? 1 : 0;
     }
-    __syncthreads();
-    const int ns = S.total;
-    int P2 = 1;
-    while (P2 < ns) P2 <<= 1;
-    for (int i = ns + tid; i < P2; i += DEC_THREADS) S.cand[i] = INFINITY;
-    __syncthreads();
-    for (int k = 2; k <= P2; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < P2; i += DEC_THREADS) {
-          const int ixj = i ^ j;
-          if (ixj > i) {
-            const double x = S.cand[i], y = S.cand[ixj];
-            if ((x > y) == ((i & k) == 0)) { S.cand[i] = y; S.cand[ixj] = x; }
-          }
+    int ns, dummy;
+    block_sum2(nloc, 0, ns, dummy, S.red_n2);
+    double lo = 0.0, hi = 0.0;
+    if (ns >= 2) {
+      const int idx = (ns * 2) / 1000;
+      double cur_lo = -INFINITY, cur_hi = INFINITY;
+      int below = 0, above = 0;
+      bool lo_done = false, hi_done = false;
+      while (!(lo_done && hi_done)) {  // block-uniform
+        double mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          const double x = xs[k];
+          if (x > cur_lo) mn = fmin(mn, x);
+          if (x < cur_hi) mx = fmax(mx, x);
         }
-        __syncthreads();
+        double gmn, gmx;
+        block_minmax(mn, mx, gmn, gmx, S.red_d);
+        int c1 = 0, c2 = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) { c1 += xs[k] == gmn ? 1 : 0; c2 += xs[k] == gmx ? 1 : 0; }
+        int g1, g2;
+        block_sum2(c1, c2, g1, g2, S.red_n2);
+        if (!lo_done) { if (below + g1 > idx) { lo = gmn; lo_done = true; } else { below += g1; cur_lo = gmn; } }
+        if (!hi_done) { if (above + g2 > idx) { hi = gmx; hi_done = true; } else { above += g2; cur_hi = gmx; } }
       }
     }
     if (tid == 0) {
-      double lo = 0.0, hi = 0.0;
-      if (ns >= 2) {
-        lo = S.cand[(ns * 2) / 1000];
-        hi = S.cand[ns - 1 - (ns * 2) / 1000];
-      }
       const double rng = hi - lo;
       S.vmin = lo;
       S.scale = (rng > 0.0 && rng <= 1.0e300) ? (double)HB / rng : 0.0;
@@ -834,8 +1027,43 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
       });
     }
     __syncthreads();
-    // ---------------- bitonic sort of the candidates (slot ranges are value-ordered)
-    {
+    // ---------------- order statistics inside the slots.  Small slots (the usual case: a
+    // few dozen members each) use counting selection: the member whose rank inside its slot
+    // (ties broken by position) equals the target's residual rank is the order statistic --
+    // one pass, no barriers.  Large slots fall back to a bitonic sort of all candidates.
+    if (tid == 0) {
+      int64_t work = 0;
+      S.tpre[0] = 0;
+      for (int i = 0; i < S.ntgt; ++i) {
+        const Slot& sl = S.slots[S.tslot[i]];
+        const int c = sl.resolved ? 0 : sl.count;
+        S.tpre[i + 1] = S.tpre[i] + c;
+        work += (int64_t)c * c;
+      }
+      S.sel_count = work <= (int64_t)DEC_THREADS * 512;
+    }
+    __syncthreads();
+    if (S.sel_count) {
+      const int ntg = S.ntgt, tot = S.tpre[ntg];
+      for (int p = tid; p < tot; p += DEC_THREADS) {
+        int t2 = 0;
+        while (S.tpre[t2 + 1] <= p) ++t2;
+        const Slot& sl = S.slots[S.tslot[t2]];
+        const int i = p - S.tpre[t2];
+        const double* c = S.cand + sl.off;
+        const double x = c[i];
+        int rank = 0;
+        for (int j = 0; j < sl.count; ++j) {
+          const double y = c[j];
+          rank += (y < x || (y == x && j < i)) ? 1 : 0;
+        }
+        if (rank == S.tres[t2]) S.tval[t2] = x;
+      }
+      if (tid < ntg) {
+        const Slot& sl = S.slots[S.tslot[tid]];
+        if (sl.resolved) S.tval[tid] = sl.value;
+      }
+    } else {
       const int tot = S.total;
       int P2 = 1;
       while (P2 < tot) P2 <<= 1;
@@ -854,10 +1082,10 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
           __syncthreads();
         }
       }
-    }
-    if (tid < S.ntgt) {
-      const Slot& s = S.slots[S.tslot[tid]];
-      S.tval[tid] = s.resolved ? s.value : S.cand[s.off + S.tres[tid]];
+      if (tid < S.ntgt) {
+        const Slot& sl = S.slots[S.tslot[tid]];
+        S.tval[tid] = sl.resolved ? sl.value : S.cand[sl.off + S.tres[tid]];
+      }
     }
     __syncthreads();
     // ---------------- edges (NumPy _lerp) and duplicates='drop'
@@ -1213,12 +1441,39 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 }
 
 // =====================================================================================
+// Panel re-blocking [T_d][N] -> [ceil(N/128)][T_d][128] (csm_tile_panel).  Both sides are
+// contiguous 1 KiB (tile, day) rows; assets past N in the last tile are ABSENT.
+// =====================================================================================
+#define CSM_TILE 128
+__global__ __launch_bounds__(256) void k_tile_panel(const double* __restrict__ P, int64_t T_d,
+                                                    int64_t N, double* __restrict__ Pt) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (tile, day)
+  const int lane = threadIdx.x & 63;
+  const int64_t tiles = (N + CSM_TILE - 1) / CSM_TILE;
+  if (row >= tiles * T_d) return;
+  const int64_t tile = row / T_d, d = row - tile * T_d;
+  const int64_t a = tile * CSM_TILE + 2 * lane;
+  double2 v;
+  if (a + 1 < N) {
+    v = *reinterpret_cast<const double2*>(P + d * N + a);
+  } else {
+    v.x = a < N ? P[d * N + a] : absent_val();
+    v.y = absent_val();
+  }
+  *reinterpret_cast<double2*>(Pt + row * CSM_TILE + 2 * lane) = v;
+}
+
+// =====================================================================================
 // C ABI
 // =====================================================================================
 // Process-wide tuning knobs (csm_tune): kernel variants for A/B measurement in one process.
-static int g_tune_signal_vec = 2;   // k_signal assets per lane: 1 or 2
-static int g_tune_signal_nbuf = 3;  // k_signal month buffers: 3 or 4
-static int g_tune_dec_ablate = 0;   // k_deciles pass ablation bitmask (profiling only: wrong results)
+static int g_tune_signal_vec = 2;      // k_signal assets per lane: 1 or 2
+static int g_tune_signal_nbuf = 4;     // k_signal month buffers: 3 or 4
+static int g_tune_dec_ablate = 0;      // k_deciles pass ablation bitmask (profiling only: wrong results)
+static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<.., NW, NB>
+static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
+static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
+static int g_tune_month_end_rows = 0;  // >0: csm_month_end uses k_month_end_rows (value = max month days)
 
 struct csm_ctx {
   int device;
@@ -1267,6 +1522,11 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_nbuf") && (value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
   if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
+  if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
+  if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
+  if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
+  if (!strcmp(key, "signal_mw") && (value == 0 || value == 21 || value == 22 || value == 41 ||
+                                    value == 42)) { g_tune_signal_mw = value; return CSM_OK; }
   return CSM_E_INVAL;
 }
 
@@ -1315,6 +1575,15 @@ int csm_month_end(csm_ctx* ctx, const double* P, const double* V, int64_t T_d, i
     return set_err(ctx, CSM_E_INVAL, "csm_month_end: V and VOL must both be given or both NULL");
   if (T_m == 0) return CSM_OK;
   const bool v2 = (N % 2 == 0) && aligned16(P) && aligned16(PM) && (!V || aligned16(V));
+  if (v2 && !V && g_tune_month_end_rows > 0 && T_d > 0) {
+    // one-shot variant: every month must fit MAXD rows (host-checked bound)
+    const int maxd = g_tune_month_end_rows;
+    dim3 g2((unsigned)((N / 2 + 255) / 256), (unsigned)T_m);
+    if (maxd <= 24) hipLaunchKernelGGL((k_month_end_rows<24>), g2, dim3(256), 0, ctx->stream, P, month_start, N, PM);
+    else hipLaunchKernelGGL((k_month_end_rows<32>), g2, dim3(256), 0, ctx->stream, P, month_start, N, PM);
+    LAUNCH_CHECK(ctx, "k_month_end_rows");
+    return CSM_OK;
+  }
   const int vec = v2 ? 2 : 1;
   dim3 grid((unsigned)((N + 256LL * vec - 1) / (256LL * vec)), (unsigned)T_m);
   if (v2) {
@@ -1349,43 +1618,118 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
   return CSM_OK;
 }
 
-int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
-               int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
-               double* M, double* NR, const double* carry, const double* next_pm,
-               double* carry_out) {
+static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double* P, int64_t T_d,
+                         int64_t N, const int64_t* month_start, int32_t T_m,
+                         int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
+                         double* M, double* NR, const double* carry, const double* next_pm,
+                         double* carry_out) {
   int r = prep(ctx);
   if (r) return r;
   if (!P || !month_start || !M || !NR || N <= 0 || T_d < 0 || T_m < 0 || J < 1 || skip < 0 ||
       J + skip > 256 || max_month_days < 1)
-    return set_err(ctx, CSM_E_INVAL, "csm_signal: bad arguments (N=%lld T_m=%d J=%d skip=%d)",
+    return set_err(ctx, CSM_E_INVAL, "%s: bad arguments (N=%lld T_m=%d J=%d skip=%d)", who,
                    (long long)N, T_m, J, skip);
   if (max_month_days > 32)
-    return set_err(ctx, CSM_E_INVAL, "csm_signal: months longer than 32 days are not supported "
-                   "(use csm_month_end + csm_momentum)");
+    return set_err(ctx, CSM_E_INVAL, "%s: months longer than 32 days are not supported "
+                   "(use csm_month_end + csm_momentum)", who);
+  if (tiled && (N % 2 != 0 || !aligned16(P) || !aligned16(M) || !aligned16(NR) ||
+                (PM && !aligned16(PM)) || (R && !aligned16(R))))
+    return set_err(ctx, CSM_E_INVAL, "%s: the tiled panel needs even N and 16-B aligned buffers", who);
   if (T_m == 0) return CSM_OK;
   const int W = J + skip;
   const bool can2 = (N % 2 == 0) && aligned16(P) && (!PM || aligned16(PM));
-  const int vec = (g_tune_signal_vec == 1 || !can2) ? 1 : 2;
-  const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : 4;
-  const size_t lds = (size_t)W * 64 * vec * sizeof(double);
-  const unsigned blocks = (unsigned)((N / vec + 63) / 64);
-  const void* fn = nullptr;
-#define SIG(MD, V, NB) (const void*)k_signal<MD, V, NB>
-  if (max_month_days <= 24)
-    fn = vec == 2 ? (nbuf == 3 ? SIG(24, 2, 3) : SIG(24, 2, 4)) : (nbuf == 3 ? SIG(24, 1, 3) : SIG(24, 1, 4));
-  else
-    fn = vec == 2 ? (nbuf == 3 ? SIG(32, 2, 3) : SIG(32, 2, 4)) : (nbuf == 3 ? SIG(32, 1, 3) : SIG(32, 1, 4));
-#undef SIG
-  if (lds > 65536)
-    HIP_CHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  {
+  if (!tiled && can2 && g_tune_signal_mw != 0) {
+    const int nw = g_tune_signal_mw / 10, nb = g_tune_signal_mw % 10;
+    const void* fm = nullptr;
+#define SMW(MD, NW_, NB_) (const void*)k_signal_mw<MD, NW_, NB_>
+    if (max_month_days <= 24)
+      fm = nw == 2 ? (nb == 1 ? SMW(24, 2, 1) : SMW(24, 2, 2)) : (nb == 1 ? SMW(24, 4, 1) : SMW(24, 4, 2));
+    else
+      fm = nw == 2 ? (nb == 1 ? SMW(32, 2, 1) : SMW(32, 2, 2)) : (nb == 1 ? SMW(32, 4, 1) : SMW(32, 4, 2));
+#undef SMW
+    const size_t ldsm = (size_t)(2 * nw + W) * 128 * sizeof(double);
+    if (ldsm > 65536)
+      HIP_CHECK(ctx, hipFuncSetAttribute(fm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsm));
     int T_m_ = T_m, J_ = J, skip_ = skip;
     int64_t N_ = N;
     void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
                     (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out};
-    HIP_CHECK(ctx, hipLaunchKernel(fn, dim3(blocks), dim3(64), args, lds, ctx->stream));
+    HIP_CHECK(ctx, hipLaunchKernel(fm, dim3((unsigned)((N + 127) / 128)), dim3(64 * nw), args, ldsm,
+                                   ctx->stream));
+    LAUNCH_CHECK(ctx, who);
+    return CSM_OK;
   }
-  LAUNCH_CHECK(ctx, "k_signal");
+  const int vec = tiled ? 2 : ((g_tune_signal_vec == 1 || !can2) ? 1 : 2);
+  const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : 4;
+  const int bw = (!tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
+  const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double);
+  const unsigned blocks = (unsigned)((N / vec + 64 * bw - 1) / (64 * bw));
+  const void* fn = nullptr;
+#define SIG(MD, V, NB) (const void*)k_signal<MD, V, NB, false>
+#define SIGT(MD, NB) (const void*)k_signal<MD, 2, NB, true>
+  if (tiled)
+    fn = max_month_days <= 24 ? (nbuf == 3 ? SIGT(24, 3) : SIGT(24, 4))
+                              : (nbuf == 3 ? SIGT(32, 3) : SIGT(32, 4));
+  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_bw == 2)
+    fn = (const void*)k_signal<24, 2, 4, false, 0, 2>;
+  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_bw == 4)
+    fn = (const void*)k_signal<24, 2, 4, false, 0, 4>;
+  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 1)
+    fn = (const void*)k_signal<24, 2, 4, false, 1>;
+  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 2)
+    fn = (const void*)k_signal<24, 2, 4, false, 2>;
+  else if (max_month_days <= 24)
+    fn = vec == 2 ? (nbuf == 3 ? SIG(24, 2, 3) : SIG(24, 2, 4)) : (nbuf == 3 ? SIG(24, 1, 3) : SIG(24, 1, 4));
+  else
+    fn = vec == 2 ? (nbuf == 3 ? SIG(32, 2, 3) : SIG(32, 2, 4)) : (nbuf == 3 ? SIG(32, 1, 3) : SIG(32, 1, 4));
+#undef SIG
+#undef SIGT
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  {
+    int T_m_ = T_m, J_ = J, skip_ = skip;
+    int64_t N_ = N, T_d_ = T_d;
+    void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
+                    (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out, &T_d_};
+    HIP_CHECK(ctx, hipLaunchKernel(fn, dim3(blocks), dim3(64 * bw), args, lds, ctx->stream));
+  }
+  LAUNCH_CHECK(ctx, who);
+  return CSM_OK;
+}
+
+int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
+               int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
+               double* M, double* NR, const double* carry, const double* next_pm,
+               double* carry_out) {
+  return signal_launch(ctx, "csm_signal", false, P, T_d, N, month_start, T_m, max_month_days, J,
+                       skip, PM, R, M, NR, carry, next_pm, carry_out);
+}
+
+int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
+                     const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
+                     int32_t skip, double* PM, double* R, double* M, double* NR,
+                     const double* carry, const double* next_pm, double* carry_out) {
+  return signal_launch(ctx, "csm_signal_tiled", true, Pt, T_d, N, month_start, T_m,
+                       max_month_days, J, skip, PM, R, M, NR, carry, next_pm, carry_out);
+}
+
+int64_t csm_tiled_size(int64_t T_d, int64_t N) {
+  if (T_d < 0 || N <= 0) return 0;
+  return ((N + CSM_TILE - 1) / CSM_TILE) * T_d * CSM_TILE;
+}
+
+int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double* Pt) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !Pt || N <= 0 || T_d < 0 || (N % 2) != 0 || !aligned16(P) || !aligned16(Pt))
+    return set_err(ctx, CSM_E_INVAL, "csm_tile_panel: bad arguments (N=%lld T_d=%lld; N even, "
+                   "16-B aligned buffers)", (long long)N, (long long)T_d);
+  if (T_d == 0) return CSM_OK;
+  const int64_t tiles = (N + CSM_TILE - 1) / CSM_TILE;
+  const int64_t rows = tiles * T_d;  // one 64-lane wave moves one 1 KiB (tile, day) row
+  const unsigned blocks = (unsigned)((rows + 3) / 4);
+  hipLaunchKernelGGL(k_tile_panel, dim3(blocks), dim3(256), 0, ctx->stream, P, T_d, N, Pt);
+  LAUNCH_CHECK(ctx, "k_tile_panel");
   return CSM_OK;
 }
 

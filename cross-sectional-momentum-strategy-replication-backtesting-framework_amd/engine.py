@@ -198,6 +198,40 @@ class Engine:
                    _ptr(next_pm), _ptr(carry_out))
         return PM, R, M, NR
 
+    def tile_panel(self, P, out=None):
+        """Re-block a row-major [T_d][N] panel into the asset-tiled layout
+        [ceil(N/128)][T_d][128] (csm_tile_panel); returns the flat tiled tensor."""
+        T_d, N = P.shape
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        n = int(self.lib.csm_tiled_size(T_d, N))
+        Pt = self.empty((n,)) if out is None else out
+        _need(Pt, "Pt", torch.float64, (n,), self.device)
+        self._call("csm_tile_panel", _ptr(P), T_d, N, _ptr(Pt))
+        return Pt
+
+    def signal_tiled(self, Pt, T_d, N, month_start, max_month_days, J=12, skip=1,
+                     with_pm=False, with_ret=False, carry=None, next_pm=None, carry_out=None,
+                     out=None):
+        """csm_signal_tiled: the fused month-end + scan over the tiled panel."""
+        T_m = month_start.numel() - 1
+        _need(Pt, "Pt", torch.float64, (int(self.lib.csm_tiled_size(T_d, N)),), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        W = J + skip
+        for t, nm, shp in ((carry, "carry", (W + 2, N)), (next_pm, "next_pm", (N,)),
+                           (carry_out, "carry_out", (W + 2, N))):
+            if t is not None:
+                _need(t, nm, torch.float64, shp, self.device)
+        if out is None:
+            PM = self.empty((T_m, N)) if with_pm else None
+            R = self.empty((T_m, N)) if with_ret else None
+            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
+        else:
+            PM, R, M, NR = out
+        self._call("csm_signal_tiled", _ptr(Pt), T_d, N, _ptr(month_start), T_m,
+                   int(max_month_days), int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR),
+                   _ptr(carry), _ptr(next_pm), _ptr(carry_out))
+        return PM, R, M, NR
+
     def deciles(self, M, NR=None, n_bins=10, out=None, with_nv=False):
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)

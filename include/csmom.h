@@ -108,6 +108,26 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
                double* carry_out);
 
 /*
+ * Asset-tiled daily panel (the engine's preferred HBM layout for the signal pass):
+ * Pt[ceil(N/128)][T_d][128] float64, assets past N ABSENT.  A 128-asset tile's whole history
+ * is one contiguous stream, so the per-asset time walk of csm_signal_tiled reads sequential
+ * KiB rows instead of rows N * 8 B apart.  csm_tiled_size returns the element count of Pt.
+ * csm_tile_panel re-blocks a row-major [T_d][N] panel (even N, 16-B aligned) into Pt; the
+ * host pivot (panel.py) can also write Pt directly.
+ */
+int64_t csm_tiled_size(int64_t T_d, int64_t N);
+int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double* Pt);
+
+/*
+ * csm_signal over the tiled panel Pt (same outputs, row-major [T_m][N]; same carry
+ * contract).  N even; 16-B aligned buffers.
+ */
+int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
+                     const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
+                     int32_t skip, double* PM, double* R, double* M, double* NR,
+                     const double* carry, const double* next_pm, double* carry_out);
+
+/*
  * Per-date qcut labels, fused with the equal-weight decile means.  Replaces
  * run_demo.py:18-29 (assign_deciles_per_date via pd.qcut(duplicates='drop')),
  * run_demo.py:46 (groupby('date').transform) and run_demo.py:49-55 (dropna +

@@ -229,8 +229,53 @@ def test_fused_odd_n_and_variants(engine):
                         assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (vec, nbuf)
     finally:
         lib.csm_tune(b"signal_vec", 2)
-        lib.csm_tune(b"signal_nbuf", 3)
+        lib.csm_tune(b"signal_nbuf", 4)
     assert lib.csm_tune(b"nope", 1) != 0
+
+
+@pytest.mark.parametrize("name", ["edge", "c1"])
+def test_signal_kernel_variants_bit_identical(engine, name):
+    """Every k_signal variant -- asset-tiled panel, multi-wave month reductions (k_signal_mw),
+    multi-wave workgroups, nontemporal stores -- and the one-shot month-end kernel produce the
+    same bits as the default fused kernel."""
+    z = load_golden(name)
+    P = z["P"]
+    if P.shape[1] % 2:
+        P = P[:, :-1]
+    ms_h = z["month_start"].astype(np.int64)
+    maxd = int(np.diff(ms_h).max())
+    T_d, N = P.shape
+    Pd, ms = _up(P), _up(ms_h)
+    lib = engine.lib
+    base = engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True)
+
+    def check(got, tag):
+        for a, b in zip(got, base):
+            if a is not None:
+                assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), tag
+    Pt = engine.tile_panel(Pd)
+    check(engine.signal_tiled(Pt, T_d, N, ms, maxd, 12, 1, with_pm=True, with_ret=True), "tiled")
+    # the tiled panel itself: tile t, day d, slot k holds asset 128 t + k (ABSENT past N)
+    pt = Pt.cpu().numpy().reshape(-1, T_d, 128)
+    for t in range(pt.shape[0]):
+        w = min(128, N - 128 * t)
+        assert bits_equal(pt[t, :, :w], P[:, 128 * t:128 * t + w])
+        assert O.is_absent(pt[t, :, w:]).all()
+    try:
+        for knob, vals in ((b"signal_mw", (21, 22, 41, 42)), (b"signal_bw", (2, 4)),
+                           (b"signal_store", (1,))):
+            for v in vals:
+                assert lib.csm_tune(knob, v) == 0
+                check(engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True),
+                      f"{knob}={v}")
+                lib.csm_tune(knob, 0 if knob != b"signal_bw" else 1)
+        assert lib.csm_tune(b"month_end_rows", maxd) == 0
+        PM, _ = engine.month_end(Pd, ms)
+        assert bits_equal(PM.cpu().numpy(), base[0].cpu().numpy())
+    finally:
+        for knob, v in ((b"signal_mw", 0), (b"signal_bw", 1), (b"signal_store", 0),
+                        (b"month_end_rows", 0)):
+            lib.csm_tune(knob, v)
 
 
 def test_fused_rejects_long_months(engine):
