@@ -1,0 +1,60 @@
+// csm_common.h -- shared by the engine's translation units: the NaN-payload presence
+// encoding, the context object and the status/error plumbing of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/csmom.h"
+
+#define ABSENT_BITS 0x7FF4000000000001ULL
+#define ABSENT_MASK 0x7FF7FFFFFFFFFFFFULL
+
+__device__ __forceinline__ bool is_absent(double x) {
+  return (((uint64_t)__double_as_longlong(x)) & ABSENT_MASK) == ABSENT_BITS;
+}
+__device__ __forceinline__ double absent_val() { return __longlong_as_double((long long)ABSENT_BITS); }
+__device__ __forceinline__ double qnan() { return __longlong_as_double(0x7FF8000000000000LL); }
+__device__ __forceinline__ bool isnan_d(double x) { return x != x; }
+
+
+struct csm_ctx {
+  int device;
+  hipStream_t stream;
+  char err[512];
+};
+
+static inline int set_err(csm_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(c->err, sizeof(c->err), fmt, ap);
+    va_end(ap);
+  }
+  return code;
+}
+
+#define HIP_CHECK(ctx, call)                                                               \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return set_err(ctx, CSM_E_HIP, "%s: %s", #call, hipGetErrorString(e_));              \
+  } while (0)
+
+#define LAUNCH_CHECK(ctx, name)                                                            \
+  do {                                                                                     \
+    hipError_t e_ = hipGetLastError();                                                     \
+    if (e_ != hipSuccess) return set_err(ctx, CSM_E_HIP, "%s launch: %s", name, hipGetErrorString(e_)); \
+  } while (0)
+
+static inline int prep(csm_ctx* c) {
+  if (!c) return CSM_E_INVAL;
+  c->err[0] = 0;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  return CSM_OK;
+}
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

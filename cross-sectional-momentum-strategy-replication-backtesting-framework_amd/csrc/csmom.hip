@@ -20,17 +20,8 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "../../include/csmom.h"
 
-#define ABSENT_BITS 0x7FF4000000000001ULL
-#define ABSENT_MASK 0x7FF7FFFFFFFFFFFFULL
-
-__device__ __forceinline__ bool is_absent(double x) {
-  return (((uint64_t)__double_as_longlong(x)) & ABSENT_MASK) == ABSENT_BITS;
-}
-__device__ __forceinline__ double absent_val() { return __longlong_as_double((long long)ABSENT_BITS); }
-__device__ __forceinline__ double qnan() { return __longlong_as_double(0x7FF8000000000000LL); }
-__device__ __forceinline__ bool isnan_d(double x) { return x != x; }
+#include "csm_common.h"
 
 // =====================================================================================
 // Kernel A: month-end aggregation.  One thread per (month, VEC assets); a wave streams
@@ -1474,44 +1465,6 @@ static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<..,
 static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
 static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
 static int g_tune_month_end_rows = 0;  // >0: csm_month_end uses k_month_end_rows (value = max month days)
-
-struct csm_ctx {
-  int device;
-  hipStream_t stream;
-  char err[512];
-};
-
-static int set_err(csm_ctx* c, int code, const char* fmt, ...) {
-  if (c) {
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(c->err, sizeof(c->err), fmt, ap);
-    va_end(ap);
-  }
-  return code;
-}
-
-#define HIP_CHECK(ctx, call)                                                               \
-  do {                                                                                     \
-    hipError_t e_ = (call);                                                                \
-    if (e_ != hipSuccess)                                                                  \
-      return set_err(ctx, CSM_E_HIP, "%s: %s", #call, hipGetErrorString(e_));              \
-  } while (0)
-
-#define LAUNCH_CHECK(ctx, name)                                                            \
-  do {                                                                                     \
-    hipError_t e_ = hipGetLastError();                                                     \
-    if (e_ != hipSuccess) return set_err(ctx, CSM_E_HIP, "%s launch: %s", name, hipGetErrorString(e_)); \
-  } while (0)
-
-static int prep(csm_ctx* c) {
-  if (!c) return CSM_E_INVAL;
-  c->err[0] = 0;
-  HIP_CHECK(c, hipSetDevice(c->device));
-  return CSM_OK;
-}
-
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 extern "C" {
 

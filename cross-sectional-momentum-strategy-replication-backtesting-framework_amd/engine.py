@@ -72,6 +72,15 @@ class PipelineOut:
     NV: torch.Tensor | None = None
 
 
+@dataclass
+class PortfolioOut:
+    PR: torch.Tensor                 # [T_m][B][n_bins] overlapped decile returns
+    LS: torch.Tensor                 # [T_m][B] long-short (NaN = dropped month)
+    TURN: torch.Tensor | None = None  # [T_m][B] long-short turnover
+    COST: torch.Tensor | None = None  # [T_m][B] transaction cost
+    NET: torch.Tensor | None = None   # [T_m][B] LS - COST
+
+
 class Engine:
     """Signal (J, skip) -> per-date n_bins labels -> equal-weight long-short, on one GPU."""
 
@@ -256,6 +265,50 @@ class Engine:
         LS = self.empty((T_m,)) if LS is None else LS
         self._call("csm_long_short", _ptr(EW), _ptr(CNT), T_m, nb, _ptr(LS))
         return LS
+
+    def portfolio(self, L, NR, n_bins=10, K=1, W=None, B=1, half_spread=0.0005, k_impact=0.1,
+                  aum=0.0, ADV=None, SIG=None, with_costs=True, out=None, workspace=None):
+        """csm_portfolio: K-overlapping cohorts, equal (W None) or value weights, long-short
+        turnover and costs (rules E1..E5).  L/NR/W/ADV/SIG are [T_m][B*N] (B panels side by
+        side, the sweep layout) or [T_m][N] with B = 1.  Returns a PortfolioOut."""
+        T_m, BN = L.shape
+        if B < 1 or BN % B:
+            raise ValueError(f"row width {BN} is not B={B} panels")
+        N = BN // B
+        _need(L, "L", torch.int8, (T_m, BN), self.device)
+        _need(NR, "NR", torch.float64, (T_m, BN), self.device)
+        for t, nm in ((W, "W"), (ADV, "ADV"), (SIG, "SIG")):
+            if t is not None:
+                _need(t, nm, torch.float64, (T_m, BN), self.device)
+        if out is None:
+            PR = self.empty((T_m, B, n_bins))
+            LS = self.empty((T_m, B))
+            TURN = self.empty((T_m, B)) if with_costs else None
+            COST = self.empty((T_m, B)) if with_costs else None
+            NET = self.empty((T_m, B)) if with_costs else None
+        else:
+            PR, LS, TURN, COST, NET = out
+        nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, int(n_bins), int(K)))
+        if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
+            workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
+        self._call("csm_portfolio", _ptr(L), _ptr(NR), _ptr(W), T_m, int(B), N, int(n_bins),
+                   int(K), float(half_spread), float(k_impact), float(aum), _ptr(ADV), _ptr(SIG),
+                   _ptr(PR), _ptr(LS), _ptr(TURN), _ptr(COST), _ptr(NET), _ptr(workspace))
+        return PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET)
+
+    def bootstrap(self, R, B, b0=0, seed=5000, mean_block=6.0, p0=100.0, out=None):
+        """csm_bootstrap: B stationary-bootstrap month panels of the base month-return panel
+        R[T_m][N] (rule E6) -> (src [B][T_m] int32, PMb [T_m][B*N] month prices)."""
+        T_m, N = R.shape
+        _need(R, "R", torch.float64, (T_m, N), self.device)
+        if out is None:
+            src = self.empty((B, T_m), torch.int32)
+            PMb = self.empty((T_m, B * N))
+        else:
+            src, PMb = out
+        self._call("csm_bootstrap", _ptr(R), T_m, N, int(B), int(b0), ctypes.c_uint64(int(seed)),
+                   float(mean_block), float(p0), _ptr(src), _ptr(PMb))
+        return src, PMb
 
     def shard_summary(self, PM, J, skip, out=None):
         T_m, N = PM.shape

@@ -169,6 +169,38 @@ int csm_shard_summary(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, in
 int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, int64_t N,
                    int32_t J, int32_t skip, double* carry, double* next_pm);
 
+/*
+ * Portfolio accounting beyond the reference's K = 1 equal-weight case (SURVEY 8(f) rank 2;
+ * rules E1..E5 in DESIGN.md section 8 / oracle/portfolio_oracle.py).  The reference counterpart
+ * is run_demo.py:49-67 (K = 1, equal weight, no costs), which this collapses to.
+ * Panels are batched [T_m][B][N] (B cross-sections per month row; B = 1 for one panel).
+ *   L         int8 labels from csm_deciles (-1 = not ranked)
+ *   NR        next-row returns (the return held over (t, t+1])
+ *   W         nullable: formation weights (value weighting, e.g. market cap); NULL = equal
+ *   K         holding months: month t averages the cohorts formed at t-K+1 .. t
+ *   half_spread, k_impact, aum, ADV (nullable [T_m][B][N] dollar ADV), SIG (nullable
+ *             volatility, NaN/NULL -> 0.02): the cost model of src/execution_models.py:4-12
+ *   PR [T_m][B][n_bins]  overlapped decile returns;  LS [T_m][B] long-short (NaN = dropped)
+ *   TURN, COST, NET [T_m][B] nullable: long-short turnover (1/2 sum |dw|), cost, LS - COST
+ *   workspace: device buffer of csm_portfolio_workspace(T_m, B, n_bins, K) bytes
+ * n_bins in {2,3,4,5,10,20}.
+ */
+int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int32_t n_bins, int32_t K);
+int csm_portfolio(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
+                  int32_t B, int64_t N, int32_t n_bins, int32_t K, double half_spread,
+                  double k_impact, double aum, const double* ADV, const double* SIG, double* PR,
+                  double* LS, double* TURN, double* COST, double* NET, void* workspace);
+
+/*
+ * Stationary month bootstrap (BASELINE config C5; rule E6): panels b0 .. b0+B-1 of the base
+ * month-return panel R[T_m][N] (csm_momentum's R; NaN = no row).  src[B][T_m] int32 out: the
+ * source months; PMb[T_m][B][N] out: month prices p0 * prod(1 + r) over the resampled months,
+ * ABSENT where the source return is NaN.  The random stream is splitmix64 keyed by
+ * (seed, panel, month), so panel b is the same on every device and shard.
+ */
+int csm_bootstrap(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t B, int64_t b0,
+                  uint64_t seed, double mean_block, double p0, int32_t* src, double* PMb);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,143 @@
+"""GPU: csm_portfolio (K-overlap, value weights, turnover, costs) and csm_bootstrap against the
+portfolio oracle (rules E1..E6).  Bar: the bootstrap's source months and month prices are
+bit-exact (integer hashing, sequential fp64 products); portfolio returns, turnover and costs
+agree within 1e-10 relative (fp64 sums in a different order)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits_equal, load_golden, max_rel
+from oracle import csmom_oracle as O
+from oracle import portfolio_oracle as PO
+
+pytestmark = pytest.mark.gpu
+REL = 1e-10
+
+
+def _up(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
+
+
+def _labels(engine, name, J=12, skip=1):
+    z = load_golden(name)
+    P = z["P"]
+    ms = z["month_start"].astype(np.int64)
+    PM, _ = engine.month_end(_up(P), _up(ms))
+    R, M, NR = engine.momentum(PM, J, skip, with_ret=True)
+    L, _, _, _ = engine.deciles(M, None, 10)
+    return L, NR, R, PM
+
+
+def _close(got, ref, what, rel=REL):
+    g = got.cpu().numpy() if isinstance(got, torch.Tensor) else got
+    assert np.array_equal(np.isnan(g), np.isnan(ref)), what
+    m = ~np.isnan(ref)
+    scale = np.maximum(np.abs(ref[m]), 1e-12)
+    assert (np.abs(g[m] - ref[m]) <= rel * scale + 1e-15).all(), (what, max_rel(g, ref))
+
+
+@pytest.mark.parametrize("K", [1, 3, 6, 12])
+@pytest.mark.parametrize("vw", [False, True])
+def test_portfolio_vs_oracle(engine, K, vw):
+    L, NR, _, PM = _labels(engine, "c1")
+    Lh, NRh = L.cpu().numpy(), NR.cpu().numpy()
+    rng = np.random.default_rng(K * 10 + vw)
+    T_m, N = Lh.shape
+    W = None
+    if vw:
+        W = np.abs(PM.cpu().numpy()) * rng.uniform(1e5, 1e7, N)   # price x shares
+        W[rng.random(W.shape) < 0.01] = np.nan
+    ADV = rng.uniform(1e5, 1e8, (T_m, N))
+    SIG = rng.uniform(0.005, 0.05, (T_m, N))
+    SIG[rng.random(SIG.shape) < 0.02] = np.nan
+    ref = PO.portfolio(Lh, NRh, 10, K=K, W=W, aum=5e6, ADV=ADV, SIG=SIG)
+    out = engine.portfolio(L, NR, 10, K=K, W=None if W is None else _up(W), aum=5e6,
+                           ADV=_up(ADV), SIG=_up(SIG))
+    _close(out.PR, ref["PR"], "PR")
+    _close(out.LS, ref["LS"], "LS")
+    _close(out.TURN, ref["TURN"], "TURN")
+    _close(out.COST, ref["COST"], "COST")
+    _close(out.NET, ref["NET"], "NET")
+
+
+def test_portfolio_k1_equal_weight_is_reference_path(engine):
+    """K = 1, equal weight, no costs: the same numbers as the fused decile means (the
+    reference's run_demo.py:49-67 path) and the golden fixture."""
+    z = load_golden("c1")
+    L, NR, _, _ = _labels(engine, "c1")
+    _, EW, CNT, _ = engine.deciles(*_mom(engine, "c1"), 10)
+    out = engine.portfolio(L, NR, 10, K=1, with_costs=False)
+    _close(out.PR[:, 0, :], z["J12s1_EW"], "PR vs fixture")
+    _close(out.LS[:, 0], z["J12s1_LS"], "LS vs fixture")
+    _close(out.PR[:, 0, :], EW.cpu().numpy(), "PR vs k_deciles EW")
+
+
+def _mom(engine, name):
+    z = load_golden(name)
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    _, M, NR = engine.momentum(PM, 12, 1)
+    return M, NR
+
+
+def test_portfolio_batched_panels(engine):
+    L, NR, _, _ = _labels(engine, "c1")
+    Lh, NRh = L.cpu().numpy(), NR.cpu().numpy()
+    perm = np.random.default_rng(3).permutation(Lh.shape[1])
+    L3 = np.stack([Lh, Lh[:, perm], Lh[:, ::-1]], axis=1)
+    NR3 = np.stack([NRh, NRh[:, perm], NRh[:, ::-1]], axis=1)
+    T_m, B, N = L3.shape
+    ref = PO.portfolio(L3, NR3, 10, K=6)
+    out = engine.portfolio(_up(L3.reshape(T_m, B * N)), _up(NR3.reshape(T_m, B * N)), 10, K=6,
+                           B=B)
+    _close(out.PR, ref["PR"], "PR")
+    _close(out.TURN, ref["TURN"], "TURN")
+    _close(out.NET, ref["NET"], "NET")
+    # every panel is a permutation of the same cross-sections: identical returns
+    pr = out.PR.cpu().numpy()
+    assert max_rel(pr[:, 1], pr[:, 0]) <= 1e-12 and max_rel(pr[:, 2], pr[:, 0]) <= 1e-12
+
+
+def test_portfolio_rejects_bad_args(engine):
+    import csmom
+    L, NR, _, _ = _labels(engine, "c1")
+    with pytest.raises(csmom.CsmError):
+        engine.portfolio(L, NR, 7, K=1)          # unsupported n_bins
+    with pytest.raises(ValueError):
+        engine.portfolio(L, NR, 10, K=1, B=7)    # row width not a multiple of B
+
+
+@pytest.mark.parametrize("B,b0", [(5, 0), (3, 17)])
+def test_bootstrap_bit_exact(engine, B, b0):
+    _, _, R, _ = _labels(engine, "c1")
+    Rh = R.cpu().numpy()
+    T_m, N = Rh.shape
+    src, PMb = engine.bootstrap(R, B, b0=b0, seed=5000, mean_block=6.0)
+    ref_src = PO.bootstrap_indices(T_m, B, 5000, 6.0, b0=b0)
+    assert np.array_equal(src.cpu().numpy().astype(np.int64), ref_src)
+    ref = PO.bootstrap_panel(Rh, ref_src)
+    got = PMb.cpu().numpy().reshape(T_m, B, N)
+    assert (O.is_absent(got) == O.is_absent(ref)).all()
+    assert bits_equal(got, ref)
+
+
+def test_bootstrap_sweep_end_to_end(engine):
+    """C5 in miniature: bootstrap panels -> scan -> deciles -> K-overlap portfolios with costs,
+    all batched as [T_m][B*N], against the oracle stage by stage."""
+    _, _, R, _ = _labels(engine, "c1")
+    Rh = R.cpu().numpy()
+    T_m, N = Rh.shape
+    B = 4
+    src, PMb = engine.bootstrap(R, B, b0=100, seed=5000, mean_block=6.0)
+    pm_ref = PO.bootstrap_panel(Rh, PO.bootstrap_indices(T_m, B, 5000, 6.0, b0=100))
+    for J, K in ((3, 1), (12, 6)):
+        _, M, NR = engine.momentum(PMb, J, 1)
+        L, _, _, _ = engine.deciles(M.view(T_m * B, N), None, 10)
+        L = L.view(T_m, B * N)
+        out = engine.portfolio(L, NR, 10, K=K, B=B)
+        _, Mr, NRr, _ = O.momentum_scan(pm_ref.reshape(T_m, B * N), J, 1)
+        assert bits_equal(M.cpu().numpy(), Mr) and bits_equal(NR.cpu().numpy(), NRr)
+        Lr = O.assign_deciles(Mr.reshape(T_m * B, N), 10).reshape(T_m, B, N)
+        assert np.array_equal(L.cpu().numpy().reshape(T_m, B, N), Lr)
+        ref = PO.portfolio(Lr, NRr.reshape(T_m, B, N), 10, K=K)
+        _close(out.PR, ref["PR"], f"PR J{J}K{K}")
+        _close(out.NET, ref["NET"], f"NET J{J}K{K}")
