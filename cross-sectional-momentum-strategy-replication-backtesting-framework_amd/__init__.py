@@ -10,17 +10,22 @@ a Python identifier).  Public API (reference file:line it replaces):
   monthly_replication                   run_demo.py:31-79          (GPU + host summary)
   sharpe / ensure_dir / save_plot       src/utils.py:5-21          (host)
   Engine                                dense device pipeline (bench / multi-GPU)
+  Engine.portfolio / Engine.bootstrap   K-overlap, value weights, turnover, costs, bootstrap
+                                        (beyond run_demo.py:49-67)
+  SweepRunner                           (J, K) grids over panels / bootstrap panels (C3, C5)
 """
 from ._lib import ABSENT_BITS, CsmError, CsmUnavailable, lib_path, load_library
-from .engine import Engine, PipelineOut, absent_tensor, is_absent, quantile_table
+from .engine import Engine, PipelineOut, PortfolioOut, absent_tensor, is_absent, quantile_table
 from .features import compute_monthly_momentum_from_daily, compute_monthly_turnover, get_engine
 from .panel import DensePanel, from_long, month_offsets, monthly_frame
 from .replication import ReplicationResult, assign_deciles_per_date, monthly_replication
+from .sweep import SUMMARY_FIELDS, SweepConfig, SweepRunner, strategy_grid
 from .utils import ensure_dir, save_plot, sharpe
 
 __all__ = [
     "ABSENT_BITS", "CsmError", "CsmUnavailable", "lib_path", "load_library", "Engine",
-    "PipelineOut", "absent_tensor", "is_absent", "quantile_table",
+    "PipelineOut", "PortfolioOut", "SweepConfig", "SweepRunner", "SUMMARY_FIELDS",
+    "strategy_grid", "absent_tensor", "is_absent", "quantile_table",
     "compute_monthly_momentum_from_daily", "compute_monthly_turnover", "get_engine",
     "DensePanel", "from_long", "month_offsets", "monthly_frame", "ReplicationResult",
     "assign_deciles_per_date", "monthly_replication", "ensure_dir", "save_plot", "sharpe",

@@ -1,0 +1,148 @@
+"""(J, K) strategy sweeps and bootstrap panels (BASELINE configs C3 and C5).
+
+The reference runs one strategy (J = 12, skip = 1, K = 1, equal weight) per call of
+`monthly_replication` (run_demo.py:31-79).  A sweep runs a grid of strategies over one or many
+panels with the month-end aggregation done once per panel:
+
+  * per J: one scan of the month panel (ret_1m / mom_J / next_ret, features.py:44-52,
+    run_demo.py:48) and one qcut pass (run_demo.py:18-29) -- all B panels of a batch at once,
+    laid out side by side as [T_m][B*N] (the scan is per asset; the labels are per (month,
+    panel) row of N assets);
+  * per (J, K): one csm_portfolio pass (K-overlap cohorts, equal or value weights, turnover,
+    spread + square-root-impact costs; rules E1..E5);
+  * per (J, K, panel): a summary row (months, mean and Sharpe of the long-short as in
+    src/utils.py:8-16 at 12 periods a year, mean turnover, mean cost, mean / Sharpe of net).
+
+Multi-GPU: sweep units are independent, so panels are split across ranks in contiguous
+ranges (a panel's bootstrap stream is keyed by its global id, never by the rank) and the only
+collective is one all-gather of the summary table at the end.  The stage implementation is
+injected (`Engine` on the GPU; the CPU tests drive the same orchestration with gloo and an
+oracle-backed adapter).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from .distributed import all_gather_stack
+
+SUMMARY_FIELDS = ("months", "mean", "sharpe", "turnover", "cost", "net_mean", "net_sharpe")
+
+
+def strategy_grid(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12)):
+    return [(int(J), int(K)) for J in Js for K in Ks]
+
+
+def panel_partition(n_panels: int, G: int):
+    """Contiguous panel ranges per rank (earlier ranks take the remainder)."""
+    base, rem = divmod(n_panels, G)
+    out, p0 = [], 0
+    for g in range(G):
+        p1 = p0 + base + (1 if g < rem else 0)
+        out.append((p0, p1))
+        p0 = p1
+    return out
+
+
+def summarize(LS: torch.Tensor, TURN, COST, NET, freq: int = 12) -> torch.Tensor:
+    """Per-panel summary rows [B][len(SUMMARY_FIELDS)] from [T_m][B] series; NaN months are
+    dropped (run_demo.py:67) and the Sharpe ratio is src/utils.py:8-16's."""
+    def stats(x):
+        ok = ~torch.isnan(x)
+        n = ok.sum(0).to(x.dtype)
+        xs = torch.where(ok, x, torch.zeros_like(x))
+        mean = xs.sum(0) / n
+        dev = torch.where(ok, x - mean, torch.zeros_like(x))
+        var = (dev * dev).sum(0) / (n - 1)
+        sd = torch.sqrt(var)
+        sh = torch.where(sd > 0, mean * freq / (sd * freq ** 0.5), torch.full_like(sd, float("nan")))
+        return n, mean, sh
+    n, mean, sh = stats(LS)
+    ok = ~torch.isnan(LS)
+    zero = torch.zeros_like(LS)
+    if TURN is not None:
+        turn = torch.where(ok, TURN, zero).sum(0) / n
+        cost = torch.where(ok, COST, zero).sum(0) / n
+        _, nmean, nsh = stats(NET)
+    else:
+        turn = cost = nmean = nsh = torch.full_like(mean, float("nan"))
+    return torch.stack([n, mean, sh, turn, cost, nmean, nsh], dim=1)
+
+
+@dataclass
+class SweepConfig:
+    Js: tuple = (3, 6, 9, 12)
+    Ks: tuple = (3, 6, 9, 12)
+    skip: int = 1
+    n_bins: int = 10
+    half_spread: float = 0.0005
+    k_impact: float = 0.1
+    aum: float = 0.0
+    costs: bool = True
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def strategies(self):
+        return strategy_grid(self.Js, self.Ks)
+
+
+class SweepRunner:
+    """Runs the (J, K) grid on batches of month panels.
+
+    stages: object with `momentum`, `deciles`, `portfolio`, `bootstrap` (Engine signatures).
+    """
+
+    def __init__(self, stages, cfg: SweepConfig | None = None, group=None):
+        self.st = stages
+        self.cfg = cfg or SweepConfig()
+        self.group = group
+        self.G = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+
+    def run_batch(self, PMb: torch.Tensor, B: int, W=None, ADV=None, SIG=None):
+        """PMb [T_m][B*N] month prices of B panels -> summary [B][S][F] and the per-strategy
+        long-short series {(J, K): PortfolioOut}."""
+        c, st = self.cfg, self.st
+        T_m, BN = PMb.shape
+        N = BN // B
+        rows, series = [], {}
+        by_j = {}
+        for J in c.Js:
+            _, M, NR = st.momentum(PMb, J, c.skip)
+            L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
+            by_j[J] = (L.reshape(T_m, BN), NR)
+        for (J, K) in c.strategies:
+            L, NR = by_j[J]
+            out = st.portfolio(L, NR, c.n_bins, K=K, W=W, B=B, half_spread=c.half_spread,
+                               k_impact=c.k_impact, aum=c.aum, ADV=ADV, SIG=SIG,
+                               with_costs=c.costs)
+            series[(J, K)] = out
+            rows.append(summarize(out.LS, out.TURN, out.COST, out.NET))
+        return torch.stack(rows, dim=1), series                  # [B][S][F]
+
+    def run_bootstrap(self, R_base: torch.Tensor, n_panels: int, seed: int = 5000,
+                      mean_block: float = 6.0, batch: int = 64):
+        """C5: n_panels stationary-bootstrap panels of the base month returns, this rank's
+        contiguous share in batches; one all-gather of the summary table.  Returns the full
+        [n_panels][S][F] table on every rank."""
+        T_m, N = R_base.shape
+        p0, p1 = panel_partition(n_panels, self.G)[self.rank]
+        S, F = len(self.cfg.strategies), len(SUMMARY_FIELDS)
+        mine = []
+        for b0 in range(p0, p1, batch):
+            B = min(batch, p1 - b0)
+            _, PMb = self.st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
+            summ, _ = self.run_batch(PMb, B)
+            mine.append(summ)
+        local = (torch.cat(mine, 0) if mine else
+                 torch.empty((0, S, F), dtype=R_base.dtype, device=R_base.device))
+        if self.G == 1:
+            return local
+        width = max(b - a for a, b in panel_partition(n_panels, self.G))
+        pad = torch.full((width, S, F), float("nan"), dtype=local.dtype, device=local.device)
+        pad[:local.shape[0]] = local
+        allp = all_gather_stack(pad, self.group)                   # the one collective
+        parts = panel_partition(n_panels, self.G)
+        return torch.cat([allp[g, :b - a] for g, (a, b) in enumerate(parts)], 0)

@@ -141,3 +141,20 @@ def test_bootstrap_sweep_end_to_end(engine):
         ref = PO.portfolio(Lr, NRr.reshape(T_m, B, N), 10, K=K)
         _close(out.PR, ref["PR"], f"PR J{J}K{K}")
         _close(out.NET, ref["NET"], f"NET J{J}K{K}")
+
+
+def test_sweep_runner_gpu_vs_oracle(engine):
+    """SweepRunner on the Engine (bootstrap -> scan -> qcut -> portfolios, batched) against
+    the same orchestration on the oracle stages."""
+    import csmom
+    from test_sweep_gloo import OracleSweepStages
+    _, _, R, _ = _labels(engine, "c1")
+    cfg = csmom.SweepConfig(Js=(3, 12), Ks=(1, 6), skip=1)
+    got = csmom.SweepRunner(engine, cfg).run_bootstrap(R, 5, seed=5000, mean_block=6.0,
+                                                       batch=3).cpu().numpy()
+    ref = csmom.SweepRunner(OracleSweepStages(), cfg).run_bootstrap(
+        R.cpu(), 5, seed=5000, mean_block=6.0, batch=5).numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(got[..., 0], ref[..., 0])
+    m = ~np.isnan(ref)
+    assert np.allclose(got[m], ref[m], rtol=1e-9, atol=1e-13)
