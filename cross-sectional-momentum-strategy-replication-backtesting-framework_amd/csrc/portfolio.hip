@@ -1,14 +1,21 @@
 // portfolio.hip -- portfolio accounting beyond the reference's K = 1 equal-weight case
 // (rules E1..E6 in oracle/portfolio_oracle.py and DESIGN.md 8).
 //
-//   k_cohort       one workgroup per (holding month t, panel b, cohort age k): decile sums of
-//                  w * next_ret and w over the members of the cohort formed at t - k whose
-//                  next_ret[t] is valid (E1), plus the formation totals of the two legs (k = 0)
-//   k_turnover     one workgroup per (t, b): aggregate leg weights of the K overlapping
-//                  cohorts at t and t - 1, |dw| summed into turnover and into the spread +
-//                  square-root-impact cost of src/execution_models.py:4-12 (E4, E5)
-//   k_overlap_ls   one workgroup per panel: cohort means -> overlapped decile returns (E2),
-//                  the reference's long-short rule (run_demo.py:60-67) per panel (E3), net
+//   k_cohort       one workgroup per (asset chunk c, holding month t, panel b[, cohort k]):
+//                  decile partial sums of w * next_ret and w over the chunk's members of the
+//                  cohort formed at t - k whose next_ret[t] is valid (E1), plus the chunk's
+//                  formation totals of the two legs (k = 0)
+//   k_turnover     one workgroup per (asset chunk, t, b): aggregate leg weights of the K
+//                  overlapping cohorts at t and t - 1, |dw| summed into turnover and into the
+//                  spread + square-root-impact cost of src/execution_models.py:4-12 (E4, E5)
+//   k_overlap      one workgroup per (t, b): chunk partials summed in chunk order, cohort
+//                  means -> overlapped decile returns (E2), turnover / cost totals
+//   k_ls           one workgroup per panel: the reference's long-short rule
+//                  (run_demo.py:60-67) per panel (E3), net = long-short - cost
+//
+// Chunking: narrow panels (few (t, b) rows) split each row over asset chunks, and wide ones
+// run one chunk, so every launch has thousands of workgroups; partial sums go to a workspace
+// and are combined in a fixed order.
 //   k_bootstrap_*  stationary month bootstrap with a counter-based splitmix64 stream (E6)
 //
 // Panels are batched as [T_m][B][N] rows (B cross-sections per month), the sweep layout.
@@ -19,7 +26,8 @@
 
 #define PF_THREADS 256
 #define PF_WAVES (PF_THREADS / 64)
-#define PF_MAXB 20
+#define PF_CHUNK_MIN 256     // assets per chunk, at least one per thread
+#define TO_MAXK 240
 
 __device__ __forceinline__ double wave_sum(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -39,113 +47,128 @@ __device__ __forceinline__ double member_w(int lab, int d, const double* W, int6
 }
 
 // -------------------------------------------------------------------------------- E1
-template <int NB>
+// Cohort sums do not depend on the holding period: a pass with Kmax cohorts serves every
+// K <= Kmax (the sweep runs one pass per J for all its K).  Per-lane decile accumulators
+// live in registers (predicated adds; SW > 0 doubles as "the cohort has a valid member",
+// weights being > 0, so no count is kept).
+template <int NB, bool VW>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort(
     const int8_t* __restrict__ L, const double* __restrict__ NR, const double* __restrict__ W,
-    int T_m, int B, int64_t N, int K, double* __restrict__ SWR, double* __restrict__ SW,
-    int32_t* __restrict__ CNT, double* __restrict__ FW) {
-  const int k = blockIdx.x;
-  const int tb = blockIdx.y;           // t * B + b
+    int T_m, int B, int64_t N, int K, int C, int64_t CH, int kpar, double* __restrict__ SWRp,
+    double* __restrict__ SWp, double* __restrict__ FWp) {
+  __shared__ double red[PF_WAVES][2 * NB + 2];
+  const int c = blockIdx.x;
+  const int tb = blockIdx.y;
   const int t = tb / B, b = tb - t * B;
-  const int s = t - k;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t obase = ((int64_t)tb * K + k) * NB;
-  if (s < 0) {
-    if (tid < NB) { SWR[obase + tid] = 0.0; SW[obase + tid] = 0.0; CNT[obase + tid] = 0; }
-    return;
-  }
-  const int64_t rs = ((int64_t)s * B + b) * N;   // formation row
-  const int64_t rt = ((int64_t)t * B + b) * N;   // holding row
-  double swr[NB], sw[NB];
-  int cn[NB];
+  const int64_t a0 = (int64_t)c * CH;
+  const int64_t a1 = a0 + CH < N ? a0 + CH : N;
+  const int64_t rt = ((int64_t)t * B + b) * N;
+  const int k_lo = kpar ? (int)blockIdx.z : 0, k_hi = kpar ? k_lo + 1 : K;
+  for (int k = k_lo; k < k_hi; ++k) {
+    const int s = t - k;
+    const int64_t ob = (((int64_t)tb * K + k) * C + c) * NB;
+    if (s < 0) {
+      if (tid < NB) { SWRp[ob + tid] = 0.0; SWp[ob + tid] = 0.0; }
+      continue;
+    }
+    const int64_t rs = ((int64_t)s * B + b) * N;
+    double swr[NB], sw[NB];
 #pragma unroll
-  for (int d = 0; d < NB; ++d) { swr[d] = 0.0; sw[d] = 0.0; cn[d] = 0; }
-  double ft = 0.0, fb = 0.0;  // formation totals of the top / bottom legs (k == 0 only)
-  for (int64_t i = tid; i < N; i += PF_THREADS) {
-    const int lab = L[rs + i];
-    if (lab < 0) continue;
-    const double r = NR[rt + i];
-    double w = 1.0;
-    if (W) {
-      w = W[rs + i];
-      if (!(w > 0.0 && w < INFINITY)) continue;
+    for (int d = 0; d < NB; ++d) { swr[d] = 0.0; sw[d] = 0.0; }
+    double ft = 0.0, fb = 0.0;
+    for (int64_t i = a0 + tid; i < a1; i += PF_THREADS) {
+      const int lab = L[rs + i];
+      const double r = NR[rt + i];
+      double w = 1.0;
+      if (VW) {
+        const double x = W[rs + i];
+        w = (x > 0.0 && x < INFINITY) ? x : 0.0;   // invalid weight: not a member
+      }
+      if (k == 0) {
+        ft += lab == NB - 1 ? w : 0.0;
+        fb += lab == 0 ? w : 0.0;
+      }
+      const bool ok = r == r;
+      const double wr = ok ? (VW ? w * r : r) : 0.0;
+      const double wv = ok ? w : 0.0;
+#pragma unroll
+      for (int d = 0; d < NB; ++d) {
+        const bool h = lab == d;
+        swr[d] += h ? wr : 0.0;
+        sw[d] += h ? wv : 0.0;
+      }
     }
-    if (k == 0) {
-      ft += lab == NB - 1 ? w : 0.0;
-      fb += lab == 0 ? w : 0.0;
-    }
-    if (r != r) continue;
 #pragma unroll
     for (int d = 0; d < NB; ++d) {
-      const bool h = lab == d;
-      swr[d] += h ? w * r : 0.0;
-      sw[d] += h ? w : 0.0;
-      cn[d] += h ? 1 : 0;
+      const double x = wave_sum(swr[d]), y = wave_sum(sw[d]);
+      if (lane == 0) { red[wid][d] = x; red[wid][NB + d] = y; }
     }
-  }
-  __shared__ double red[PF_WAVES][2 * NB + 2];
-  __shared__ int redc[PF_WAVES][NB];
-#pragma unroll
-  for (int d = 0; d < NB; ++d) {
-    const double a = wave_sum(swr[d]), c = wave_sum(sw[d]);
-    const int n = wave_sumi(cn[d]);
-    if (lane == 0) { red[wid][d] = a; red[wid][NB + d] = c; redc[wid][d] = n; }
-  }
-  if (k == 0) {
-    const double a = wave_sum(ft), c = wave_sum(fb);
-    if (lane == 0) { red[wid][2 * NB] = a; red[wid][2 * NB + 1] = c; }
-  }
-  __syncthreads();
-  if (tid < NB) {
-    double a = 0.0, c = 0.0;
-    int n = 0;
-    for (int w2 = 0; w2 < PF_WAVES; ++w2) { a += red[w2][tid]; c += red[w2][NB + tid]; n += redc[w2][tid]; }
-    SWR[obase + tid] = a;
-    SW[obase + tid] = c;
-    CNT[obase + tid] = n;
-  }
-  if (k == 0 && tid < 2) {
-    double a = 0.0;
-    for (int w2 = 0; w2 < PF_WAVES; ++w2) a += red[w2][2 * NB + tid];
-    FW[(int64_t)tb * 2 + tid] = a;   // [t][b][leg]: leg 0 = top, 1 = bottom
+    if (k == 0) {
+      const double x = wave_sum(ft), y = wave_sum(fb);
+      if (lane == 0) { red[wid][2 * NB] = x; red[wid][2 * NB + 1] = y; }
+    }
+    __syncthreads();
+    if (tid < NB) {
+      double x = 0.0, y = 0.0;
+      for (int w2 = 0; w2 < PF_WAVES; ++w2) { x += red[w2][tid]; y += red[w2][NB + tid]; }
+      SWRp[ob + tid] = x;
+      SWp[ob + tid] = y;
+    }
+    if (k == 0 && tid < 2) {
+      double x = 0.0;
+      for (int w2 = 0; w2 < PF_WAVES; ++w2) x += red[w2][2 * NB + tid];
+      FWp[((int64_t)tb * C + c) * 2 + tid] = x;   // leg 0 = top, 1 = bottom
+    }
+    __syncthreads();  // red is reused by the next cohort
   }
 }
 
 // ------------------------------------------------------------------------------ E4, E5
-// Aggregate weight of asset a in leg (label d, totals index li) at month u (over the K
-// cohorts u-K+1..u); returns 0 when no cohort is non-empty.
-__device__ __forceinline__ double leg_weight(const int8_t* __restrict__ L,
-                                             const double* __restrict__ W,
-                                             const double* __restrict__ FW, int u, int B, int b,
-                                             int64_t N, int64_t a, int K, int d, int li) {
-  if (u < 0) return 0.0;
-  double acc = 0.0;
-  int kt = 0;
-  for (int k = 0; k < K; ++k) {
-    const int s = u - k;
-    if (s < 0) break;
-    const double tot = FW[((int64_t)s * B + b) * 2 + li];
-    if (!(tot > 0.0)) continue;
-    ++kt;
-    const int64_t o = ((int64_t)s * B + b) * N + a;
-    const double w = member_w(L[o], d, W, o);
-    acc += w / tot;
-  }
-  return kt > 0 ? acc / (double)kt : 0.0;
-}
-
+// w_u = (1/K_u) sum over the non-empty cohorts s in (u-K, u] of omega_s, omega_s[a] =
+// W[s][a] / total_s.  When both windows of months t and t-1 are full (K non-empty cohorts
+// each), w_t - w_{t-1} = (omega_t - omega_{t-K}) / K: two label reads per leg instead of 2K.
+// The per-cohort inverse totals of the K+1 months involved are staged in LDS once per
+// workgroup (chunk partials summed in chunk order), so the inner loop multiplies.
 __global__ __launch_bounds__(PF_THREADS) void k_turnover(
-    const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FW,
-    int T_m, int B, int64_t N, int K, int n_bins, double half_spread, double k_impact,
-    double aum, const double* __restrict__ ADV, const double* __restrict__ SIG,
-    double* __restrict__ TURN, double* __restrict__ COST) {
-  const int tb = blockIdx.x;
+    const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
+    int T_m, int B, int64_t N, int K, int n_bins, int Cf, int64_t CH, double half_spread,
+    double k_impact, double aum, const double* __restrict__ ADV, const double* __restrict__ SIG,
+    double* __restrict__ TURNp, double* __restrict__ COSTp) {
+  const int c = blockIdx.x, Ct = gridDim.x;
+  const int tb = blockIdx.y;
   const int t = tb / B, b = tb - t * B;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ double inv[2][TO_MAXK + 1];   // [leg][j]: 1/total of cohort s = t - j (0 = empty)
+  __shared__ double sk[2][2];              // [leg][0: month t, 1: month t-1]: 1/K_u (0 if none)
+  __shared__ int full[2];
+  for (int j = tid; j <= K; j += PF_THREADS) {
+    const int s = t - j;
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      double tot = 0.0;
+      if (s >= 0)
+        for (int cc = 0; cc < Cf; ++cc) tot += FWp[(((int64_t)s * B + b) * Cf + cc) * 2 + li];
+      inv[li][j] = tot > 0.0 ? 1.0 / tot : 0.0;
+    }
+  }
+  __syncthreads();
+  if (tid < 2) {
+    const int li = tid;
+    int k1 = 0, k0 = 0;
+    for (int j = 0; j < K; ++j) k1 += inv[li][j] > 0.0 ? 1 : 0;                    // month t
+    for (int j = 1; j <= K; ++j) k0 += (t >= 1 && inv[li][j] > 0.0) ? 1 : 0;        // month t-1
+    sk[li][0] = k1 > 0 ? 1.0 / (double)k1 : 0.0;
+    sk[li][1] = k0 > 0 ? 1.0 / (double)k0 : 0.0;
+    full[li] = (k1 == K && k0 == K) ? 1 : 0;
+  }
+  __syncthreads();
+  const int64_t a0 = (int64_t)c * CH;
+  const int64_t a1 = a0 + CH < N ? a0 + CH : N;
   const int64_t rt = ((int64_t)t * B + b) * N;
   const bool impact = ADV && aum > 0.0;
   double turn = 0.0, cost = 0.0;
-  for (int64_t a = tid; a < N; a += PF_THREADS) {
+  for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
     double unit_sig = 0.02, adv = 0.0;
     if (impact) {
       adv = ADV[rt + a];
@@ -154,9 +177,24 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
 #pragma unroll
     for (int li = 0; li < 2; ++li) {
       const int d = li == 0 ? n_bins - 1 : 0;
-      const double w1 = leg_weight(L, W, FW, t, B, b, N, a, K, d, li);
-      const double w0 = leg_weight(L, W, FW, t - 1, B, b, N, a, K, d, li);
-      const double dw = fabs(w1 - w0);
+      double dw;
+      if (full[li]) {
+        const int64_t o1 = rt + a, o0 = ((int64_t)(t - K) * B + b) * N + a;
+        const double w1 = member_w(L[o1], d, W, o1) * inv[li][0];
+        const double w0 = member_w(L[o0], d, W, o0) * inv[li][K];
+        dw = fabs(w1 - w0) * sk[li][0];
+      } else {
+        double x1 = 0.0, x0 = 0.0;
+        for (int j = 0; j <= K; ++j) {
+          const double iv = inv[li][j];
+          if (iv == 0.0) continue;
+          const int64_t o = ((int64_t)(t - j) * B + b) * N + a;
+          const double w = member_w(L[o], d, W, o) * iv;
+          if (j < K) x1 += w;
+          if (j >= 1) x0 += w;
+        }
+        dw = fabs(x1 * sk[li][0] - x0 * sk[li][1]);
+      }
       turn += dw;
       double unit = half_spread;
       if (impact && adv > 0.0) {
@@ -167,41 +205,64 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     }
   }
   __shared__ double red[PF_WAVES][2];
-  const double a = wave_sum(turn), c = wave_sum(cost);
-  if (lane == 0) { red[wid][0] = a; red[wid][1] = c; }
+  const double x1 = wave_sum(turn), y1 = wave_sum(cost);
+  if (lane == 0) { red[wid][0] = x1; red[wid][1] = y1; }
   __syncthreads();
   if (tid == 0) {
     double x = 0.0, y = 0.0;
     for (int w2 = 0; w2 < PF_WAVES; ++w2) { x += red[w2][0]; y += red[w2][1]; }
-    if (TURN) TURN[tb] = 0.5 * x;
-    if (COST) COST[tb] = y;
+    TURNp[(int64_t)tb * Ct + c] = 0.5 * x;
+    COSTp[(int64_t)tb * Ct + c] = y;
   }
 }
 
 // ------------------------------------------------------------------------------ E2, E3
-__global__ __launch_bounds__(PF_THREADS) void k_overlap_ls(
-    const double* __restrict__ SWR, const double* __restrict__ SW,
-    const int32_t* __restrict__ CNT, int T_m, int B, int K, int nb, double* __restrict__ PR,
-    double* __restrict__ LS, const double* __restrict__ COST, double* __restrict__ NET) {
+// one 64-lane workgroup per (t, b): lane d < nb combines decile d over the chunks and the
+// cohorts; lane 0 also totals the turnover / cost partials.
+__global__ __launch_bounds__(64) void k_overlap(
+    const double* __restrict__ SWRp, const double* __restrict__ SWp, int K, int Kmax, int C, int nb,
+    const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
+    double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST) {
+  const int64_t tb = blockIdx.x;
+  const int d = threadIdx.x;
+  if (d < nb) {
+    double acc = 0.0;
+    int n = 0;
+    for (int k = 0; k < K; ++k) {
+      double x = 0.0, y = 0.0;
+      for (int c = 0; c < C; ++c) {
+        const int64_t o = ((tb * Kmax + k) * C + c) * nb + d;
+        x += SWRp[o];
+        y += SWp[o];
+      }
+      if (y > 0.0) { acc += x / y; ++n; }
+    }
+    PR[tb * nb + d] = n > 0 ? acc / (double)n : qnan();
+  }
+  if (d == 0 && TURNp) {
+    double x = 0.0, y = 0.0;
+    for (int c = 0; c < Ct; ++c) { x += TURNp[tb * Ct + c]; y += COSTp[tb * Ct + c]; }
+    if (TURN) TURN[tb] = x;
+    if (COST) COST[tb] = y;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ls(const double* __restrict__ PR, int T_m, int B, int nb,
+                                            double* __restrict__ LS,
+                                            const double* __restrict__ COST,
+                                            double* __restrict__ NET) {
   const int b = blockIdx.x;
   __shared__ int has_lo, has_hi;
   if (threadIdx.x == 0) { has_lo = 0; has_hi = 0; }
   __syncthreads();
+  int lo = 0, hi = 0;
   for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
-    const int64_t tb = (int64_t)t * B + b;
-    for (int d = 0; d < nb; ++d) {
-      double s = 0.0;
-      int n = 0;
-      for (int k = 0; k < K; ++k) {
-        const int64_t o = (tb * K + k) * nb + d;
-        if (CNT[o] > 0) { s += SWR[o] / SW[o]; ++n; }
-      }
-      const double v = n > 0 ? s / (double)n : qnan();
-      PR[tb * nb + d] = v;
-      if (n > 0 && d == 0) atomicOr(&has_lo, 1);
-      if (n > 0 && d == nb - 1) atomicOr(&has_hi, 1);
-    }
+    const double* e = PR + ((int64_t)t * B + b) * nb;
+    lo |= e[0] == e[0];
+    hi |= e[nb - 1] == e[nb - 1];
   }
+  if (lo) atomicOr(&has_lo, 1);
+  if (hi) atomicOr(&has_hi, 1);
   __syncthreads();
   const bool both = has_lo && has_hi;
   for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
@@ -214,7 +275,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_overlap_ls(
     double v = qnan();
     if (any) v = both ? (e[nb - 1] - e[0]) : (mx - mn);
     LS[tb] = v;
-    if (NET) NET[tb] = v - (COST ? COST[tb] : 0.0);
+    if (NET) NET[tb] = v - COST[tb];
   }
 }
 
@@ -276,64 +337,144 @@ __global__ __launch_bounds__(256) void k_bootstrap_panel(const double* __restric
 }
 
 // ------------------------------------------------------------------------------- C ABI
+struct PfPlan {
+  int C, kpar, Ct;
+  int64_t CH, CHt;
+};
+
+// Enough workgroups to fill 256 CUs several times over, chunks of >= PF_CHUNK_MIN assets.
+static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
+  PfPlan p;
+  const int64_t rows = (int64_t)T_m * B;
+  const int64_t want = 4096;
+  const int64_t cmax = (N + PF_CHUNK_MIN - 1) / PF_CHUNK_MIN;
+  // the chunking depends on (rows, N) only, so a cohort pass gives the same partial sums
+  // whatever Kmax it was planned for (portfolio_multi == per-K portfolio, bit for bit)
+  // (cohort-parallel grids, kpar = 1, made tens of thousands of tiny workgroups at C3 and
+  // ran slower than one workgroup walking its K cohorts over a chunk.)
+  (void)K;
+  p.kpar = 0;
+  int64_t C = (want + rows - 1) / rows;
+  C = C < 1 ? 1 : (C > cmax ? cmax : C);
+  p.C = (int)C;
+  p.CH = (N + C - 1) / C;
+  int64_t Ct = (want + rows - 1) / rows;
+  Ct = Ct < 1 ? 1 : (Ct > cmax ? cmax : Ct);
+  p.Ct = (int)Ct;
+  p.CHt = (N + Ct - 1) / Ct;
+  return p;
+}
+
 template <int NB>
-static void launch_cohort(hipStream_t st, const int8_t* L, const double* NR, const double* W,
-                          int T_m, int B, int64_t N, int K, double* SWR, double* SW,
-                          int32_t* CNT, double* FW) {
-  hipLaunchKernelGGL(k_cohort<NB>, dim3(K, (unsigned)(T_m * B)), dim3(PF_THREADS), 0, st, L, NR,
-                     W, T_m, B, N, K, SWR, SW, CNT, FW);
+static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
+                          const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
+                          double* SWp, double* FWp) {
+  const dim3 g((unsigned)pl.C, (unsigned)(T_m * B), pl.kpar ? (unsigned)K : 1u);
+  if (W)
+    hipLaunchKernelGGL((k_cohort<NB, true>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
+                       pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp);
+  else
+    hipLaunchKernelGGL((k_cohort<NB, false>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
+                       pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp);
+}
+
+// Workspace layout of the cohort partials for (T_m, B, N, n_bins, Kmax): SWRp, SWp
+// [rows][Kmax][C][n_bins], FWp [rows][C][2], then the turnover partials [rows][Ct] x 2.
+struct PfLayout {
+  PfPlan p;
+  int64_t rows, swr, sw, fw, turn, cost, bytes;
+};
+static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax) {
+  PfLayout l;
+  l.p = pf_plan(T_m, B, N, Kmax);
+  l.rows = (int64_t)T_m * B;
+  const int64_t cs = l.rows * Kmax * l.p.C * n_bins;
+  l.swr = 0;
+  l.sw = cs;
+  l.fw = 2 * cs;
+  l.turn = l.fw + l.rows * l.p.C * 2;
+  l.cost = l.turn + l.rows * l.p.Ct;
+  l.bytes = (l.cost + l.rows * l.p.Ct) * 8 + 256;
+  return l;
 }
 
 extern "C" {
 
-int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int32_t n_bins, int32_t K) {
-  if (T_m < 0 || B < 1 || n_bins < 1 || K < 1) return 0;
-  const int64_t cells = (int64_t)T_m * B * K * n_bins;
-  return cells * (8 + 8 + 4) + (int64_t)T_m * B * 2 * 8 + 64;
+int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t K) {
+  if (T_m < 0 || B < 1 || N <= 0 || n_bins < 1 || K < 1) return 0;
+  return pf_layout(T_m, B, N, n_bins, K).bytes;
+}
+
+int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
+                    int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, void* workspace) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!L || !NR || !workspace || T_m < 0 || B < 1 || N <= 0 || Kmax < 1 || Kmax > TO_MAXK ||
+      (int64_t)T_m * B > 0x7FFFFFFF)
+    return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: bad arguments (T_m=%d B=%d N=%lld Kmax=%d)",
+                   T_m, B, (long long)N, Kmax);
+  if (T_m == 0) return CSM_OK;
+  const PfLayout lay = pf_layout(T_m, B, N, n_bins, Kmax);
+  double* ws = (double*)workspace;
+  hipStream_t st = ctx->stream;
+  switch (n_bins) {
+#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw); break;
+    PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20)
+#undef PF_CASE
+    default:
+      return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: n_bins=%d unsupported (2,3,4,5,10,20)", n_bins);
+  }
+  LAUNCH_CHECK(ctx, "k_cohort");
+  return CSM_OK;
+}
+
+int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, int32_t T_m,
+                               int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, int32_t K,
+                               double half_spread, double k_impact, double aum, const double* ADV,
+                               const double* SIG, double* PR, double* LS, double* TURN,
+                               double* COST, double* NET, void* workspace) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!L || !PR || !LS || !workspace || T_m < 0 || B < 1 || N <= 0 || K < 1 || K > Kmax ||
+      Kmax > TO_MAXK || n_bins < 2 || n_bins > 20 || !(half_spread >= 0.0) ||
+      !(k_impact >= 0.0) || !(aum >= 0.0) || (int64_t)T_m * B > 0x7FFFFFFF)
+    return set_err(ctx, CSM_E_INVAL, "csm_portfolio_from_cohorts: bad arguments (T_m=%d B=%d N=%lld K=%d Kmax=%d)",
+                   T_m, B, (long long)N, K, Kmax);
+  if (NET && !COST)
+    return set_err(ctx, CSM_E_INVAL, "csm_portfolio: NET needs COST");
+  if (T_m == 0) return CSM_OK;
+  const PfLayout lay = pf_layout(T_m, B, N, n_bins, Kmax);
+  double* ws = (double*)workspace;
+  hipStream_t st = ctx->stream;
+  const bool costs = TURN || COST;
+  if (costs) {
+    hipLaunchKernelGGL(k_turnover, dim3((unsigned)lay.p.Ct, (unsigned)lay.rows), dim3(PF_THREADS),
+                       0, st, L, W, (const double*)(ws + lay.fw), T_m, B, N, K, n_bins, lay.p.C,
+                       lay.p.CHt, half_spread, k_impact, aum, ADV, SIG, ws + lay.turn,
+                       ws + lay.cost);
+    LAUNCH_CHECK(ctx, "k_turnover");
+  }
+  hipLaunchKernelGGL(k_overlap, dim3((unsigned)lay.rows), dim3(64), 0, st,
+                     (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), K, Kmax,
+                     lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
+                     (const double*)(ws + lay.cost), lay.p.Ct, PR, TURN, COST);
+  LAUNCH_CHECK(ctx, "k_overlap");
+  hipLaunchKernelGGL(k_ls, dim3((unsigned)B), dim3(256), 0, st, (const double*)PR, T_m, B, n_bins,
+                     LS, (const double*)COST, NET);
+  LAUNCH_CHECK(ctx, "k_ls");
+  return CSM_OK;
 }
 
 int csm_portfolio(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
                   int32_t B, int64_t N, int32_t n_bins, int32_t K, double half_spread,
                   double k_impact, double aum, const double* ADV, const double* SIG, double* PR,
                   double* LS, double* TURN, double* COST, double* NET, void* workspace) {
-  int r = prep(ctx);
+  int r = csm_cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, K, workspace);
   if (r) return r;
-  if (!L || !NR || !PR || !LS || !workspace || T_m < 0 || B < 1 || N <= 0 || K < 1 ||
-      K > 240 || !(half_spread >= 0.0) || !(k_impact >= 0.0) || !(aum >= 0.0) ||
-      (int64_t)T_m * B > 0x7FFFFFFF)
-    return set_err(ctx, CSM_E_INVAL, "csm_portfolio: bad arguments (T_m=%d B=%d N=%lld K=%d)",
-                   T_m, B, (long long)N, K);
-  if (NET && !COST)
-    return set_err(ctx, CSM_E_INVAL, "csm_portfolio: NET needs COST");
-  if (T_m == 0) return CSM_OK;
-  const int64_t cells = (int64_t)T_m * B * K * n_bins;
-  double* SWR = (double*)workspace;
-  double* SW = SWR + cells;
-  double* FW = SW + cells;
-  int32_t* CNT = (int32_t*)(FW + (int64_t)T_m * B * 2);
-  hipStream_t st = ctx->stream;
-  switch (n_bins) {
-    case 2: launch_cohort<2>(st, L, NR, W, T_m, B, N, K, SWR, SW, CNT, FW); break;
-    case 3: launch_cohort<3>(st, L, NR, W, T_m, B, N, K, SWR, SW, CNT, FW); break;
-    case 4: launch_cohort<4>(st, L, NR, W, T_m, B, N, K, SWR, SW, CNT, FW); break;
-    case 5: launch_cohort<5>(st, L, NR, W, T_m, B, N, K, SWR, SW, CNT, FW); break;
-    case 10: launch_cohort<10>(st, L, NR, W, T_m, B, N, K, SWR, SW, CNT, FW); break;
-    case 20: launch_cohort<20>(st, L, NR, W, T_m, B, N, K, SWR, SW, CNT, FW); break;
-    default:
-      return set_err(ctx, CSM_E_INVAL, "csm_portfolio: n_bins=%d unsupported (2,3,4,5,10,20)", n_bins);
-  }
-  LAUNCH_CHECK(ctx, "k_cohort");
-  if (TURN || COST) {
-    hipLaunchKernelGGL(k_turnover, dim3((unsigned)(T_m * B)), dim3(PF_THREADS), 0, st, L, W,
-                       (const double*)FW, T_m, B, N, K, n_bins, half_spread, k_impact, aum, ADV,
-                       SIG, TURN, COST);
-    LAUNCH_CHECK(ctx, "k_turnover");
-  }
-  hipLaunchKernelGGL(k_overlap_ls, dim3((unsigned)B), dim3(PF_THREADS), 0, st,
-                     (const double*)SWR, (const double*)SW, (const int32_t*)CNT, T_m, B, K,
-                     n_bins, PR, LS, (const double*)COST, NET);
-  LAUNCH_CHECK(ctx, "k_overlap_ls");
-  return CSM_OK;
+  if (!PR || !LS)
+    return set_err(ctx, CSM_E_INVAL, "csm_portfolio: PR and LS are required");
+  return csm_portfolio_from_cohorts(ctx, L, W, T_m, B, N, n_bins, K, K, half_spread, k_impact,
+                                    aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace);
 }
 
 int csm_bootstrap(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t B, int64_t b0,

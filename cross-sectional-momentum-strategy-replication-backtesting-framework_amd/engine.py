@@ -134,8 +134,14 @@ class Engine:
         return PM, VOL
 
     def momentum(self, PM, J=12, skip=1, with_ret=False, carry=None, next_pm=None,
-                 carry_out=None, out=None):
+                 carry_out=None, out=None, chunked="auto"):
+        """csm_momentum.  chunked="auto": panels too narrow to fill the chip (few assets)
+        take the time-chunked scan (csm_momentum_chunked, the same bits) when no carry is
+        involved."""
         T_m, N = PM.shape
+        if (chunked == "auto" and carry is None and next_pm is None and carry_out is None
+                and self.default_chunks(T_m, N, J, skip) > 1):
+            return self.momentum_chunked(PM, J, skip, with_ret=with_ret, out=out)
         _need(PM, "PM", torch.float64, (T_m, N), self.device)
         W = J + skip
         if carry is not None:
@@ -288,13 +294,47 @@ class Engine:
             NET = self.empty((T_m, B)) if with_costs else None
         else:
             PR, LS, TURN, COST, NET = out
-        nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, int(n_bins), int(K)))
+        nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, N, int(n_bins), int(K)))
         if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
             workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
         self._call("csm_portfolio", _ptr(L), _ptr(NR), _ptr(W), T_m, int(B), N, int(n_bins),
                    int(K), float(half_spread), float(k_impact), float(aum), _ptr(ADV), _ptr(SIG),
                    _ptr(PR), _ptr(LS), _ptr(TURN), _ptr(COST), _ptr(NET), _ptr(workspace))
         return PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET)
+
+    def portfolio_multi(self, L, NR, n_bins=10, Ks=(1,), W=None, B=1, half_spread=0.0005,
+                        k_impact=0.1, aum=0.0, ADV=None, SIG=None, with_costs=True,
+                        workspace=None):
+        """One cohort-sum pass (csm_cohort_sums, Kmax = max(Ks)) shared by the accounting of
+        every holding period K in Ks (csm_portfolio_from_cohorts).  Returns {K: PortfolioOut}."""
+        T_m, BN = L.shape
+        if B < 1 or BN % B:
+            raise ValueError(f"row width {BN} is not B={B} panels")
+        N = BN // B
+        _need(L, "L", torch.int8, (T_m, BN), self.device)
+        _need(NR, "NR", torch.float64, (T_m, BN), self.device)
+        for t, nm in ((W, "W"), (ADV, "ADV"), (SIG, "SIG")):
+            if t is not None:
+                _need(t, nm, torch.float64, (T_m, BN), self.device)
+        Ks = [int(k) for k in Ks]
+        Kmax = max(Ks)
+        nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, N, int(n_bins), Kmax))
+        if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
+            workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
+        self._call("csm_cohort_sums", _ptr(L), _ptr(NR), _ptr(W), T_m, int(B), N, int(n_bins),
+                   Kmax, _ptr(workspace))
+        res = {}
+        for K in Ks:
+            PR, LS = self.empty((T_m, B, n_bins)), self.empty((T_m, B))
+            TURN = self.empty((T_m, B)) if with_costs else None
+            COST = self.empty((T_m, B)) if with_costs else None
+            NET = self.empty((T_m, B)) if with_costs else None
+            self._call("csm_portfolio_from_cohorts", _ptr(L), _ptr(W), T_m, int(B), N,
+                       int(n_bins), Kmax, K, float(half_spread), float(k_impact), float(aum),
+                       _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS), _ptr(TURN), _ptr(COST),
+                       _ptr(NET), _ptr(workspace))
+            res[K] = PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET)
+        return res
 
     def bootstrap(self, R, B, b0=0, seed=5000, mean_block=6.0, p0=100.0, out=None):
         """csm_bootstrap: B stationary-bootstrap month panels of the base month-return panel

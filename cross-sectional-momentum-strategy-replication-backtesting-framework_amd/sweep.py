@@ -8,8 +8,9 @@ panels with the month-end aggregation done once per panel:
     run_demo.py:48) and one qcut pass (run_demo.py:18-29) -- all B panels of a batch at once,
     laid out side by side as [T_m][B*N] (the scan is per asset; the labels are per (month,
     panel) row of N assets);
-  * per (J, K): one csm_portfolio pass (K-overlap cohorts, equal or value weights, turnover,
-    spread + square-root-impact costs; rules E1..E5);
+  * per J: one cohort-sum pass for the largest K (cohort sums do not depend on K), then per
+    (J, K) the K-overlap accounting (equal or value weights, turnover, spread +
+    square-root-impact costs; rules E1..E5);
   * per (J, K, panel): a summary row (months, mean and Sharpe of the long-short as in
     src/utils.py:8-16 at 12 periods a year, mean turnover, mean cost, mean / Sharpe of net).
 
@@ -108,17 +109,22 @@ class SweepRunner:
         T_m, BN = PMb.shape
         N = BN // B
         rows, series = [], {}
-        by_j = {}
-        for J in c.Js:
+        kw = dict(W=W, B=B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum, ADV=ADV,
+                  SIG=SIG, with_costs=c.costs)
+        for J in c.Js:   # one J's monthly panels live at a time
             _, M, NR = st.momentum(PMb, J, c.skip)
             L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
-            by_j[J] = (L.reshape(T_m, BN), NR)
+            del M
+            L = L.reshape(T_m, BN)
+            if hasattr(st, "portfolio_multi"):   # one cohort pass serves every K of this J
+                outs = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, **kw)
+            else:
+                outs = {K: st.portfolio(L, NR, c.n_bins, K=K, **kw) for K in c.Ks}
+            for K in c.Ks:
+                series[(J, K)] = outs[K]
+            del L, NR
         for (J, K) in c.strategies:
-            L, NR = by_j[J]
-            out = st.portfolio(L, NR, c.n_bins, K=K, W=W, B=B, half_spread=c.half_spread,
-                               k_impact=c.k_impact, aum=c.aum, ADV=ADV, SIG=SIG,
-                               with_costs=c.costs)
-            series[(J, K)] = out
+            out = series[(J, K)]
             rows.append(summarize(out.LS, out.TURN, out.COST, out.NET))
         return torch.stack(rows, dim=1), series                  # [B][S][F]
 

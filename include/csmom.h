@@ -182,14 +182,28 @@ int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, 
  *             volatility, NaN/NULL -> 0.02): the cost model of src/execution_models.py:4-12
  *   PR [T_m][B][n_bins]  overlapped decile returns;  LS [T_m][B] long-short (NaN = dropped)
  *   TURN, COST, NET [T_m][B] nullable: long-short turnover (1/2 sum |dw|), cost, LS - COST
- *   workspace: device buffer of csm_portfolio_workspace(T_m, B, n_bins, K) bytes
+ *   workspace: device buffer of csm_portfolio_workspace(T_m, B, N, n_bins, K) bytes
  * n_bins in {2,3,4,5,10,20}.
  */
-int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int32_t n_bins, int32_t K);
+int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t K);
 int csm_portfolio(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
                   int32_t B, int64_t N, int32_t n_bins, int32_t K, double half_spread,
                   double k_impact, double aum, const double* ADV, const double* SIG, double* PR,
                   double* LS, double* TURN, double* COST, double* NET, void* workspace);
+
+/*
+ * The two halves of csm_portfolio, for sweeps over K: cohort sums do not depend on the
+ * holding period, so one csm_cohort_sums pass with Kmax cohorts (workspace of
+ * csm_portfolio_workspace(T_m, B, N, n_bins, Kmax) bytes) serves csm_portfolio_from_cohorts
+ * for every K <= Kmax (same L / W; outputs as csm_portfolio).
+ */
+int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
+                    int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, void* workspace);
+int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, int32_t T_m,
+                               int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, int32_t K,
+                               double half_spread, double k_impact, double aum, const double* ADV,
+                               const double* SIG, double* PR, double* LS, double* TURN,
+                               double* COST, double* NET, void* workspace);
 
 /*
  * Stationary month bootstrap (BASELINE config C5; rule E6): panels b0 .. b0+B-1 of the base

@@ -40,7 +40,7 @@ def test_fixture_pipeline(engine, name):
         assert bits_equal(pm.reshape(-1)[idx], z["PM_sample"])
     for tag in golden_tags(z):
         J, s = parse_tag(tag)
-        R, M, NR = engine.momentum(PM, J, s, with_ret=True)
+        R, M, NR = engine.momentum(PM, J, s, with_ret=True, chunked=False)
         L, EW, CNT, NV = engine.deciles(M, NR, 10, with_nv=True)
         LS = engine.long_short(EW, CNT)
         r, m, nr = R.cpu().numpy(), M.cpu().numpy(), NR.cpu().numpy()

@@ -158,3 +158,44 @@ def test_sweep_runner_gpu_vs_oracle(engine):
     assert np.array_equal(got[..., 0], ref[..., 0])
     m = ~np.isnan(ref)
     assert np.allclose(got[m], ref[m], rtol=1e-9, atol=1e-13)
+
+
+@pytest.mark.parametrize("n_bins", [2, 5, 20])
+def test_portfolio_nbins(engine, n_bins):
+    z = load_golden("c1")
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    _, M, NR = engine.momentum(PM, 6, 1)
+    L, _, _, _ = engine.deciles(M, None, n_bins)
+    ref = PO.portfolio(L.cpu().numpy(), NR.cpu().numpy(), n_bins, K=4)
+    out = engine.portfolio(L, NR, n_bins, K=4)
+    _close(out.PR, ref["PR"], "PR")
+    _close(out.LS, ref["LS"], "LS")
+    _close(out.TURN, ref["TURN"], "TURN")
+
+
+def test_portfolio_wide_panel_single_chunk(engine):
+    """Wide batches (many (t, b) rows) take the one-chunk, cohort-loop plan; narrow ones the
+    chunked, cohort-parallel plan: both against the oracle."""
+    L, NR, _, _ = _labels(engine, "c1")
+    Lh, NRh = L.cpu().numpy(), NR.cpu().numpy()
+    B = 16
+    L16 = np.stack([np.roll(Lh, i, axis=1) for i in range(B)], axis=1)
+    NR16 = np.stack([np.roll(NRh, i, axis=1) for i in range(B)], axis=1)
+    T_m, _, N = L16.shape
+    ref = PO.portfolio(L16, NR16, 10, K=12)
+    out = engine.portfolio(_up(L16.reshape(T_m, B * N)), _up(NR16.reshape(T_m, B * N)), 10,
+                           K=12, B=B)
+    _close(out.PR, ref["PR"], "PR")
+    _close(out.TURN, ref["TURN"], "TURN")
+    _close(out.NET, ref["NET"], "NET")
+
+
+def test_portfolio_multi_shares_cohort_pass(engine):
+    """One cohort-sum pass with Kmax serves every K <= Kmax: identical to per-K calls."""
+    L, NR, _, PM = _labels(engine, "c1")
+    W = _up(np.abs(PM.cpu().numpy()) * 1e6)
+    multi = engine.portfolio_multi(L, NR, 10, Ks=(3, 6, 9, 12), W=W)
+    for K, got in multi.items():
+        one = engine.portfolio(L, NR, 10, K=K, W=W)
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(got, f).cpu().numpy(), getattr(one, f).cpu().numpy()), (K, f)
