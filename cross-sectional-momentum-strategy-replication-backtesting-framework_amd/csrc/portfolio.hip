@@ -74,34 +74,51 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
     }
     const int64_t rs = ((int64_t)s * B + b) * N;
     double swr[NB], sw[NB];
+    uint32_t cnt[NB];   // equal weight: the weight sum is a count
 #pragma unroll
-    for (int d = 0; d < NB; ++d) { swr[d] = 0.0; sw[d] = 0.0; }
+    for (int d = 0; d < NB; ++d) { swr[d] = 0.0; sw[d] = 0.0; cnt[d] = 0; }
     double ft = 0.0, fb = 0.0;
-    for (int64_t i = a0 + tid; i < a1; i += PF_THREADS) {
-      const int lab = L[rs + i];
-      const double r = NR[rt + i];
-      double w = 1.0;
-      if (VW) {
-        const double x = W[rs + i];
-        w = (x > 0.0 && x < INFINITY) ? x : 0.0;   // invalid weight: not a member
-      }
-      if (k == 0) {
-        ft += lab == NB - 1 ? w : 0.0;
-        fb += lab == 0 ? w : 0.0;
-      }
-      const bool ok = r == r;
-      const double wr = ok ? (VW ? w * r : r) : 0.0;
-      const double wv = ok ? w : 0.0;
+    // CU cells per lane per trip, all loads issued before the first use (memory-level
+    // parallelism; a one-cell loop waits out a full memory round trip per cell)
+    constexpr int CU = 8;
+    for (int64_t i0 = a0 + tid; i0 < a1; i0 += CU * PF_THREADS) {
+      int lab[CU];
+      double r[CU], wx[CU];
 #pragma unroll
-      for (int d = 0; d < NB; ++d) {
-        const bool h = lab == d;
-        swr[d] += h ? wr : 0.0;
-        sw[d] += h ? wv : 0.0;
+      for (int u = 0; u < CU; ++u) {
+        const int64_t i = i0 + (int64_t)u * PF_THREADS;
+        const bool in = i < a1;
+        lab[u] = in ? (int)L[rs + i] : -1;
+        r[u] = in ? NR[rt + i] : 0.0;
+        if (VW) wx[u] = in ? W[rs + i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < CU; ++u) {
+        double w = 1.0;
+        if (VW) w = (wx[u] > 0.0 && wx[u] < INFINITY) ? wx[u] : 0.0;   // invalid: not a member
+        if (k == 0) {
+          ft += lab[u] == NB - 1 ? w : 0.0;
+          fb += lab[u] == 0 ? w : 0.0;
+        }
+        // a cell with no valid return (or weight) joins no decile sum; the one-hot factor
+        // hd in {0, 1} makes each decile one select + one fma: fma(1, x, s) rounds exactly
+        // like s + x and fma(0, x, s) == s, so the sums equal plain conditional adds
+        const bool ok = r[u] == r[u] && (!VW || w > 0.0);
+        const int lb = ok ? lab[u] : -1;
+        const double wr = ok ? (VW ? w * r[u] : r[u]) : 0.0;   // fma(0, NaN, s) would be NaN
+#pragma unroll
+        for (int d = 0; d < NB; ++d) {
+          const bool h = lb == d;
+          const double hd = h ? 1.0 : 0.0;
+          swr[d] = fma(hd, wr, swr[d]);
+          if (VW) sw[d] = fma(hd, w, sw[d]);
+          else cnt[d] += h ? 1u : 0u;
+        }
       }
     }
 #pragma unroll
     for (int d = 0; d < NB; ++d) {
-      const double x = wave_sum(swr[d]), y = wave_sum(sw[d]);
+      const double x = wave_sum(swr[d]), y = wave_sum(VW ? sw[d] : (double)cnt[d]);
       if (lane == 0) { red[wid][d] = x; red[wid][NB + d] = y; }
     }
     if (k == 0) {
@@ -168,7 +185,50 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
   const int64_t rt = ((int64_t)t * B + b) * N;
   const bool impact = ADV && aum > 0.0;
   double turn = 0.0, cost = 0.0;
-  for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
+  const bool both_full = full[0] && full[1];
+  const int64_t rk = ((int64_t)(t - K) * B + b) * N;   // month t-K (valid when full)
+  // steady state (both windows full): 4 cells per lane per trip, loads issued up front
+  constexpr int TU = 4;
+  int64_t a_tail = a0 + tid;
+  if (both_full) {
+    for (int64_t i0 = a0 + tid; i0 < a1; i0 += TU * PF_THREADS) {
+      int l1[TU], l0[TU];
+      double x1[TU], x0[TU], adv[TU], sg[TU];
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int64_t a = i0 + (int64_t)u * PF_THREADS;
+        const bool in = a < a1;
+        l1[u] = in ? (int)L[rt + a] : -1;
+        l0[u] = in ? (int)L[rk + a] : -1;
+        x1[u] = (W && in) ? W[rt + a] : 1.0;
+        x0[u] = (W && in) ? W[rk + a] : 1.0;
+        adv[u] = (impact && in) ? ADV[rt + a] : 0.0;
+        sg[u] = (impact && SIG && in) ? SIG[rt + a] : 0.02;
+      }
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const double vw1 = (x1[u] > 0.0 && x1[u] < INFINITY) ? x1[u] : 0.0;
+        const double vw0 = (x0[u] > 0.0 && x0[u] < INFINITY) ? x0[u] : 0.0;
+        const double unit_sig = sg[u] == sg[u] ? sg[u] : 0.02;
+#pragma unroll
+        for (int li = 0; li < 2; ++li) {
+          const int d = li == 0 ? n_bins - 1 : 0;
+          const double w1 = (l1[u] == d ? vw1 : 0.0) * inv[li][0];
+          const double w0 = (l0[u] == d ? vw0 : 0.0) * inv[li][K];
+          const double dw = fabs(w1 - w0) * sk[li][0];
+          turn += dw;
+          double unit = half_spread;
+          if (impact && adv[u] > 0.0) {
+            const double im = k_impact * unit_sig * sqrt(dw * aum / adv[u]);
+            unit = unit + ((im == im) ? im : 0.0);
+          }
+          cost += dw * unit;
+        }
+      }
+    }
+    a_tail = a1;  // nothing left for the general loop
+  }
+  for (int64_t a = a_tail; a < a1; a += PF_THREADS) {
     double unit_sig = 0.02, adv = 0.0;
     if (impact) {
       adv = ADV[rt + a];
@@ -179,7 +239,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
       const int d = li == 0 ? n_bins - 1 : 0;
       double dw;
       if (full[li]) {
-        const int64_t o1 = rt + a, o0 = ((int64_t)(t - K) * B + b) * N + a;
+        const int64_t o1 = rt + a, o0 = rk + a;
         const double w1 = member_w(L[o1], d, W, o1) * inv[li][0];
         const double w0 = member_w(L[o0], d, W, o0) * inv[li][K];
         dw = fabs(w1 - w0) * sk[li][0];
