@@ -9,6 +9,7 @@ a Python identifier).  Public API (reference file:line it replaces):
   assign_deciles_per_date               run_demo.py:18-29          (GPU)
   monthly_replication                   run_demo.py:31-79          (GPU + host summary)
   sharpe / ensure_dir / save_plot       src/utils.py:5-21          (host)
+  fetch_daily / normalize_daily_columns src/data_io.py:23-73,131-180 (host, cached CSVs only)
   Engine                                dense device pipeline (bench / multi-GPU)
   Engine.portfolio / Engine.bootstrap   K-overlap, value weights, turnover, costs, bootstrap
                                         (beyond run_demo.py:49-67)
@@ -16,6 +17,7 @@ a Python identifier).  Public API (reference file:line it replaces):
 """
 from ._lib import ABSENT_BITS, CsmError, CsmUnavailable, lib_path, load_library
 from .engine import Engine, PipelineOut, PortfolioOut, absent_tensor, is_absent, quantile_table
+from .data import fetch_daily, load_daily_panel, normalize_daily_columns
 from .features import compute_monthly_momentum_from_daily, compute_monthly_turnover, get_engine
 from .panel import DensePanel, from_long, month_offsets, monthly_frame
 from .replication import ReplicationResult, assign_deciles_per_date, monthly_replication
@@ -25,7 +27,8 @@ from .utils import ensure_dir, save_plot, sharpe
 __all__ = [
     "ABSENT_BITS", "CsmError", "CsmUnavailable", "lib_path", "load_library", "Engine",
     "PipelineOut", "PortfolioOut", "SweepConfig", "SweepRunner", "SUMMARY_FIELDS",
-    "strategy_grid", "absent_tensor", "is_absent", "quantile_table",
+    "strategy_grid", "fetch_daily", "load_daily_panel", "normalize_daily_columns",
+    "absent_tensor", "is_absent", "quantile_table",
     "compute_monthly_momentum_from_daily", "compute_monthly_turnover", "get_engine",
     "DensePanel", "from_long", "month_offsets", "monthly_frame", "ReplicationResult",
     "assign_deciles_per_date", "monthly_replication", "ensure_dir", "save_plot", "sharpe",
