@@ -23,7 +23,8 @@ EXPORTS = (
     "csm_shard_summary", "csm_fold_carry", "csm_signal", "csm_momentum_chunked",
     "csm_momentum_chunked_workspace", "csm_tune", "csm_signal_tiled", "csm_tile_panel",
     "csm_tiled_size", "csm_portfolio", "csm_portfolio_workspace", "csm_bootstrap",
-    "csm_cohort_sums", "csm_portfolio_from_cohorts",
+    "csm_cohort_sums", "csm_portfolio_from_cohorts", "csm_turnover_features",
+    "csm_double_sort_labels",
 )
 
 
@@ -72,6 +73,9 @@ def _declare(lib):
         "csm_portfolio_from_cohorts": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32, _i32,
                                                       _i32, _f64, _f64, _f64, _p, _p, _p, _p,
                                                       _p, _p, _p, _p]),
+        "csm_turnover_features": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p,
+                                                 _p]),
+        "csm_double_sort_labels": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p]),
         "csm_bootstrap": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64,
                                          _f64, _p, _p]),
         "csm_tile_panel": (ctypes.c_int, [_p, _p, _i64, _i64, _p]),

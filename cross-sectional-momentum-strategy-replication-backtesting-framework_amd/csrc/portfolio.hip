@@ -479,10 +479,10 @@ int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const doubl
   hipStream_t st = ctx->stream;
   switch (n_bins) {
 #define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw); break;
-    PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20)
+    PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20) PF_CASE(30)
 #undef PF_CASE
     default:
-      return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: n_bins=%d unsupported (2,3,4,5,10,20)", n_bins);
+      return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: n_bins=%d unsupported (2,3,4,5,10,20,30)", n_bins);
   }
   LAUNCH_CHECK(ctx, "k_cohort");
   return CSM_OK;
@@ -496,7 +496,7 @@ int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, i
   int r = prep(ctx);
   if (r) return r;
   if (!L || !PR || !LS || !workspace || T_m < 0 || B < 1 || N <= 0 || K < 1 || K > Kmax ||
-      Kmax > TO_MAXK || n_bins < 2 || n_bins > 20 || !(half_spread >= 0.0) ||
+      Kmax > TO_MAXK || n_bins < 2 || n_bins > 30 || !(half_spread >= 0.0) ||
       !(k_impact >= 0.0) || !(aum >= 0.0) || (int64_t)T_m * B > 0x7FFFFFFF)
     return set_err(ctx, CSM_E_INVAL, "csm_portfolio_from_cohorts: bad arguments (T_m=%d B=%d N=%lld K=%d Kmax=%d)",
                    T_m, B, (long long)N, K, Kmax);
@@ -551,6 +551,149 @@ int csm_bootstrap(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t
   hipLaunchKernelGGL(k_bootstrap_panel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0,
                      ctx->stream, R, T_m, B, N, (const int32_t*)src, p0, PMb);
   LAUNCH_CHECK(ctx, "k_bootstrap_panel");
+  return CSM_OK;
+}
+
+}  // extern "C"
+
+// =====================================================================================
+// Share-turnover features (src/features.py:60-107) and the momentum x volume double sort
+// (LeSw00 section II; rules T1, T2 in oracle/features_oracle.py).
+// =====================================================================================
+#define TF_THREADS 128
+#define TF_MAXLB 48
+
+// One thread per asset walks its present rows in order.  turn_avg is pandas 2.3.3's
+// roll_mean (fixed window, min_periods = 1) restated: Kahan-compensated add / remove with
+// separate compensations, the consecutive-same-value and all-positive / all-negative
+// fix-ups -- bit for bit (-ffp-contract=off keeps every product / sum rounded on its own).
+__global__ __launch_bounds__(TF_THREADS) void k_turn_features(
+    const double* __restrict__ PM, const double* __restrict__ VOL, const double* __restrict__ so,
+    const double* __restrict__ mcap, int T_m, int64_t N, int lb, double* __restrict__ ADV,
+    double* __restrict__ SH, double* __restrict__ TURN, double* __restrict__ TAVG) {
+  __shared__ double ring[TF_MAXLB * TF_THREADS];
+  const int tid = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * TF_THREADS + tid;
+  if (a >= N) return;
+  double* rg = ring + tid;
+  const double s_out = so[a], m_cap = mcap[a];
+  int n = 0;                                  // present rows so far
+  int64_t nobs = 0, neg = 0, same = 0;
+  double sx = 0.0, cadd = 0.0, crem = 0.0, prev = 0.0;
+  for (int t = 0; t < T_m; ++t) {
+    const int64_t o = (int64_t)t * N + a;
+    const double p = PM[o];
+    if (is_absent(p)) {
+      ADV[o] = qnan(); SH[o] = qnan(); TURN[o] = qnan(); TAVG[o] = qnan();
+      continue;
+    }
+    double vol = VOL[o];
+    vol = vol == vol ? vol : 0.0;
+    const double adv = vol / 21.0;
+    double sh = qnan();
+    if (s_out == s_out) {
+      sh = s_out;
+    } else if (m_cap != 0.0 && p == p && p > 0.0) {   // NaN market cap is truthy in Python
+      const double q = m_cap / p;
+      sh = (q == q && fabs(q) < INFINITY) ? trunc(q) : qnan();
+    }
+    const double tv = sh > 0.0 ? adv / sh : qnan();
+    ADV[o] = adv; SH[o] = sh; TURN[o] = tv;
+    // rolling mean over the last lb present rows
+    if (n == 0) {
+      nobs = neg = same = 0;
+      sx = cadd = crem = 0.0;
+      prev = tv;
+    } else if (n >= lb) {
+      const double v = rg[((n - lb) % lb) * TF_THREADS];   // leaves the window
+      if (v == v) {
+        --nobs;
+        const double y = -v - crem;
+        const double u = sx + y;
+        crem = (u - sx) - y;
+        sx = u;
+        if (signbit(v)) --neg;
+      }
+    }
+    if (tv == tv) {
+      ++nobs;
+      const double y = tv - cadd;
+      const double u = sx + y;
+      cadd = (u - sx) - y;
+      sx = u;
+      if (signbit(tv)) ++neg;
+      same = (tv == prev) ? same + 1 : 1;
+      prev = tv;
+    }
+    rg[(n % lb) * TF_THREADS] = tv;
+    ++n;
+    double r = qnan();
+    if (nobs >= 1) {
+      r = sx / (double)nobs;
+      if (same >= nobs) r = prev;
+      else if (neg == 0 && r < 0.0) r = 0.0;
+      else if (neg == nobs && r > 0.0) r = 0.0;
+    }
+    TAVG[o] = r;
+  }
+}
+
+// X masked to the rows where M is valid (the double sort's tercile universe)
+__global__ __launch_bounds__(256) void k_mask_nan(const double* __restrict__ M,
+                                                  const double* __restrict__ X, int64_t n,
+                                                  double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = M[i] == M[i] ? X[i] : qnan();
+}
+
+__global__ __launch_bounds__(256) void k_combine_labels(const int8_t* __restrict__ Lm,
+                                                        const int8_t* __restrict__ Lv,
+                                                        int64_t n, int nv,
+                                                        int8_t* __restrict__ Lc) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const int a = Lm[i], b = Lv[i];
+    Lc[i] = (a >= 0 && b >= 0) ? (int8_t)(a * nv + b) : (int8_t)-1;
+  }
+}
+
+extern "C" {
+
+int csm_turnover_features(csm_ctx* ctx, const double* PM, const double* VOL, const double* so,
+                          const double* mcap, int32_t T_m, int64_t N, int32_t lookback,
+                          double* ADV, double* SH, double* TURN, double* TAVG) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!PM || !VOL || !so || !mcap || !ADV || !SH || !TURN || !TAVG || T_m < 0 || N <= 0 ||
+      lookback < 1 || lookback > TF_MAXLB)
+    return set_err(ctx, CSM_E_INVAL, "csm_turnover_features: bad arguments (T_m=%d N=%lld lookback=%d, max %d)",
+                   T_m, (long long)N, lookback, TF_MAXLB);
+  if (T_m == 0) return CSM_OK;
+  hipLaunchKernelGGL(k_turn_features, dim3((unsigned)((N + TF_THREADS - 1) / TF_THREADS)),
+                     dim3(TF_THREADS), 0, ctx->stream, PM, VOL, so, mcap, T_m, N, lookback, ADV,
+                     SH, TURN, TAVG);
+  LAUNCH_CHECK(ctx, "k_turn_features");
+  return CSM_OK;
+}
+
+int csm_double_sort_labels(csm_ctx* ctx, const double* M, const double* X, const int8_t* Lm,
+                           const int8_t* Lv, int32_t T_m, int64_t N, int32_t n_vol, double* Xm,
+                           int8_t* Lc) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!M || T_m < 0 || N <= 0 || n_vol < 1 || (!Xm && !Lc) || (Xm && !X) || (Lc && (!Lm || !Lv)))
+    return set_err(ctx, CSM_E_INVAL, "csm_double_sort_labels: bad arguments");
+  const int64_t n = (int64_t)T_m * N;
+  if (n == 0) return CSM_OK;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (Xm) {
+    hipLaunchKernelGGL(k_mask_nan, dim3(g), dim3(256), 0, ctx->stream, M, X, n, Xm);
+    LAUNCH_CHECK(ctx, "k_mask_nan");
+  }
+  if (Lc) {
+    hipLaunchKernelGGL(k_combine_labels, dim3(g), dim3(256), 0, ctx->stream, Lm, Lv, n, n_vol, Lc);
+    LAUNCH_CHECK(ctx, "k_combine_labels");
+  }
   return CSM_OK;
 }
 

@@ -336,6 +336,37 @@ class Engine:
             res[K] = PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET)
         return res
 
+    def turnover_features(self, PM, VOL, so, mcap, lookback=3):
+        """csm_turnover_features (src/features.py:60-107, rule T1): (ADV, SH, TURN, TAVG)."""
+        T_m, N = PM.shape
+        _need(PM, "PM", torch.float64, (T_m, N), self.device)
+        _need(VOL, "VOL", torch.float64, (T_m, N), self.device)
+        _need(so, "so", torch.float64, (N,), self.device)
+        _need(mcap, "mcap", torch.float64, (N,), self.device)
+        outs = [self.empty((T_m, N)) for _ in range(4)]
+        self._call("csm_turnover_features", _ptr(PM), _ptr(VOL), _ptr(so), _ptr(mcap), T_m, N,
+                   int(lookback), *[_ptr(o) for o in outs])
+        return tuple(outs)
+
+    def mask_by(self, M, X):
+        """X where M is valid, NaN elsewhere (csm_double_sort_labels)."""
+        T_m, N = M.shape
+        _need(X, "X", torch.float64, (T_m, N), self.device)
+        Xm = self.empty((T_m, N))
+        self._call("csm_double_sort_labels", _ptr(M), _ptr(X), None, None, T_m, N, 1, _ptr(Xm),
+                   None)
+        return Xm
+
+    def combine_labels(self, Lm, Lv, n_vol):
+        """n_vol * Lm + Lv where both are valid, else -1 (csm_double_sort_labels)."""
+        T_m, N = Lm.shape
+        _need(Lv, "Lv", torch.int8, (T_m, N), self.device)
+        Lc = self.empty((T_m, N), torch.int8)
+        dummy = self.empty((1,))
+        self._call("csm_double_sort_labels", _ptr(dummy), None, _ptr(Lm), _ptr(Lv), T_m, N,
+                   int(n_vol), None, _ptr(Lc))
+        return Lc
+
     def bootstrap(self, R, B, b0=0, seed=5000, mean_block=6.0, p0=100.0, out=None):
         """csm_bootstrap: B stationary-bootstrap month panels of the base month-return panel
         R[T_m][N] (rule E6) -> (src [B][T_m] int32, PMb [T_m][B*N] month prices)."""

@@ -183,7 +183,7 @@ int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, 
  *   PR [T_m][B][n_bins]  overlapped decile returns;  LS [T_m][B] long-short (NaN = dropped)
  *   TURN, COST, NET [T_m][B] nullable: long-short turnover (1/2 sum |dw|), cost, LS - COST
  *   workspace: device buffer of csm_portfolio_workspace(T_m, B, N, n_bins, K) bytes
- * n_bins in {2,3,4,5,10,20}.
+ * n_bins in {2,3,4,5,10,20,30}.
  */
 int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t K);
 int csm_portfolio(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
@@ -214,6 +214,29 @@ int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, i
  */
 int csm_bootstrap(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t B, int64_t b0,
                   uint64_t seed, double mean_block, double p0, int32_t* src, double* PMb);
+
+/*
+ * Share-turnover features, replacing src/features.py:60-107 (compute_monthly_turnover) on the
+ * dense monthly layout (rule T1): per present row adv = VOL / 21, shares = so[a] when not NaN
+ * else trunc(mcap[a] / PM) when mcap != 0 and PM > 0 (NaN when that is not finite),
+ * turnover = adv / shares when shares > 0, and turn_avg = pandas' rolling(lookback,
+ * min_periods=1).mean() over the asset's present rows (bit-exact restatement).
+ *   PM, VOL [T_m][N] from csm_month_end;  so, mcap [N] (NaN = not given)
+ *   ADV, SH, TURN, TAVG [T_m][N] out (NaN where the asset has no row); lookback in [1, 48]
+ */
+int csm_turnover_features(csm_ctx* ctx, const double* PM, const double* VOL, const double* so,
+                          const double* mcap, int32_t T_m, int64_t N, int32_t lookback,
+                          double* ADV, double* SH, double* TURN, double* TAVG);
+
+/*
+ * Momentum x volume double sort helpers (LeSw00 section II; rule T2):
+ *   Xm = X where M is valid, NaN elsewhere (the tercile universe; nullable)
+ *   Lc = n_vol * Lm + Lv where both labels are valid, -1 elsewhere (nullable)
+ * The cell returns then come from csm_portfolio with n_bins = n_mom * n_vol (30 supported).
+ */
+int csm_double_sort_labels(csm_ctx* ctx, const double* M, const double* X, const int8_t* Lm,
+                           const int8_t* Lv, int32_t T_m, int64_t N, int32_t n_vol, double* Xm,
+                           int8_t* Lc);
 
 #ifdef __cplusplus
 }

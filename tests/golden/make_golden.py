@@ -1,7 +1,7 @@
 """Generate the golden fixtures by running the REFERENCE itself (run once, in the build
 container; the reference never travels to the GPU box).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--only-turnover]
 
 * The reference is imported from /root/reference with a `yfinance` stub (the network is
   never touched) and executed from a scratch working directory with plotting disabled, so
@@ -246,8 +246,57 @@ def decile_cases(rd, n_cases=3000, seed=7):
     print(f"  deciles: {len(offs) - 1} cross-sections")
 
 
+def turnover_case(rd, feats):
+    """compute_monthly_turnover (src/features.py:60-107) on the edge panel's monthly frame with
+    a shares map mixing every branch of its _get_shares: shares_outstanding given, market_cap
+    only (positive, zero, negative, NaN), and missing tickers.  Looks back 3 (run_demo's value)
+    and 2 / 5 months."""
+    ed = make_panel(160, 640, seed=11, start="2015-01-01", late=0.15, delist=0.15,
+                    nan_day=0.03, absent_month=0.03, nan_month=0.03, cents=True)
+    P, V, days, ms, mend, tickers = (ed["P"], ed["V"], ed["days"], ed["month_start"],
+                                     ed["month_end"], ed["tickers"])
+    T_m, N = len(ms) - 1, P.shape[1]
+    tix = {t: i for i, t in enumerate(tickers)}
+    mix = {d: i for i, d in enumerate(mend)}
+    rng = np.random.default_rng(23)
+    so = np.full(N, np.nan)
+    mcap = np.full(N, np.nan)
+    shares = {}
+    for i, t in enumerate(tickers):
+        kind = i % 6
+        if kind in (0, 1):
+            so[i] = float(int(rng.integers(10**6, 10**9)))
+            shares[t] = {"shares_outstanding": int(so[i]), "market_cap": None}
+        elif kind == 2:
+            mcap[i] = float(rng.uniform(1e8, 1e11))
+            shares[t] = {"shares_outstanding": None, "market_cap": mcap[i]}
+        elif kind == 3:
+            mcap[i] = [0.0, -5.0e9, np.nan][i % 3]
+            shares[t] = {"shares_outstanding": np.nan, "market_cap": mcap[i]}
+        elif kind == 4:
+            shares[t] = {}
+    daily = to_long(dict(P=P, V=V, days=days, tickers=tickers))
+    monthly = feats.compute_monthly_momentum_from_daily(daily, lookback_months=12, skip_months=1)
+    arrays = dict(P=P, V=V, day_ns=days.asi8, month_start=ms, month_end_ns=mend.asi8,
+                  tickers=tickers.astype("U"), so=so, mcap=mcap,
+                  pandas_version=np.array(pd.__version__), numpy_version=np.array(np.__version__))
+    for lb in (3, 2, 5):
+        out = feats.compute_monthly_turnover(monthly, shares_info_map=shares, lookback_months=lb)
+        for col in ("adv_est", "shares_outstanding", "turnover_monthly", "turn_avg"):
+            key = col if lb == 3 or col == "turn_avg" else None
+            if key is None:
+                continue
+            arrays[f"lb{lb}_{col}"] = to_dense(out, col, tix, mix, T_m, N)
+        print(f"  turnover lb={lb}: rows={len(out)} "
+              f"valid turn_avg={int(out['turn_avg'].notna().sum())}")
+    np.savez_compressed(OUT / "turnover.npz", **arrays)
+
+
 def main():
     rd, data_io, feats, utils = load_reference()
+    if "--only-turnover" in sys.argv:
+        turnover_case(rd, feats)
+        return
     print("real data ...")
     real_data_case(rd, data_io, feats, utils)
     print("deciles ...")
@@ -272,6 +321,8 @@ def main():
                     nan_month=0.01)
     run_case("longwin", rd, feats, utils, lw["P"], lw["V"], lw["days"], lw["month_start"],
              lw["month_end"], lw["tickers"], [(24, 1), (48, 3)])
+    print("turnover features ...")
+    turnover_case(rd, feats)
 
 
 if __name__ == "__main__":
