@@ -24,7 +24,8 @@ EXPORTS = (
     "csm_momentum_chunked_workspace", "csm_tune", "csm_signal_tiled", "csm_tile_panel",
     "csm_tiled_size", "csm_portfolio", "csm_portfolio_workspace", "csm_bootstrap",
     "csm_cohort_sums", "csm_portfolio_from_cohorts", "csm_turnover_features",
-    "csm_double_sort_labels",
+    "csm_double_sort_labels", "csm_tune_ptr", "csm_next_present",
+    "csm_last_present_month",
 )
 
 
@@ -54,6 +55,9 @@ def _declare(lib):
     sig = {
         "csm_abi_version": (ctypes.c_int, []),
         "csm_tune": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+        "csm_tune_ptr": (ctypes.c_int, [ctypes.c_char_p, _p]),
+        "csm_next_present": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _p, _p]),
+        "csm_last_present_month": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _p]),
         "csm_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
         "csm_destroy": (ctypes.c_int, [_p]),
         "csm_last_error": (ctypes.c_char_p, [_p]),

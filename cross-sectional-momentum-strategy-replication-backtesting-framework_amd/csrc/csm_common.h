@@ -25,6 +25,8 @@ struct csm_ctx {
   int device;
   hipStream_t stream;
   char err[512];
+  void* scratch;          // context-owned device workspace (k_deciles bucket ids), grown lazily
+  size_t scratch_bytes;
 };
 
 static inline int set_err(csm_ctx* c, int code, const char* fmt, ...) {

@@ -561,6 +561,53 @@ void k_signal_mw(
 }
 
 // =====================================================================================
+// Next present month price after a month boundary (the next_pm input of a segment of the
+// fused signal): for each asset, the month price (last valid, NaN if the month has rows but
+// no price) of the first month >= m0 in which it has a daily row; ABSENT if none.  Usually
+// month m0 itself, so one month of daily rows is read.
+// =====================================================================================
+// last_month (nullable): each asset's last month with a daily row (csm_last_present_month,
+// panel metadata computed once at ingestion) -- stops the search at a delisting instead of
+// walking every remaining month.
+__global__ __launch_bounds__(256) void k_next_present(const double* __restrict__ P,
+                                                      const int64_t* __restrict__ month_start,
+                                                      int T_m, int64_t N, int m0,
+                                                      const int32_t* __restrict__ last_month,
+                                                      double* __restrict__ out) {
+  const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (a >= N) return;
+  double res = absent_val();
+  const int mlast = last_month ? last_month[a] : T_m - 1;
+  for (int m = m0; m <= mlast; ++m) {
+    const int64_t d0 = month_start[m], d1 = month_start[m + 1];
+    bool pr = false, v = false;
+    double last = 0.0;
+    for (int64_t d = d0; d < d1; ++d) {
+      const double x = P[d * N + a];
+      pr |= !is_absent(x);
+      const bool ok = x == x;
+      v |= ok;
+      last = ok ? x : last;
+    }
+    if (pr) { res = v ? last : qnan(); break; }
+  }
+  out[a] = res;
+}
+
+// one thread per (asset, month): presence of the month -> atomicMax of the last present month
+__global__ __launch_bounds__(256) void k_last_present_month(const double* __restrict__ P,
+                                                            const int64_t* __restrict__ month_start,
+                                                            int64_t N, int32_t* __restrict__ last) {
+  const int m = blockIdx.y;
+  const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (a >= N) return;
+  const int64_t d0 = month_start[m], d1 = month_start[m + 1];
+  bool pr = false;
+  for (int64_t d = d0; d < d1 && !pr; ++d) pr = !is_absent(P[d * N + a]);
+  if (pr) atomicMax(last + a, m);
+}
+
+// =====================================================================================
 // Kernel C: per-date qcut labels + fused equal-weight decile means (K = 1).
 // One workgroup per date.  Exact order statistics by bucket-select:
 //   pass 1  count / min / max of the ranked values
@@ -574,6 +621,13 @@ void k_signal_mw(
 #define CAP 4096
 #define MAXQ 21  // n_bins + 1 <= 21
 #define MAXT 42  // distinct target ranks (2 per interior quantile + min + max)
+
+// Phase timestamps (profiling aid, csm_tune_ptr("dec_timing", buf)): per date row, wall-clock
+// ticks at DEC_NPH phase boundaries, written by thread 0 when the pointer is set.
+#define DEC_NPH 9
+__device__ __forceinline__ void dec_mark(int64_t* tim, int t, int ph) {
+  if (tim && threadIdx.x == 0) tim[(int64_t)t * DEC_NPH + ph] = (int64_t)wall_clock64();
+}
 
 struct QTab {
   double q[MAXQ];
@@ -637,8 +691,45 @@ __device__ __forceinline__ int vbucket(double x, double lo, double scale) {
 // Row sweep with ROW_U independent 16-B (or 8-B) loads issued per lane before use, so a
 // 512-thread block keeps ROW_U KiB x 8 waves in flight.
 #define ROW_U 8
-template <bool V2, typename F>
+// REV walks the row's blocks from the end: a pass right after a forward pass then re-reads
+// the most recently touched part of the row first, while it is still in the Infinity Cache
+// (all dates' rows together exceed its 256 MB at C4, so the row's head has been evicted).
+template <bool V2, bool REV = false, typename F>
 __device__ __forceinline__ void for_row(const double* __restrict__ row, int64_t N, F&& f) {
+  if (REV) {
+    const int64_t step = (V2 ? 2 : 1) * DEC_THREADS;
+    const int64_t blk = ROW_U * step;
+    const int64_t i0 = (V2 ? 2 : 1) * (int64_t)threadIdx.x;
+    for (int64_t b = (N + blk - 1) / blk - 1; b >= 0; --b) {
+      const int64_t base = b * blk + i0;
+      if (V2) {
+        double2 v[ROW_U];
+#pragma unroll
+        for (int u = 0; u < ROW_U; ++u) {
+          const int64_t i = base + u * step;
+          v[u] = i < N ? *reinterpret_cast<const double2*>(row + i) : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < ROW_U; ++u) {
+          const int64_t i = base + u * step;
+          if (i < N) { f(i, v[u].x); f(i + 1, v[u].y); }
+        }
+      } else {
+        double v[ROW_U];
+#pragma unroll
+        for (int u = 0; u < ROW_U; ++u) {
+          const int64_t i = base + u * step;
+          v[u] = i < N ? row[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < ROW_U; ++u) {
+          const int64_t i = base + u * step;
+          if (i < N) f(i, v[u]);
+        }
+      }
+    }
+    return;
+  }
   if (V2) {
     const int64_t step = 2 * DEC_THREADS;
     int64_t i = 2 * (int64_t)threadIdx.x;
@@ -728,14 +819,20 @@ __device__ __forceinline__ bool slot_member(const Slot& s, int b, uint64_t k) {
   return b == s.b0 && k >= s.klo && k <= s.khi;
 }
 
-template <int NB, bool V2>
+// IDS (N % 4 == 0): the histogram pass also writes each cell's 12-bit bucket id (u16,
+// 0xFFFF = NaN) to a [T_m][N] scratch, and the gather and label passes read the ids (2 B per
+// cell) instead of M (8 B): M is re-read only for the few cells whose bucket holds a target
+// order statistic or a bin edge.  Four cells per lane, loads issued before use.
+template <int NB, bool V2, bool IDS>
 __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __restrict__ Mx,
                                                          const double* __restrict__ NRx,
                                                          int64_t N, int n_bins, QTab qt,
                                                          int8_t* __restrict__ L,
                                                          double* __restrict__ EW,
                                                          int32_t* __restrict__ CNT,
-                                                         int32_t* __restrict__ NV, int ablate) {
+                                                         int32_t* __restrict__ NV, int ablate,
+                                                         int64_t* __restrict__ tim,
+                                                         uint16_t* __restrict__ IDSx) {
   __shared__ DecShared S;
   const int t = blockIdx.x;
   const int tid = threadIdx.x;
@@ -744,6 +841,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
   const double* nrow = NRx ? NRx + (int64_t)t * N : nullptr;
   int8_t* lrow = L + (int64_t)t * N;
 
+  dec_mark(tim, t, 0);
   // ---------------- pass 0: robust bucketing range from a coalesced sample.
   // The histogram below is monotone for ANY [lo, hi] (values outside clamp into the end
   // buckets), so lo/hi need not be the exact extremes: a 0.2 %..99.8 % range of a sample
@@ -800,18 +898,58 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     for (int b2 = tid; b2 < HB; b2 += DEC_THREADS) S.hist[b2] = 0;
     __syncthreads();
   }
+  dec_mark(tim, t, 1);
   // ---------------- pass 1: value-bucket histogram + exact count / min / max
   const double blo = S.vmin, bscale = S.scale;
   {
     int64_t cnt = 0;
     double lo = INFINITY, hi = -INFINITY;
-    for_row<V2>(row, N, [&](int64_t, double x) {
-      const bool ok = x == x;
-      cnt += ok ? 1 : 0;
-      lo = fmin(lo, x);  // fmin / fmax ignore a NaN operand
-      hi = fmax(hi, x);
-      atomicAdd(&S.hist[vbucket(x, blo, bscale)], ok ? 1u : 0u);
-    });
+    if (IDS) {
+      uint16_t* irow = IDSx + (int64_t)t * N;
+      const int64_t step = 4 * DEC_THREADS;
+      constexpr int HU = 4;
+      for (int64_t i0 = 4 * (int64_t)tid; i0 < N; i0 += HU * step) {
+        double2 a[HU], b[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          const int64_t i = i0 + u * step;
+          if (i < N) {
+            a[u] = *reinterpret_cast<const double2*>(row + i);
+            b[u] = *reinterpret_cast<const double2*>(row + i + 2);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          const int64_t i = i0 + u * step;
+          if (i >= N) break;
+          const double xs[4] = {a[u].x, a[u].y, b[u].x, b[u].y};
+          uint32_t id[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const double x = xs[k];
+            const bool ok = x == x;
+            cnt += ok ? 1 : 0;
+            lo = fmin(lo, x);
+            hi = fmax(hi, x);
+            const int bk = vbucket(x, blo, bscale);
+            if (ok) atomicAdd(&S.hist[bk], 1u);
+            id[k] = ok ? (uint32_t)bk : 0xFFFFu;
+          }
+          uint2 pk;
+          pk.x = id[0] | (id[1] << 16);
+          pk.y = id[2] | (id[3] << 16);
+          *reinterpret_cast<uint2*>(irow + i) = pk;
+        }
+      }
+    } else {
+      for_row<V2>(row, N, [&](int64_t, double x) {
+        const bool ok = x == x;
+        cnt += ok ? 1 : 0;
+        lo = fmin(lo, x);  // fmin / fmax ignore a NaN operand
+        hi = fmax(hi, x);
+        atomicAdd(&S.hist[vbucket(x, blo, bscale)], ok ? 1u : 0u);
+      });
+    }
     for (int o = 32; o > 0; o >>= 1) {
       cnt += __shfl_down(cnt, o, 64);
       lo = fmin(lo, __shfl_down(lo, o, 64));
@@ -827,6 +965,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     __syncthreads();
   }
   const int64_t n = S.n;
+  dec_mark(tim, t, 2);
   if (NV && tid == 0) NV[t] = (int32_t)n;
   const bool degenerate = (n == 0) || !(S.vmin < S.vmax);
 
@@ -887,6 +1026,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     }
     __syncthreads();
 
+    dec_mark(tim, t, 3);
     // ---------------- (rare) key-space refinement of the largest slot until all fit.
     // Each refinement shrinks a slot's key range >= 4096x (<= 6 per target before it is a
     // single key), so the bound below is never reached on consistent state.
@@ -981,6 +1121,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
       __syncthreads();
     }
 
+    dec_mark(tim, t, 4);
     // ---------------- pass 3: gather candidates of unresolved slots
     if (tid == 0) {
       int off = 0;
@@ -1000,12 +1141,9 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     if (!(ablate & 2)) {
       const double lo = blo, sc = bscale;
       const int nsl = S.nslot;
-      for_row<V2>(row, N, [&](int64_t, double x) {
-        const uint32_t si = S.hist[vbucket(x, lo, sc)];
-        if (si == 0xFFFFFFFFu || !(x == x)) return;  // common case: not a target bucket
-        const int b = vbucket(x, lo, sc);
+      auto offer = [&](double x, int b) {
         const uint64_t k = dkey(x);
-        for (int i = (int)si; i < nsl && S.slots[i].b0 == b; ++i) {
+        for (int i = (int)S.hist[b]; i < nsl && S.slots[i].b0 == b; ++i) {
           const Slot& s = S.slots[i];
           if (k >= s.klo && k <= s.khi) {
             if (!s.resolved) {
@@ -1015,9 +1153,39 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
             break;
           }
         }
-      });
+      };
+      if (IDS) {
+        const uint16_t* irow = IDSx + (int64_t)t * N;
+        const int64_t step = 4 * DEC_THREADS;
+        constexpr int GU = 8;
+        for (int64_t i0 = 4 * (int64_t)tid; i0 < N; i0 += GU * step) {
+          uint2 pk[GU];
+#pragma unroll
+          for (int u = 0; u < GU; ++u) {
+            const int64_t i = i0 + u * step;
+            pk[u] = i < N ? *reinterpret_cast<const uint2*>(irow + i) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+          }
+#pragma unroll
+          for (int u = 0; u < GU; ++u) {
+            const int64_t i = i0 + u * step;
+            const uint32_t id[4] = {pk[u].x & 0xFFFFu, pk[u].x >> 16, pk[u].y & 0xFFFFu, pk[u].y >> 16};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              if (id[k] == 0xFFFFu || S.hist[id[k]] == 0xFFFFFFFFu) continue;  // not a target bucket
+              offer(row[i + k], (int)id[k]);   // exact value: re-read M for this cell only
+            }
+          }
+        }
+      } else {
+        for_row<V2, true>(row, N, [&](int64_t, double x) {
+          const uint32_t si = S.hist[vbucket(x, lo, sc)];
+          if (si == 0xFFFFFFFFu || !(x == x)) return;  // common case: not a target bucket
+          offer(x, vbucket(x, lo, sc));
+        });
+      }
     }
     __syncthreads();
+    dec_mark(tim, t, 5);
     // ---------------- order statistics inside the slots.  Small slots (the usual case: a
     // few dozen members each) use counting selection: the member whose rank inside its slot
     // (ties broken by position) equals the target's residual rank is the order statistic --
@@ -1079,6 +1247,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
       }
     }
     __syncthreads();
+    dec_mark(tim, t, 6);
     // ---------------- edges (NumPy _lerp) and duplicates='drop'
     if (tid == 0) {
       auto order_stat = [&](int64_t r) -> double {
@@ -1131,6 +1300,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
     __syncthreads();
   }
 
+  dec_mark(tim, t, 7);
   // ---------------- pass 4: labels + equal-weight accumulation
   // Labels come from the bucket table; only values in a bucket that holds an edge are
   // compared against the edges.  Per lane the next_ret sums are plain fp64 (a few dozen
@@ -1165,6 +1335,59 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
   };
   if (ablate & 4) {
     // profiling ablation: no label pass
+  } else if (IDS) {
+    // label from the bucket id; exact comparison (re-reading M) only in edge buckets.  The
+    // decile sums use a one-hot fma per label (fma(1, r, s) rounds like s + r, fma(0, r, s)
+    // is s) and integer counts.
+    const uint16_t* irow = IDSx + (int64_t)t * N;
+    const int64_t step = 4 * DEC_THREADS;
+    constexpr int LU4 = 2;
+    for (int64_t i0 = 4 * (int64_t)tid; i0 < N; i0 += LU4 * step) {
+      uint2 pk[LU4];
+      double2 ra[LU4], rb[LU4];
+#pragma unroll
+      for (int u = 0; u < LU4; ++u) {
+        const int64_t i = i0 + u * step;
+        if (i < N) {
+          pk[u] = *reinterpret_cast<const uint2*>(irow + i);
+          if (NB > 0 && nrow) {
+            ra[u] = *reinterpret_cast<const double2*>(nrow + i);
+            rb[u] = *reinterpret_cast<const double2*>(nrow + i + 2);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < LU4; ++u) {
+        const int64_t i = i0 + u * step;
+        if (i >= N) break;
+        const uint32_t id[4] = {pk[u].x & 0xFFFFu, pk[u].x >> 16, pk[u].y & 0xFFFFu, pk[u].y >> 16};
+        int lab[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          int l = (id[k] == 0xFFFFu || nb == 0) ? -1 : (int)S.blab[id[k]];
+          if (l == -2) l = label_of(row[i + k]);
+          lab[k] = l;
+        }
+        char4 lv;
+        lv.x = (char)lab[0]; lv.y = (char)lab[1]; lv.z = (char)lab[2]; lv.w = (char)lab[3];
+        *reinterpret_cast<char4*>(lrow + i) = lv;
+        if (NB > 0 && nrow && !(ablate & 1)) {
+          const double rs[4] = {ra[u].x, ra[u].y, rb[u].x, rb[u].y};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool ok = lab[k] >= 0 && rs[k] == rs[k];
+            const int lb = ok ? lab[k] : -1;
+            const double r = ok ? rs[k] : 0.0;
+#pragma unroll
+            for (int d = 0; d < NB; ++d) {
+              const bool h = lb == d;
+              hs[d] = fma(h ? 1.0 : 0.0, r, hs[d]);
+              cn[d] += h ? 1 : 0;
+            }
+          }
+        }
+      }
+    }
   } else if (V2) {
     const int64_t step = 2 * DEC_THREADS;
     int64_t i = 2 * (int64_t)tid;
@@ -1203,6 +1426,7 @@ __global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __rest
       if (NB > 0 && nrow && l0 >= 0) accumulate(l0, nrow[i]);
     }
   }
+  dec_mark(tim, t, 8);
   if (NB > 0 && nrow && EW) {
     // deterministic block reduction: wave shfl_down tree, then waves in order
     __shared__ double wh[DEC_THREADS / 64][NB > 0 ? NB : 1], wl[DEC_THREADS / 64][NB > 0 ? NB : 1];
@@ -1464,7 +1688,11 @@ static int g_tune_dec_ablate = 0;      // k_deciles pass ablation bitmask (profi
 static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<.., NW, NB>
 static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
 static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
-static int g_tune_month_end_rows = 0;  // >0: csm_month_end uses k_month_end_rows (value = max month days)
+static int g_tune_month_end_rows = 0;
+static int64_t* g_dec_timing = nullptr;
+// k_deciles bucket-id scratch path (N % 4 == 0): 1 on, 0 off.  Off by default: it moves
+// fewer bytes but measured slower at C4 (0.44 vs 0.40 ms, profiles/r01/experiments).
+static int g_tune_dec_ids = 0;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
 
 extern "C" {
 
@@ -1475,11 +1703,18 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_nbuf") && (value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
   if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
+  if (!strcmp(key, "dec_ids") && (value == 0 || value == 1)) { g_tune_dec_ids = value; return CSM_OK; }
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
   if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
   if (!strcmp(key, "signal_mw") && (value == 0 || value == 21 || value == 22 || value == 41 ||
                                     value == 42)) { g_tune_signal_mw = value; return CSM_OK; }
+  return CSM_E_INVAL;
+}
+
+int csm_tune_ptr(const char* key, void* p) {
+  if (!key) return CSM_E_INVAL;
+  if (!strcmp(key, "dec_timing")) { g_dec_timing = (int64_t*)p; return CSM_OK; }
   return CSM_E_INVAL;
 }
 
@@ -1498,6 +1733,10 @@ int csm_create(int device, csm_ctx** out) {
 }
 
 int csm_destroy(csm_ctx* ctx) {
+  if (ctx && ctx->scratch) {
+    hipSetDevice(ctx->device);
+    hipFree(ctx->scratch);
+  }
   free(ctx);
   return CSM_OK;
 }
@@ -1666,6 +1905,34 @@ int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
                        max_month_days, J, skip, PM, R, M, NR, carry, next_pm, carry_out);
 }
 
+int csm_last_present_month(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                           const int64_t* month_start, int32_t T_m, int32_t* last_month) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !last_month || N <= 0 || T_d < 0 || T_m < 0 || T_m > 65535)
+    return set_err(ctx, CSM_E_INVAL, "csm_last_present_month: bad arguments");
+  HIP_CHECK(ctx, hipMemsetAsync(last_month, 0xFF, (size_t)N * sizeof(int32_t), ctx->stream));  // -1
+  if (T_m == 0) return CSM_OK;
+  hipLaunchKernelGGL(k_last_present_month, dim3((unsigned)((N + 255) / 256), (unsigned)T_m),
+                     dim3(256), 0, ctx->stream, P, month_start, N, last_month);
+  LAUNCH_CHECK(ctx, "k_last_present_month");
+  return CSM_OK;
+}
+
+int csm_next_present(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                     const int64_t* month_start, int32_t T_m, int32_t m0,
+                     const int32_t* last_month, double* next_pm) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !next_pm || N <= 0 || T_d < 0 || T_m < 0 || m0 < 0 || m0 > T_m)
+    return set_err(ctx, CSM_E_INVAL, "csm_next_present: bad arguments (N=%lld T_m=%d m0=%d)",
+                   (long long)N, T_m, m0);
+  hipLaunchKernelGGL(k_next_present, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream,
+                     P, month_start, T_m, N, m0, last_month, next_pm);
+  LAUNCH_CHECK(ctx, "k_next_present");
+  return CSM_OK;
+}
+
 int64_t csm_tiled_size(int64_t T_d, int64_t N) {
   if (T_d < 0 || N <= 0) return 0;
   return ((N + CSM_TILE - 1) / CSM_TILE) * T_d * CSM_TILE;
@@ -1691,10 +1958,12 @@ int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double
 template <int NB>
 static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                           int32_t* CNT, int32_t* NV) {
+                           int32_t* CNT, int32_t* NV, uint16_t* ids) {
   const int ab = g_tune_dec_ablate;
-  if (v2) hipLaunchKernelGGL((k_deciles<NB, true>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab);
-  else hipLaunchKernelGGL((k_deciles<NB, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab);
+  int64_t* tm = g_dec_timing;
+  if (ids) hipLaunchKernelGGL((k_deciles<NB, true, true>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+  else if (v2) hipLaunchKernelGGL((k_deciles<NB, true, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+  else hipLaunchKernelGGL((k_deciles<NB, false, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
 }
 
 extern "C" {
@@ -1713,16 +1982,28 @@ int csm_deciles(csm_ctx* ctx, const double* M, const double* NR, int32_t T_m, in
   QTab q;
   for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
   const bool v2 = (N % 2 == 0) && aligned16(M) && (!NR || aligned16(NR)) && (((uintptr_t)L & 1u) == 0);
+  uint16_t* ids = nullptr;
+  if (g_tune_dec_ids && N % 4 == 0 && v2 && (((uintptr_t)L & 3u) == 0)) {
+    const size_t need = (size_t)T_m * (size_t)N * sizeof(uint16_t);
+    if (ctx->scratch_bytes < need) {
+      if (ctx->scratch) HIP_CHECK(ctx, hipFree(ctx->scratch));
+      ctx->scratch = nullptr;
+      ctx->scratch_bytes = 0;
+      HIP_CHECK(ctx, hipMalloc(&ctx->scratch, need));
+      ctx->scratch_bytes = need;
+    }
+    ids = (uint16_t*)ctx->scratch;
+  }
   if (!NR) {
-    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV);
+    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids);
   } else {
     switch (n_bins) {
-      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
-      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
-      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
-      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
-      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
-      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV); break;
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
       default:
         return set_err(ctx, CSM_E_INVAL, "csm_deciles: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", n_bins);
     }

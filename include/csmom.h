@@ -43,6 +43,9 @@ int csm_abi_version(void);
  * that SKIPS decile passes and so produces wrong results).  Returns CSM_E_INVAL for an
  * unknown key or value. */
 int csm_tune(const char* key, int value);
+/* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
+ * wall-clock ticks (100 MHz) at its phase boundaries (NULL switches it off). */
+int csm_tune_ptr(const char* key, void* p);
 
 /* Create a context bound to HIP device `device` (stream = the null stream). */
 int csm_create(int device, csm_ctx** out);
@@ -106,6 +109,20 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
                int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, double* PM,
                double* R, double* M, double* NR, const double* carry, const double* next_pm,
                double* carry_out);
+
+/*
+ * next_pm[N] for a month boundary m0: the month price of each asset's first present month
+ * >= m0 (ABSENT if none).  With csm_signal's carry_out / carry this splits the fused pass into
+ * month segments that chain bit for bit (so per-date ranking of early segments can overlap
+ * the signal of later ones).
+ */
+int csm_next_present(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                     const int64_t* month_start, int32_t T_m, int32_t m0,
+                     const int32_t* last_month, double* next_pm);
+/* Panel metadata for csm_next_present (nullable there): each asset's last month with a
+ * daily row, -1 if none (one pass over the panel, computed once when it is loaded). */
+int csm_last_present_month(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                           const int64_t* month_start, int32_t T_m, int32_t* last_month);
 
 /*
  * Asset-tiled daily panel (the engine's preferred HBM layout for the signal pass):

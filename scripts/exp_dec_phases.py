@@ -1,0 +1,48 @@
+"""Where k_deciles spends its time on C4: per-date phase durations from the in-kernel
+wall-clock marks (csm_tune_ptr("dec_timing")).  Dev tool: prints one JSON line."""
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import csmom  # noqa: E402
+from csmom.synth import bday_calendar, make_device_panel  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+TD = 10_000
+days, ms, _ = bday_calendar("1985-01-01", TD)
+pan = make_device_panel(N, days, ms, seed=4, device="cuda:0")
+eng = csmom.Engine(0)
+T_m = len(ms) - 1
+maxd = int(np.diff(ms).max())
+M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
+L = eng.empty((T_m, N), torch.int8)
+EW, CNT = eng.empty((T_m, 10)), eng.empty((T_m, 10), torch.int32)
+eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
+for _ in range(3):
+    eng.deciles(M, NR, 10, out=(L, EW, CNT, None))
+tim = torch.full((T_m, 9), -1, dtype=torch.int64, device="cuda:0")
+eng.lib.csm_tune_ptr(b"dec_timing", ctypes.c_void_p(tim.data_ptr()))
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+eng.deciles(M, NR, 10, out=(L, EW, CNT, None))
+e1.record()
+torch.cuda.synchronize()
+eng.lib.csm_tune_ptr(b"dec_timing", None)
+t = tim.cpu().numpy().astype(np.float64) / 100.0   # 100 MHz ticks -> us
+ok = (tim.cpu().numpy() >= 0).all(axis=1)
+t = t[ok]
+names = ["sample", "histogram", "targets", "refine", "gather", "select", "edges+table",
+         "labels+sums", ]
+d = np.diff(t, axis=1)
+out = {"N": N, "rows_timed": int(ok.sum()), "kernel_ms": round(e0.elapsed_time(e1), 4),
+       "phase_us_mean": {n: round(float(d[:, i].mean()), 2) for i, n in enumerate(names)},
+       "phase_us_max": {n: round(float(d[:, i].max()), 2) for i, n in enumerate(names)},
+       "row_us_mean": round(float((t[:, -1] - t[:, 0]).mean()), 2),
+       "start_spread_us": round(float(t[:, 0].max() - t[:, 0].min()), 2),
+       "span_us": round(float(t[:, -1].max() - t[:, 0].min()), 2)}
+print(json.dumps(out), flush=True)

@@ -35,7 +35,7 @@ for rnd in range(5):
 tune("signal_vec", 2); tune("signal_nbuf", 3)
 eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
 print(json.dumps({'k_signal_ms': {f'vec{v}_nbuf{b}': round(float(np.median(t)), 4) for (v, b), t in sig.items()}}), flush=True)
-abl = {a: [] for a in (0, 1, 2, 4, 1 | 2 | 4)}
+abl = {a: [] for a in (0, 1, 2, 4, 1 | 2 | 4, 8, 1 | 2 | 4 | 8)}
 for rnd in range(5):
     for a in abl:
         tune("dec_ablate", a)
@@ -46,5 +46,5 @@ tune("dec_ablate", 0)
 out = {"N": N, "T_d": TD,
        "k_signal_ms": {f"vec{v}_nbuf{b}": round(float(np.median(t)), 4) for (v, b), t in sig.items()},
        "k_deciles_ms": {f"ablate{a}": round(float(np.median(t)), 4) for a, t in abl.items()},
-       "ablate_bits": "1 no accumulate, 2 no gather pass, 4 no label pass"}
+       "ablate_bits": "1 no accumulate, 2 no gather pass, 4 no label pass, 8 no histogram atomics"}
 print(json.dumps(out))

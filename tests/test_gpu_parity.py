@@ -284,3 +284,40 @@ def test_fused_rejects_long_months(engine):
     ms2 = torch.tensor([0, 40], dtype=torch.int64, device="cuda:0")
     with pytest.raises(csmom.CsmError):
         engine.signal(P2, ms2, 40)       # month longer than 32 days
+
+
+@pytest.mark.parametrize("name", ["edge", "c1"])
+def test_deciles_bucket_id_path_equals_direct(engine, name):
+    """The bucket-id scratch path (N % 4 == 0) and the direct path give the same labels and
+    counts, and decile means equal to rounding."""
+    z = load_golden(name)
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    _, M, NR = engine.momentum(PM, 12, 1)
+    lib = engine.lib
+    a = engine.deciles(M, NR, 10, with_nv=True)
+    try:
+        assert lib.csm_tune(b"dec_ids", 1) == 0
+        b = engine.deciles(M, NR, 10, with_nv=True)
+    finally:
+        lib.csm_tune(b"dec_ids", 0)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+    ea, eb = a[1].cpu().numpy(), b[1].cpu().numpy()
+    assert np.array_equal(np.isnan(ea), np.isnan(eb)) and max_rel(ea, eb) <= 1e-13
+
+
+@pytest.mark.parametrize("segments", [1, 2, 3, 7])
+def test_segmented_overlapped_pass_bit_identical(engine, segments):
+    """run_segmented (signal segments chained by carry + next_pm, ranking of segment g-1 on
+    a side stream) equals the one-shot fused pass bit for bit."""
+    z = load_golden("edge")
+    ms_h = z["month_start"].astype(np.int64)
+    P, ms = _up(z["P"]), _up(ms_h)
+    maxd = int(np.diff(ms_h).max())
+    ref = engine.run(P, ms, 12, 1, 10, max_month_days=maxd, fused=True)
+    plan = engine.segmented_plan(P, ms_h, 12, 1, segments)
+    M, NR, L, EW, CNT, LS = engine.run_segmented(P, ms, plan, 12, 1, 10)
+    torch.cuda.synchronize()
+    for a, b in ((M, ref.M), (NR, ref.NR), (EW, ref.EW), (LS, ref.LS)):
+        assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+    assert torch.equal(L, ref.L) and torch.equal(CNT, ref.CNT)
+    assert np.array_equal(L.cpu().numpy(), z["J12s1_L"])
