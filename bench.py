@@ -76,6 +76,47 @@ def cpu_baseline(n_assets: int, days: int, start: str):
                        f"{n_assets} assets x {days} bdays, one pass {dt:.1f} s")
 
 
+def cpu_baseline_sweep(config: str, n_assets: int, days: int, start: str):
+    """The CPU oracles (NumPy ports: month-end, scan, qcut, portfolio rules E1-E6) on a bounded
+    sample of the sweep workload, one host thread, in the same unit as the GPU line."""
+    from oracle import csmom_oracle as O
+    from oracle import portfolio_oracle as PO
+    from oracle.synth_np import make_panel
+
+    pan = make_panel(n_assets, days, seed=3, start=start, with_volume=False)
+    Js = Ks = (3, 6, 9, 12)
+    t0 = time.perf_counter()
+    PM, _ = O.month_end(pan["P"], pan["month_start"])
+    T_m = PM.shape[0]
+    if config == "c3":
+        with np.errstate(invalid="ignore"):
+            W = np.abs(PM) * 1e6
+        for J in Js:
+            _, M, NR, _ = O.momentum_scan(PM, J, 1)
+            L = O.assign_deciles(M, 10)
+            for K in Ks:
+                PO.portfolio(L, NR, 10, K=K, W=W)
+        dt = time.perf_counter() - t0
+        return dict(value=n_assets * days * len(Js) * len(Ks) / dt, unit="asset-day-strategies/s",
+                    cores=1, kind="port",
+                    sample=f"oracle month-end + 4 scans + 4 qcut + 16 VW portfolios (E1-E5) on "
+                           f"{n_assets} assets x {days} bdays, {dt:.1f} s")
+    R, _, _, _ = O.momentum_scan(PM, 12, 1)
+    t0 = time.perf_counter()
+    B = 2
+    pmb = PO.bootstrap_panel(R, PO.bootstrap_indices(T_m, B, 5000, 6.0)).reshape(T_m, B * n_assets)
+    for J in Js:
+        _, M, NR, _ = O.momentum_scan(pmb, J, 1)
+        L = O.assign_deciles(M.reshape(T_m * B, n_assets), 10).reshape(T_m, B, n_assets)
+        for K in Ks:
+            PO.portfolio(L, NR.reshape(T_m, B, n_assets), 10, K=K)
+    dt = time.perf_counter() - t0
+    return dict(value=n_assets * T_m * B * len(Js) * len(Ks) / dt,
+                unit="asset-month-strategies/s", cores=1, kind="port",
+                sample=f"oracle bootstrap + 4 scans + 4 qcut + 16 portfolios with turnover/costs "
+                       f"on {B} panels x {n_assets} assets x {T_m} months, {dt:.1f} s")
+
+
 def main():
     args = parse()
     if args.config in SWEEP_CONFIGS:
@@ -448,6 +489,9 @@ def sweep_main(args):
             "result_means": res_summary,
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_sweep(args.config, 500 if args.config == "c3" else 300,
+                                                      T_d, cfg["start"])
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -60,3 +60,22 @@ static inline int prep(csm_ctx* c) {
 }
 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ---- shared by the decile kernels (csmom.hip and deciles_narrow.hip) -------------------------
+#define MAXQ 21  // n_bins + 1 <= 21
+#define MAXT 42  // distinct target ranks (2 per interior quantile + min + max)
+// Phase timestamps (profiling aid, csm_tune_ptr("dec_timing", buf)): per date row, wall-clock
+// ticks at DEC_NPH phase boundaries, written by thread 0 when the pointer is set.
+#define DEC_NPH 9
+__device__ __forceinline__ void dec_mark(int64_t* tim, int t, int ph) {
+  if (tim && threadIdx.x == 0) tim[(int64_t)t * DEC_NPH + ph] = (int64_t)wall_clock64();
+}
+struct QTab {
+  double q[MAXQ];
+};
+
+// narrow-row decile launcher (deciles_narrow.hip), NB in {0,2,3,4,5,10,20}
+template <int NB>
+void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
+                           int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
+                           int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);

@@ -608,861 +608,18 @@ __global__ __launch_bounds__(256) void k_last_present_month(const double* __rest
 }
 
 // =====================================================================================
-// Kernel C: per-date qcut labels + fused equal-weight decile means (K = 1).
-// One workgroup per date.  Exact order statistics by bucket-select:
-//   pass 1  count / min / max of the ranked values
-//   pass 2  4096-bucket histogram, linear in value over [min, max] (monotone bucketing)
-//   (rare)  oversized target buckets are refined in key space (order-preserving u64 keys)
-//   pass 3  gather the target buckets' members into LDS, bitonic sort, read ranks
-//   pass 4  edges (NumPy lerp) -> dedupe -> labels; accumulate next_ret per label
+// Kernel C: per-date qcut labels + fused decile means (csrc/deciles.inc, wide-row variant).
 // =====================================================================================
 #define DEC_THREADS 512
 #define HB 4096
 #define CAP 4096
-#define MAXQ 21  // n_bins + 1 <= 21
-#define MAXT 42  // distinct target ranks (2 per interior quantile + min + max)
-
-// Phase timestamps (profiling aid, csm_tune_ptr("dec_timing", buf)): per date row, wall-clock
-// ticks at DEC_NPH phase boundaries, written by thread 0 when the pointer is set.
-#define DEC_NPH 9
-__device__ __forceinline__ void dec_mark(int64_t* tim, int t, int ph) {
-  if (tim && threadIdx.x == 0) tim[(int64_t)t * DEC_NPH + ph] = (int64_t)wall_clock64();
-}
-
-struct QTab {
-  double q[MAXQ];
-};
-
-__device__ __forceinline__ uint64_t dkey(double x) {
-  const uint64_t b = (uint64_t)__double_as_longlong(x + 0.0);  // -0.0 -> +0.0
-  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
-}
-__device__ __forceinline__ double dval(uint64_t k) {
-  const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
-  return __longlong_as_double((long long)b);
-}
-
-struct Slot {
-  uint64_t klo, khi;  // key interval (inclusive) inside value bucket b0
-  int b0;
-  int count;          // members
-  int off;            // candidate offset
-  int resolved;       // all members share one key -> value known
-  double value;
-};
-
-struct DecShared {
-  uint32_t hist[HB];
-  double cand[CAP];
-  Slot slots[MAXT];
-  int64_t trank[MAXT];  // target ranks (sorted, distinct)
-  int64_t tres[MAXT];   // residual rank inside its slot
-  int tslot[MAXT];
-  double tval[MAXT];
-  int nslot, ntgt, total;
-  double vmin, vmax, scale;
-  uint64_t kmin_r, kmax_r;
-  double bins[MAXQ];
-  int nbins;
-  int64_t n;
-  int fill[MAXT];
-  Slot slots2[MAXT];
-  int remap[MAXT];
-  int vbe[MAXQ];          // bucket of each bin edge
-  int8_t blab[HB];        // bucket -> label (-1 NaN label, -2 bucket holds an edge: compare exactly)
-  double e[MAXQ], u[MAXQ];
-  // reduction scratch
-  double red_d[DEC_THREADS / 64][2];
-  unsigned long long red_k[DEC_THREADS / 64][2];
-  int64_t red_n[DEC_THREADS / 64];
-  int red_n2[DEC_THREADS / 64][2];
-  int tpre[MAXT + 1];   // prefix of unresolved member counts over the targets
-  int sel_count;        // 1: counting selection, 0: bitonic sort
-};
-
-// Monotone non-decreasing in x for any lo / scale (values outside [lo, lo + HB/scale)
-// clamp into the end buckets), so bucket order never contradicts value order.  Branch-free:
-// fmax/fmin clamp (NaN -> bucket 0; callers never count NaN), truncation = floor on [0, HB).
-__device__ __forceinline__ int vbucket(double x, double lo, double scale) {
-  const double f = fmin(fmax((x - lo) * scale, 0.0), (double)(HB - 1));
-  return (int)f;
-}
-
-// Row sweep with ROW_U independent 16-B (or 8-B) loads issued per lane before use, so a
-// 512-thread block keeps ROW_U KiB x 8 waves in flight.
-#define ROW_U 8
-// REV walks the row's blocks from the end: a pass right after a forward pass then re-reads
-// the most recently touched part of the row first, while it is still in the Infinity Cache
-// (all dates' rows together exceed its 256 MB at C4, so the row's head has been evicted).
-template <bool V2, bool REV = false, typename F>
-__device__ __forceinline__ void for_row(const double* __restrict__ row, int64_t N, F&& f) {
-  if (REV) {
-    const int64_t step = (V2 ? 2 : 1) * DEC_THREADS;
-    const int64_t blk = ROW_U * step;
-    const int64_t i0 = (V2 ? 2 : 1) * (int64_t)threadIdx.x;
-    for (int64_t b = (N + blk - 1) / blk - 1; b >= 0; --b) {
-      const int64_t base = b * blk + i0;
-      if (V2) {
-        double2 v[ROW_U];
-#pragma unroll
-        for (int u = 0; u < ROW_U; ++u) {
-          const int64_t i = base + u * step;
-          v[u] = i < N ? *reinterpret_cast<const double2*>(row + i) : make_double2(0.0, 0.0);
-        }
-#pragma unroll
-        for (int u = 0; u < ROW_U; ++u) {
-          const int64_t i = base + u * step;
-          if (i < N) { f(i, v[u].x); f(i + 1, v[u].y); }
-        }
-      } else {
-        double v[ROW_U];
-#pragma unroll
-        for (int u = 0; u < ROW_U; ++u) {
-          const int64_t i = base + u * step;
-          v[u] = i < N ? row[i] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < ROW_U; ++u) {
-          const int64_t i = base + u * step;
-          if (i < N) f(i, v[u]);
-        }
-      }
-    }
-    return;
-  }
-  if (V2) {
-    const int64_t step = 2 * DEC_THREADS;
-    int64_t i = 2 * (int64_t)threadIdx.x;
-    for (; i + (ROW_U - 1) * step < N; i += ROW_U * step) {
-      double2 v[ROW_U];
-#pragma unroll
-      for (int u = 0; u < ROW_U; ++u) v[u] = *reinterpret_cast<const double2*>(row + i + u * step);
-#pragma unroll
-      for (int u = 0; u < ROW_U; ++u) { f(i + u * step, v[u].x); f(i + u * step + 1, v[u].y); }
-    }
-    for (; i < N; i += step) {
-      const double2 t = *reinterpret_cast<const double2*>(row + i);
-      f(i, t.x);
-      f(i + 1, t.y);
-    }
-  } else {
-    const int64_t step = DEC_THREADS;
-    int64_t i = threadIdx.x;
-    for (; i + (ROW_U - 1) * step < N; i += ROW_U * step) {
-      double v[ROW_U];
-#pragma unroll
-      for (int u = 0; u < ROW_U; ++u) v[u] = row[i + u * step];
-#pragma unroll
-      for (int u = 0; u < ROW_U; ++u) f(i + u * step, v[u]);
-    }
-    for (; i < N; i += step) f(i, row[i]);
-  }
-}
-
-__device__ __forceinline__ double wave_sum_d(double v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  return v;
-}
-
-// Block-wide (min, max) and (sum, sum) over DEC_THREADS; every thread gets the results.
-// Two barriers each (the scratch is reusable on return).
-__device__ __forceinline__ void block_minmax(double mn, double mx, double& gmn, double& gmx,
-                                             double (*scr)[2]) {
-  for (int o = 32; o > 0; o >>= 1) {
-    mn = fmin(mn, __shfl_down(mn, o, 64));
-    mx = fmax(mx, __shfl_down(mx, o, 64));
-  }
-  if ((threadIdx.x & 63) == 0) { scr[threadIdx.x >> 6][0] = mn; scr[threadIdx.x >> 6][1] = mx; }
-  __syncthreads();
-  gmn = INFINITY; gmx = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < DEC_THREADS / 64; ++w) { gmn = fmin(gmn, scr[w][0]); gmx = fmax(gmx, scr[w][1]); }
-  __syncthreads();
-}
-__device__ __forceinline__ void block_sum2(int a, int b, int& ga, int& gb, int (*scr)[2]) {
-  for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
-  if ((threadIdx.x & 63) == 0) { scr[threadIdx.x >> 6][0] = a; scr[threadIdx.x >> 6][1] = b; }
-  __syncthreads();
-  ga = 0; gb = 0;
-#pragma unroll
-  for (int w = 0; w < DEC_THREADS / 64; ++w) { ga += scr[w][0]; gb += scr[w][1]; }
-  __syncthreads();
-}
-
-// Exclusive scan of hist[HB] in place (hist[b] becomes the count of buckets < b): per-thread
-// sums of 8 consecutive buckets, a wave scan by shuffles, then the wave totals.  Two barriers.
-__device__ void block_exclusive_scan_hist(uint32_t* hist) {
-  __shared__ uint32_t wtot[DEC_THREADS / 64];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  constexpr int per = HB / DEC_THREADS;  // 8
-  uint32_t loc[per];
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < per; ++j) { loc[j] = hist[tid * per + j]; s += loc[j]; }
-  uint32_t inc = s;  // inclusive wave scan
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  if (lane == 63) wtot[wid] = inc;
-  __syncthreads();
-  uint32_t run = inc - s;
-  for (int w = 0; w < wid; ++w) run += wtot[w];
-#pragma unroll
-  for (int j = 0; j < per; ++j) { hist[tid * per + j] = run; run += loc[j]; }
-  __syncthreads();
-}
-
-// member test for a slot (value bucket b0 and key interval)
-__device__ __forceinline__ bool slot_member(const Slot& s, int b, uint64_t k) {
-  return b == s.b0 && k >= s.klo && k <= s.khi;
-}
-
-// IDS (N % 4 == 0): the histogram pass also writes each cell's 12-bit bucket id (u16,
-// 0xFFFF = NaN) to a [T_m][N] scratch, and the gather and label passes read the ids (2 B per
-// cell) instead of M (8 B): M is re-read only for the few cells whose bucket holds a target
-// order statistic or a bin edge.  Four cells per lane, loads issued before use.
-template <int NB, bool V2, bool IDS>
-__global__ __launch_bounds__(DEC_THREADS, 4) void k_deciles(const double* __restrict__ Mx,
-                                                         const double* __restrict__ NRx,
-                                                         int64_t N, int n_bins, QTab qt,
-                                                         int8_t* __restrict__ L,
-                                                         double* __restrict__ EW,
-                                                         int32_t* __restrict__ CNT,
-                                                         int32_t* __restrict__ NV, int ablate,
-                                                         int64_t* __restrict__ tim,
-                                                         uint16_t* __restrict__ IDSx) {
-  __shared__ DecShared S;
-  const int t = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-  const double* row = Mx + (int64_t)t * N;
-  const double* nrow = NRx ? NRx + (int64_t)t * N : nullptr;
-  int8_t* lrow = L + (int64_t)t * N;
-
-  dec_mark(tim, t, 0);
-  // ---------------- pass 0: robust bucketing range from a coalesced sample.
-  // The histogram below is monotone for ANY [lo, hi] (values outside clamp into the end
-  // buckets), so lo/hi need not be the exact extremes: a 0.2 %..99.8 % range of a sample
-  // keeps heavy momentum tails from squeezing the bulk into a few buckets.  The exact
-  // count / min / max come out of the histogram pass itself.
-  {
-    // 32 chunks x 64 consecutive assets, 4 samples per thread held in registers.  The
-    // (ns * 2 / 1000)-th smallest and largest samples are found by extracting the distinct
-    // minima / maxima in rounds (each round takes every copy of a value): <= 5 rounds of two
-    // block reductions instead of sorting the sample.
-    constexpr int SCH = 32, PER = SCH * 64 / DEC_THREADS;
-    double xs[PER];
-    int nloc = 0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int c = (tid >> 6) + k * (DEC_THREADS / 64);
-      const int64_t start = (N <= SCH * 64) ? (int64_t)c * 64 : ((int64_t)c * (N - 64)) / (SCH - 1);
-      const int64_t i = start + lane;
-      xs[k] = (i < N) ? row[i] : qnan();
-      nloc += (xs[k] == xs[k]) ? 1 : 0;
-    }
-    int ns, dummy;
-    block_sum2(nloc, 0, ns, dummy, S.red_n2);
-    double lo = 0.0, hi = 0.0;
-    if (ns >= 2) {
-      const int idx = (ns * 2) / 1000;
-      double cur_lo = -INFINITY, cur_hi = INFINITY;
-      int below = 0, above = 0;
-      bool lo_done = false, hi_done = false;
-      while (!(lo_done && hi_done)) {  // block-uniform
-        double mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-          const double x = xs[k];
-          if (x > cur_lo) mn = fmin(mn, x);
-          if (x < cur_hi) mx = fmax(mx, x);
-        }
-        double gmn, gmx;
-        block_minmax(mn, mx, gmn, gmx, S.red_d);
-        int c1 = 0, c2 = 0;
-#pragma unroll
-        for (int k = 0; k < PER; ++k) { c1 += xs[k] == gmn ? 1 : 0; c2 += xs[k] == gmx ? 1 : 0; }
-        int g1, g2;
-        block_sum2(c1, c2, g1, g2, S.red_n2);
-        if (!lo_done) { if (below + g1 > idx) { lo = gmn; lo_done = true; } else { below += g1; cur_lo = gmn; } }
-        if (!hi_done) { if (above + g2 > idx) { hi = gmx; hi_done = true; } else { above += g2; cur_hi = gmx; } }
-      }
-    }
-    if (tid == 0) {
-      const double rng = hi - lo;
-      S.vmin = lo;
-      S.scale = (rng > 0.0 && rng <= 1.0e300) ? (double)HB / rng : 0.0;
-    }
-    for (int b2 = tid; b2 < HB; b2 += DEC_THREADS) S.hist[b2] = 0;
-    __syncthreads();
-  }
-  dec_mark(tim, t, 1);
-  // ---------------- pass 1: value-bucket histogram + exact count / min / max
-  const double blo = S.vmin, bscale = S.scale;
-  {
-    int64_t cnt = 0;
-    double lo = INFINITY, hi = -INFINITY;
-    if (IDS) {
-      uint16_t* irow = IDSx + (int64_t)t * N;
-      const int64_t step = 4 * DEC_THREADS;
-      constexpr int HU = 4;
-      for (int64_t i0 = 4 * (int64_t)tid; i0 < N; i0 += HU * step) {
-        double2 a[HU], b[HU];
-#pragma unroll
-        for (int u = 0; u < HU; ++u) {
-          const int64_t i = i0 + u * step;
-          if (i < N) {
-            a[u] = *reinterpret_cast<const double2*>(row + i);
-            b[u] = *reinterpret_cast<const double2*>(row + i + 2);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < HU; ++u) {
-          const int64_t i = i0 + u * step;
-          if (i >= N) break;
-          const double xs[4] = {a[u].x, a[u].y, b[u].x, b[u].y};
-          uint32_t id[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const double x = xs[k];
-            const bool ok = x == x;
-            cnt += ok ? 1 : 0;
-            lo = fmin(lo, x);
-            hi = fmax(hi, x);
-            const int bk = vbucket(x, blo, bscale);
-            if (ok) atomicAdd(&S.hist[bk], 1u);
-            id[k] = ok ? (uint32_t)bk : 0xFFFFu;
-          }
-          uint2 pk;
-          pk.x = id[0] | (id[1] << 16);
-          pk.y = id[2] | (id[3] << 16);
-          *reinterpret_cast<uint2*>(irow + i) = pk;
-        }
-      }
-    } else {
-      for_row<V2>(row, N, [&](int64_t, double x) {
-        const bool ok = x == x;
-        cnt += ok ? 1 : 0;
-        lo = fmin(lo, x);  // fmin / fmax ignore a NaN operand
-        hi = fmax(hi, x);
-        atomicAdd(&S.hist[vbucket(x, blo, bscale)], ok ? 1u : 0u);
-      });
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      cnt += __shfl_down(cnt, o, 64);
-      lo = fmin(lo, __shfl_down(lo, o, 64));
-      hi = fmax(hi, __shfl_down(hi, o, 64));
-    }
-    if (lane == 0) { S.red_n[wid] = cnt; S.red_d[wid][0] = lo; S.red_d[wid][1] = hi; }
-    __syncthreads();
-    if (tid == 0) {
-      int64_t c = 0; double l = INFINITY, h = -INFINITY;
-      for (int w = 0; w < DEC_THREADS / 64; ++w) { c += S.red_n[w]; l = fmin(l, S.red_d[w][0]); h = fmax(h, S.red_d[w][1]); }
-      S.n = c; S.vmin = l; S.vmax = h;
-    }
-    __syncthreads();
-  }
-  const int64_t n = S.n;
-  dec_mark(tim, t, 2);
-  if (NV && tid == 0) NV[t] = (int32_t)n;
-  const bool degenerate = (n == 0) || !(S.vmin < S.vmax);
-
-  if (!degenerate) {
-    // ---------------- target ranks (interior order statistics; min / max are known)
-    if (tid == 0) {
-      int nt = 0;
-      for (int k = 0; k <= n_bins; ++k) {
-        const double v = (double)(n - 1) * qt.q[k];
-        if (v >= (double)(n - 1)) continue;  // edge = max
-        const double p = floor(v);
-        const int64_t pi = (int64_t)p;
-        if (pi > 0) S.trank[nt++] = pi;
-        if (v - p != 0.0 && pi + 1 < n - 1) S.trank[nt++] = pi + 1;
-      }
-      // sort + dedupe (tiny)
-      for (int i = 1; i < nt; ++i) {
-        int64_t x = S.trank[i]; int j = i - 1;
-        while (j >= 0 && S.trank[j] > x) { S.trank[j + 1] = S.trank[j]; --j; }
-        S.trank[j + 1] = x;
-      }
-      int u = 0;
-      for (int i = 0; i < nt; ++i) if (u == 0 || S.trank[u - 1] != S.trank[i]) S.trank[u++] = S.trank[i];
-      S.ntgt = u;
-    }
-    __syncthreads();
-    // counts are needed after the scan: keep a copy of target-bucket counts via prefix diff
-    block_exclusive_scan_hist(S.hist);
-    if (tid < S.ntgt) {
-      const int64_t r = S.trank[tid];
-      // last bucket b with prefix[b] <= r
-      int lo = 0, hi = HB - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int64_t)S.hist[mid] <= r) lo = mid; else hi = mid - 1;
-      }
-      S.tslot[tid] = lo;  // temporarily: bucket id
-      S.tres[tid] = r - (int64_t)S.hist[lo];
-    }
-    __syncthreads();
-    if (tid == 0) {
-      // build slots from distinct buckets (targets are sorted, so buckets are sorted)
-      int ns = 0;
-      for (int i = 0; i < S.ntgt; ++i) {
-        const int b = S.tslot[i];
-        if (ns == 0 || S.slots[ns - 1].b0 != b) {
-          Slot& s = S.slots[ns++];
-          s.b0 = b; s.klo = 0; s.khi = ~0ULL; s.resolved = 0; s.value = 0.0;
-          const uint32_t next = (b + 1 < HB) ? S.hist[b + 1] : (uint32_t)n;
-          s.count = (int)(next - S.hist[b]);
-        }
-        S.tslot[i] = ns - 1;
-      }
-      S.nslot = ns;
-      int tot = 0;
-      for (int i = 0; i < ns; ++i) tot += S.slots[i].count;
-      S.total = tot;
-    }
-    __syncthreads();
-
-    dec_mark(tim, t, 3);
-    // ---------------- (rare) key-space refinement of the largest slot until all fit.
-    // Each refinement shrinks a slot's key range >= 4096x (<= 6 per target before it is a
-    // single key), so the bound below is never reached on consistent state.
-    for (int guard = 0; S.total > CAP && guard < 8 * MAXT; ++guard) {
-      __shared__ int rs;
-      if (tid == 0) {
-        int best = -1;
-        for (int i = 0; i < S.nslot; ++i)
-          if (!S.slots[i].resolved && (best < 0 || S.slots[i].count > S.slots[best].count)) best = i;
-        rs = best;
-      }
-      __syncthreads();
-      const Slot sl = S.slots[rs];
-      const double lo = blo, sc = bscale;
-      // key min / max of the members
-      unsigned long long kl = ~0ULL, kh = 0ULL;
-      for_row<V2>(row, N, [&](int64_t, double x) {
-        if (!isnan_d(x)) {
-          const uint64_t k = dkey(x);
-          if (slot_member(sl, vbucket(x, lo, sc), k)) { kl = k < kl ? k : kl; kh = k > kh ? k : kh; }
-        }
-      });
-      for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long a2 = __shfl_down(kl, o, 64), b2 = __shfl_down(kh, o, 64);
-        kl = a2 < kl ? a2 : kl; kh = b2 > kh ? b2 : kh;
-      }
-      if (lane == 0) { S.red_k[wid][0] = kl; S.red_k[wid][1] = kh; }
-      for (int b = tid; b < HB; b += DEC_THREADS) S.hist[b] = 0;
-      __syncthreads();
-      if (tid == 0) {
-        unsigned long long l2 = ~0ULL, h2 = 0ULL;
-        for (int w = 0; w < DEC_THREADS / 64; ++w) { l2 = S.red_k[w][0] < l2 ? S.red_k[w][0] : l2; h2 = S.red_k[w][1] > h2 ? S.red_k[w][1] : h2; }
-        S.kmin_r = l2; S.kmax_r = h2;
-      }
-      __syncthreads();
-      const uint64_t kmin = S.kmin_r, kmax = S.kmax_r;
-      if (kmin == kmax) {
-        if (tid == 0) {
-          Slot& s = S.slots[rs];
-          s.resolved = 1; s.value = dval(kmin); s.klo = kmin; s.khi = kmax;
-          S.total -= s.count;
-        }
-        __syncthreads();
-        continue;
-      }
-      const uint64_t range = kmax - kmin;
-      const int bits = 64 - __clzll((long long)range);
-      const int shift = bits > 12 ? bits - 12 : 0;
-      for_row<V2>(row, N, [&](int64_t, double x) {
-        if (!isnan_d(x)) {
-          const uint64_t k = dkey(x);
-          if (slot_member(sl, vbucket(x, lo, sc), k)) atomicAdd(&S.hist[(k - kmin) >> shift], 1u);
-        }
-      });
-      __syncthreads();
-      if (tid == 0) {
-        // split slot rs by the sub-buckets of its targets; rebuild the slot list in order
-        Slot old = S.slots[rs];
-        Slot* ns_list = S.slots2;
-        int nn = 0;
-        int* remap = S.remap;
-        for (int i = 0; i < S.nslot; ++i) remap[i] = -1;
-        for (int i = 0; i < S.nslot; ++i) {
-          if (i != rs) { ns_list[nn] = S.slots[i]; remap[i] = nn++; continue; }
-          // targets of this slot (contiguous in target order)
-          for (int ti = 0; ti < S.ntgt; ++ti) {
-            if (S.tslot[ti] != rs) continue;
-            int64_t r = S.tres[ti];
-            int j = 0;
-            int64_t acc = 0;
-            while (j < HB - 1 && acc + (int64_t)S.hist[j] <= r) { acc += S.hist[j]; ++j; }
-            const uint64_t klo = kmin + ((uint64_t)j << shift);
-            uint64_t khi = klo + (((uint64_t)1 << shift) - 1);
-            if (khi > kmax || khi < klo) khi = kmax;
-            if (nn == 0 || ns_list[nn - 1].b0 != old.b0 || ns_list[nn - 1].klo != klo) {
-              Slot& s = ns_list[nn++];
-              s = old; s.klo = klo; s.khi = khi; s.count = (int)S.hist[j]; s.resolved = 0;
-            }
-            S.tres[ti] = r - acc;
-            S.tslot[ti] = -(nn - 1) - 2;  // mark as remapped (new index encoded)
-          }
-        }
-        for (int ti = 0; ti < S.ntgt; ++ti) {
-          if (S.tslot[ti] <= -2) S.tslot[ti] = -S.tslot[ti] - 2;
-          else S.tslot[ti] = remap[S.tslot[ti]];
-        }
-        int tot = 0;
-        for (int i = 0; i < nn; ++i) { S.slots[i] = ns_list[i]; if (!ns_list[i].resolved) tot += ns_list[i].count; }
-        S.nslot = nn;
-        S.total = tot;
-      }
-      __syncthreads();
-    }
-
-    dec_mark(tim, t, 4);
-    // ---------------- pass 3: gather candidates of unresolved slots
-    if (tid == 0) {
-      int off = 0;
-      for (int i = 0; i < S.nslot; ++i) {
-        S.slots[i].off = off;
-        S.fill[i] = 0;
-        if (!S.slots[i].resolved) off += S.slots[i].count;
-      }
-      S.total = off;
-    }
-    // bucket -> first slot index map (reuses hist)
-    for (int b = tid; b < HB; b += DEC_THREADS) S.hist[b] = 0xFFFFFFFFu;
-    __syncthreads();
-    if (tid == 0)
-      for (int i = S.nslot - 1; i >= 0; --i) S.hist[S.slots[i].b0] = (uint32_t)i;
-    __syncthreads();
-    if (!(ablate & 2)) {
-      const double lo = blo, sc = bscale;
-      const int nsl = S.nslot;
-      auto offer = [&](double x, int b) {
-        const uint64_t k = dkey(x);
-        for (int i = (int)S.hist[b]; i < nsl && S.slots[i].b0 == b; ++i) {
-          const Slot& s = S.slots[i];
-          if (k >= s.klo && k <= s.khi) {
-            if (!s.resolved) {
-              const int pos = atomicAdd(&S.fill[i], 1);
-              S.cand[s.off + pos] = x;
-            }
-            break;
-          }
-        }
-      };
-      if (IDS) {
-        const uint16_t* irow = IDSx + (int64_t)t * N;
-        const int64_t step = 4 * DEC_THREADS;
-        constexpr int GU = 8;
-        for (int64_t i0 = 4 * (int64_t)tid; i0 < N; i0 += GU * step) {
-          uint2 pk[GU];
-#pragma unroll
-          for (int u = 0; u < GU; ++u) {
-            const int64_t i = i0 + u * step;
-            pk[u] = i < N ? *reinterpret_cast<const uint2*>(irow + i) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-          }
-#pragma unroll
-          for (int u = 0; u < GU; ++u) {
-            const int64_t i = i0 + u * step;
-            const uint32_t id[4] = {pk[u].x & 0xFFFFu, pk[u].x >> 16, pk[u].y & 0xFFFFu, pk[u].y >> 16};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              if (id[k] == 0xFFFFu || S.hist[id[k]] == 0xFFFFFFFFu) continue;  // not a target bucket
-              offer(row[i + k], (int)id[k]);   // exact value: re-read M for this cell only
-            }
-          }
-        }
-      } else {
-        for_row<V2, true>(row, N, [&](int64_t, double x) {
-          const uint32_t si = S.hist[vbucket(x, lo, sc)];
-          if (si == 0xFFFFFFFFu || !(x == x)) return;  // common case: not a target bucket
-          offer(x, vbucket(x, lo, sc));
-        });
-      }
-    }
-    __syncthreads();
-    dec_mark(tim, t, 5);
-    // ---------------- order statistics inside the slots.  Small slots (the usual case: a
-    // few dozen members each) use counting selection: the member whose rank inside its slot
-    // (ties broken by position) equals the target's residual rank is the order statistic --
-    // one pass, no barriers.  Large slots fall back to a bitonic sort of all candidates.
-    if (tid == 0) {
-      int64_t work = 0;
-      S.tpre[0] = 0;
-      for (int i = 0; i < S.ntgt; ++i) {
-        const Slot& sl = S.slots[S.tslot[i]];
-        const int c = sl.resolved ? 0 : sl.count;
-        S.tpre[i + 1] = S.tpre[i] + c;
-        work += (int64_t)c * c;
-      }
-      S.sel_count = work <= (int64_t)DEC_THREADS * 512;
-    }
-    __syncthreads();
-    if (S.sel_count) {
-      const int ntg = S.ntgt, tot = S.tpre[ntg];
-      for (int p = tid; p < tot; p += DEC_THREADS) {
-        int t2 = 0;
-        while (S.tpre[t2 + 1] <= p) ++t2;
-        const Slot& sl = S.slots[S.tslot[t2]];
-        const int i = p - S.tpre[t2];
-        const double* c = S.cand + sl.off;
-        const double x = c[i];
-        int rank = 0;
-        for (int j = 0; j < sl.count; ++j) {
-          const double y = c[j];
-          rank += (y < x || (y == x && j < i)) ? 1 : 0;
-        }
-        if (rank == S.tres[t2]) S.tval[t2] = x;
-      }
-      if (tid < ntg) {
-        const Slot& sl = S.slots[S.tslot[tid]];
-        if (sl.resolved) S.tval[tid] = sl.value;
-      }
-    } else {
-      const int tot = S.total;
-      int P2 = 1;
-      while (P2 < tot) P2 <<= 1;
-      for (int i = tot + tid; i < P2; i += DEC_THREADS) S.cand[i] = INFINITY;
-      __syncthreads();
-      for (int k = 2; k <= P2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = tid; i < P2; i += DEC_THREADS) {
-            const int ixj = i ^ j;
-            if (ixj > i) {
-              const double x = S.cand[i], y = S.cand[ixj];
-              const bool up = (i & k) == 0;
-              if ((x > y) == up) { S.cand[i] = y; S.cand[ixj] = x; }
-            }
-          }
-          __syncthreads();
-        }
-      }
-      if (tid < S.ntgt) {
-        const Slot& sl = S.slots[S.tslot[tid]];
-        S.tval[tid] = sl.resolved ? sl.value : S.cand[sl.off + S.tres[tid]];
-      }
-    }
-    __syncthreads();
-    dec_mark(tim, t, 6);
-    // ---------------- edges (NumPy _lerp) and duplicates='drop'
-    if (tid == 0) {
-      auto order_stat = [&](int64_t r) -> double {
-        if (r <= 0) return S.vmin;
-        if (r >= n - 1) return S.vmax;
-        int lo2 = 0, hi2 = S.ntgt - 1;
-        while (lo2 < hi2) { const int mid = (lo2 + hi2) >> 1; if (S.trank[mid] < r) lo2 = mid + 1; else hi2 = mid; }
-        return S.tval[lo2];
-      };
-      double* e = S.e;
-      for (int k = 0; k <= n_bins; ++k) {
-        const double v = (double)(n - 1) * qt.q[k];
-        if (v >= (double)(n - 1)) { e[k] = S.vmax; continue; }
-        const double p = floor(v);
-        const double g = v - p;
-        const int64_t pi = (int64_t)p;
-        const double a = order_stat(pi);
-        const double b = (g != 0.0) ? order_stat(pi + 1) : a;
-        const double d = b - a;
-        e[k] = (g >= 0.5) ? (b - d * (1.0 - g)) : (a + d * g);
-      }
-      double* u = S.u;
-      int nu = 0;
-      for (int k = 0; k <= n_bins; ++k) {
-        bool seen = false;
-        for (int j = 0; j < nu; ++j) seen |= (u[j] == e[k]);
-        if (!seen) u[nu++] = e[k];
-      }
-      const int ne = n_bins + 1;
-      if (nu < ne && ne != 2) { for (int j = 0; j < nu; ++j) S.bins[j] = u[j]; S.nbins = nu; }
-      else { for (int j = 0; j < ne; ++j) S.bins[j] = e[j]; S.nbins = ne; }
-    }
-    __syncthreads();
-    // bucket -> label table: a bucket holding no edge has one label for all its values
-    // (vbucket is monotone: vb(e) < vb(x) implies e < x, vb(e) > vb(x) implies e > x)
-    if (tid < S.nbins) S.vbe[tid] = vbucket(S.bins[tid], blo, bscale);
-    __syncthreads();
-    {
-      const int nbe = S.nbins;
-      for (int b2 = tid; b2 < HB; b2 += DEC_THREADS) {
-        int c = 0;
-        bool amb = false;
-        for (int j = 0; j < nbe; ++j) { const int vb = S.vbe[j]; c += vb < b2 ? 1 : 0; amb |= vb == b2; }
-        S.blab[b2] = (int8_t)(amb ? -2 : ((c == 0 || c == nbe) ? -1 : c - 1));
-      }
-    }
-    __syncthreads();
-  } else {
-    if (tid == 0) S.nbins = 0;
-    __syncthreads();
-  }
-
-  dec_mark(tim, t, 7);
-  // ---------------- pass 4: labels + equal-weight accumulation
-  // Labels come from the bucket table; only values in a bucket that holds an edge are
-  // compared against the edges.  Per lane the next_ret sums are plain fp64 (a few dozen
-  // terms per label), then combined across lanes and waves with a fixed-order
-  // double-double tree (deterministic; |error| ~ 1e-16 * sum |r|).
-  const int nb = S.nbins;
-  const double* bins = S.bins;  // LDS, every lane reads the same word: broadcast
-  constexpr int NBA = NB > 0 ? NB : 1;
-  double hs[NBA], ls[NBA];
-  int cn[NBA];
-#pragma unroll
-  for (int d = 0; d < NBA; ++d) { hs[d] = 0.0; ls[d] = 0.0; cn[d] = 0; }
-  auto label_of = [&](double x) -> int {
-    int lab = (nb == 0) ? -1 : (int)S.blab[vbucket(x, blo, bscale)];
-    lab = (x == x) ? lab : -1;
-    if (lab != -2) return lab;
-    int ids = 0;
-    for (int j = 0; j < nb; ++j) ids += (bins[j] < x) ? 1 : 0;
-    if (x == bins[0]) ids = 1;
-    return (ids == 0 || ids == nb) ? -1 : ids - 1;
-  };
-  auto accumulate = [&](int lab, double r) {
-    if (NB > 0 && !(ablate & 1)) {
-      const bool ok = lab >= 0 && !isnan_d(r);
-#pragma unroll
-      for (int d = 0; d < NB; ++d) {
-        const bool h = ok && lab == d;
-        hs[d] += h ? r : 0.0;
-        cn[d] += h ? 1 : 0;
-      }
-    }
-  };
-  if (ablate & 4) {
-    // profiling ablation: no label pass
-  } else if (IDS) {
-    // label from the bucket id; exact comparison (re-reading M) only in edge buckets.  The
-    // decile sums use a one-hot fma per label (fma(1, r, s) rounds like s + r, fma(0, r, s)
-    // is s) and integer counts.
-    const uint16_t* irow = IDSx + (int64_t)t * N;
-    const int64_t step = 4 * DEC_THREADS;
-    constexpr int LU4 = 2;
-    for (int64_t i0 = 4 * (int64_t)tid; i0 < N; i0 += LU4 * step) {
-      uint2 pk[LU4];
-      double2 ra[LU4], rb[LU4];
-#pragma unroll
-      for (int u = 0; u < LU4; ++u) {
-        const int64_t i = i0 + u * step;
-        if (i < N) {
-          pk[u] = *reinterpret_cast<const uint2*>(irow + i);
-          if (NB > 0 && nrow) {
-            ra[u] = *reinterpret_cast<const double2*>(nrow + i);
-            rb[u] = *reinterpret_cast<const double2*>(nrow + i + 2);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < LU4; ++u) {
-        const int64_t i = i0 + u * step;
-        if (i >= N) break;
-        const uint32_t id[4] = {pk[u].x & 0xFFFFu, pk[u].x >> 16, pk[u].y & 0xFFFFu, pk[u].y >> 16};
-        int lab[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          int l = (id[k] == 0xFFFFu || nb == 0) ? -1 : (int)S.blab[id[k]];
-          if (l == -2) l = label_of(row[i + k]);
-          lab[k] = l;
-        }
-        char4 lv;
-        lv.x = (char)lab[0]; lv.y = (char)lab[1]; lv.z = (char)lab[2]; lv.w = (char)lab[3];
-        *reinterpret_cast<char4*>(lrow + i) = lv;
-        if (NB > 0 && nrow && !(ablate & 1)) {
-          const double rs[4] = {ra[u].x, ra[u].y, rb[u].x, rb[u].y};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const bool ok = lab[k] >= 0 && rs[k] == rs[k];
-            const int lb = ok ? lab[k] : -1;
-            const double r = ok ? rs[k] : 0.0;
-#pragma unroll
-            for (int d = 0; d < NB; ++d) {
-              const bool h = lb == d;
-              hs[d] = fma(h ? 1.0 : 0.0, r, hs[d]);
-              cn[d] += h ? 1 : 0;
-            }
-          }
-        }
-      }
-    }
-  } else if (V2) {
-    const int64_t step = 2 * DEC_THREADS;
-    int64_t i = 2 * (int64_t)tid;
-    constexpr int LU = 4;
-    for (; i + (LU - 1) * step < N; i += LU * step) {
-      double2 x[LU], r[LU];
-#pragma unroll
-      for (int u = 0; u < LU; ++u) x[u] = *reinterpret_cast<const double2*>(row + i + u * step);
-      if (NB > 0 && nrow) {
-#pragma unroll
-        for (int u = 0; u < LU; ++u) r[u] = *reinterpret_cast<const double2*>(nrow + i + u * step);
-      }
-#pragma unroll
-      for (int u = 0; u < LU; ++u) {
-        const int l0 = label_of(x[u].x), l1 = label_of(x[u].y);
-        char2 lv; lv.x = (char)l0; lv.y = (char)l1;
-        *reinterpret_cast<char2*>(lrow + i + u * step) = lv;
-        if (NB > 0 && nrow) { accumulate(l0, r[u].x); accumulate(l1, r[u].y); }
-      }
-    }
-    for (; i < N; i += step) {
-      const double2 x = *reinterpret_cast<const double2*>(row + i);
-      const int l0 = label_of(x.x), l1 = label_of(x.y);
-      char2 lv; lv.x = (char)l0; lv.y = (char)l1;
-      *reinterpret_cast<char2*>(lrow + i) = lv;
-      if (NB > 0 && nrow && (l0 >= 0 || l1 >= 0)) {
-        const double2 r = *reinterpret_cast<const double2*>(nrow + i);
-        accumulate(l0, r.x);
-        accumulate(l1, r.y);
-      }
-    }
-  } else {
-    for (int64_t i = tid; i < N; i += DEC_THREADS) {
-      const int l0 = label_of(row[i]);
-      lrow[i] = (int8_t)l0;
-      if (NB > 0 && nrow && l0 >= 0) accumulate(l0, nrow[i]);
-    }
-  }
-  dec_mark(tim, t, 8);
-  if (NB > 0 && nrow && EW) {
-    // deterministic block reduction: wave shfl_down tree, then waves in order
-    __shared__ double wh[DEC_THREADS / 64][NB > 0 ? NB : 1], wl[DEC_THREADS / 64][NB > 0 ? NB : 1];
-    __shared__ int wc[DEC_THREADS / 64][NB > 0 ? NB : 1];
-#pragma unroll
-    for (int d = 0; d < NB; ++d) {
-      double h = hs[d], l = ls[d];
-      int c = cn[d];
-      for (int o = 32; o > 0; o >>= 1) {
-        const double h2 = __shfl_down(h, o, 64), l2 = __shfl_down(l, o, 64);
-        const int c2 = __shfl_down(c, o, 64);
-        const double s = h + h2;
-        const double bb = s - h;
-        const double err = (h - (s - bb)) + (h2 - bb);
-        h = s; l = (l + l2) + err; c += c2;
-      }
-      if (lane == 0) { wh[wid][d] = h; wl[wid][d] = l; wc[wid][d] = c; }
-    }
-    __syncthreads();
-    if (tid < NB) {
-      const int d = tid;
-      double h = 0.0, l = 0.0;
-      int c = 0;
-      for (int w = 0; w < DEC_THREADS / 64; ++w) {
-        const double h2 = wh[w][d];
-        const double s = h + h2;
-        const double bb = s - h;
-        const double err = (h - (s - bb)) + (h2 - bb);
-        h = s; l = (l + wl[w][d]) + err; c += wc[w][d];
-      }
-      const double sum = h + l;
-      EW[(int64_t)t * NB + d] = c > 0 ? sum / (double)c : qnan();
-      if (CNT) CNT[(int64_t)t * NB + d] = c;
-    }
-  }
-}
+namespace dec_wide {
+#include "deciles.inc"
+}  // namespace dec_wide
+using dec_wide::k_deciles;
+#undef DEC_THREADS
+#undef HB
+#undef CAP
 
 // =====================================================================================
 // Kernel E: long-short series (one workgroup; T_m * n_bins is tiny).
@@ -1692,7 +849,9 @@ static int g_tune_month_end_rows = 0;
 static int64_t* g_dec_timing = nullptr;
 // k_deciles bucket-id scratch path (N % 4 == 0): 1 on, 0 off.  Off by default: it moves
 // fewer bytes but measured slower at C4 (0.44 vs 0.40 ms, profiles/r01/experiments).
-static int g_tune_dec_ids = 0;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
+static int g_tune_dec_ids = 0;
+// rows with at most this many assets take the narrow-row decile kernel (deciles_narrow.hip)
+static int64_t g_tune_dec_narrow_max = 16384;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
 
 extern "C" {
 
@@ -1704,6 +863,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "signal_nbuf") && (value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
   if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
   if (!strcmp(key, "dec_ids") && (value == 0 || value == 1)) { g_tune_dec_ids = value; return CSM_OK; }
+  if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
   if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
@@ -1734,8 +894,8 @@ int csm_create(int device, csm_ctx** out) {
 
 int csm_destroy(csm_ctx* ctx) {
   if (ctx && ctx->scratch) {
-    hipSetDevice(ctx->device);
-    hipFree(ctx->scratch);
+    (void)hipSetDevice(ctx->device);
+    (void)hipFree(ctx->scratch);
   }
   free(ctx);
   return CSM_OK;
@@ -1961,9 +1121,13 @@ static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, co
                            int32_t* CNT, int32_t* NV, uint16_t* ids) {
   const int ab = g_tune_dec_ablate;
   int64_t* tm = g_dec_timing;
-  if (ids) hipLaunchKernelGGL((k_deciles<NB, true, true>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
-  else if (v2) hipLaunchKernelGGL((k_deciles<NB, true, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
-  else hipLaunchKernelGGL((k_deciles<NB, false, false>), dim3(T_m), dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+  if (N <= g_tune_dec_narrow_max && !ids) {   // rows of a few thousand assets (C2/C3/C5)
+    launch_deciles_narrow<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
+    return;
+  }
+  if (ids) hipLaunchKernelGGL((k_deciles<NB, true, true>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+  else if (v2) hipLaunchKernelGGL((k_deciles<NB, true, false>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+  else hipLaunchKernelGGL((k_deciles<NB, false, false>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
 }
 
 extern "C" {

@@ -145,21 +145,30 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
 // w_u = (1/K_u) sum over the non-empty cohorts s in (u-K, u] of omega_s, omega_s[a] =
 // W[s][a] / total_s.  When both windows of months t and t-1 are full (K non-empty cohorts
 // each), w_t - w_{t-1} = (omega_t - omega_{t-K}) / K: two label reads per leg instead of 2K.
-// The per-cohort inverse totals of the K+1 months involved are staged in LDS once per
-// workgroup (chunk partials summed in chunk order), so the inner loop multiplies.
+// One launch serves up to TO_MAXQ holding periods (a sweep's K values): a cell's month-t
+// label / weight is loaded once and its month t-K_q ones for every q in the same trip.  The
+// per-cohort inverse totals (chunk partials summed in chunk order) are staged in LDS, so the
+// inner loop multiplies.
+#define TO_MAXQ 4
+struct KSet {
+  int n;
+  int K[TO_MAXQ];
+};
+
 __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
-    int T_m, int B, int64_t N, int K, int n_bins, int Cf, int64_t CH, double half_spread,
-    double k_impact, double aum, const double* __restrict__ ADV, const double* __restrict__ SIG,
-    double* __restrict__ TURNp, double* __restrict__ COSTp) {
+    int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
+    double half_spread, double k_impact, double aum, const double* __restrict__ ADV,
+    const double* __restrict__ SIG, double* __restrict__ TURNp, double* __restrict__ COSTp) {
   const int c = blockIdx.x, Ct = gridDim.x;
   const int tb = blockIdx.y;
+  const int rows = gridDim.y;
   const int t = tb / B, b = tb - t * B;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  __shared__ double inv[2][TO_MAXK + 1];   // [leg][j]: 1/total of cohort s = t - j (0 = empty)
-  __shared__ double sk[2][2];              // [leg][0: month t, 1: month t-1]: 1/K_u (0 if none)
-  __shared__ int full[2];
-  for (int j = tid; j <= K; j += PF_THREADS) {
+  __shared__ double inv[2][TO_MAXK + 1];      // [leg][j]: 1/total of cohort s = t - j (0 = empty)
+  __shared__ double sk[TO_MAXQ][2][2];        // [q][leg][month t, t-1]: 1/K_u (0 if none)
+  __shared__ int full[TO_MAXQ][2];
+  for (int j = tid; j <= Kmax; j += PF_THREADS) {
     const int s = t - j;
 #pragma unroll
     for (int li = 0; li < 2; ++li) {
@@ -170,109 +179,125 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     }
   }
   __syncthreads();
-  if (tid < 2) {
-    const int li = tid;
+  if (tid < 2 * ks.n) {
+    const int q = tid >> 1, li = tid & 1, K = ks.K[q];
     int k1 = 0, k0 = 0;
     for (int j = 0; j < K; ++j) k1 += inv[li][j] > 0.0 ? 1 : 0;                    // month t
     for (int j = 1; j <= K; ++j) k0 += (t >= 1 && inv[li][j] > 0.0) ? 1 : 0;        // month t-1
-    sk[li][0] = k1 > 0 ? 1.0 / (double)k1 : 0.0;
-    sk[li][1] = k0 > 0 ? 1.0 / (double)k0 : 0.0;
-    full[li] = (k1 == K && k0 == K) ? 1 : 0;
+    sk[q][li][0] = k1 > 0 ? 1.0 / (double)k1 : 0.0;
+    sk[q][li][1] = k0 > 0 ? 1.0 / (double)k0 : 0.0;
+    full[q][li] = (k1 == K && k0 == K) ? 1 : 0;
   }
   __syncthreads();
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
   const int64_t rt = ((int64_t)t * B + b) * N;
   const bool impact = ADV && aum > 0.0;
-  double turn = 0.0, cost = 0.0;
-  const bool both_full = full[0] && full[1];
-  const int64_t rk = ((int64_t)(t - K) * B + b) * N;   // month t-K (valid when full)
-  // steady state (both windows full): 4 cells per lane per trip, loads issued up front
-  constexpr int TU = 4;
-  int64_t a_tail = a0 + tid;
-  if (both_full) {
+  const int nq = ks.n;
+  double turn[TO_MAXQ], cost[TO_MAXQ];
+#pragma unroll
+  for (int q = 0; q < TO_MAXQ; ++q) { turn[q] = 0.0; cost[q] = 0.0; }
+  auto charge = [&](int q, double dw, double adv, double unit_sig) {
+    turn[q] += dw;
+    double unit = half_spread;
+    if (impact && adv > 0.0) {
+      const double im = k_impact * unit_sig * sqrt(dw * aum / adv);
+      unit = unit + ((im == im) ? im : 0.0);
+    }
+    cost[q] += dw * unit;
+  };
+  bool all_full = true;
+  for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
+  if (all_full) {
+    // steady state: 2 cells per lane per trip, every load issued before use
+    constexpr int TU = 2;
     for (int64_t i0 = a0 + tid; i0 < a1; i0 += TU * PF_THREADS) {
-      int l1[TU], l0[TU];
-      double x1[TU], x0[TU], adv[TU], sg[TU];
+      int l1[TU], l0[TU][TO_MAXQ];
+      double x1[TU], x0[TU][TO_MAXQ], adv[TU], sg[TU];
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
         const int64_t a = i0 + (int64_t)u * PF_THREADS;
         const bool in = a < a1;
         l1[u] = in ? (int)L[rt + a] : -1;
-        l0[u] = in ? (int)L[rk + a] : -1;
         x1[u] = (W && in) ? W[rt + a] : 1.0;
-        x0[u] = (W && in) ? W[rk + a] : 1.0;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          const bool use = in && q < nq;
+          const int64_t rk = ((int64_t)(t - (use ? ks.K[q] : 0)) * B + b) * N;
+          l0[u][q] = use ? (int)L[rk + a] : -1;
+          x0[u][q] = (W && use) ? W[rk + a] : 1.0;
+        }
         adv[u] = (impact && in) ? ADV[rt + a] : 0.0;
         sg[u] = (impact && SIG && in) ? SIG[rt + a] : 0.02;
       }
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
         const double vw1 = (x1[u] > 0.0 && x1[u] < INFINITY) ? x1[u] : 0.0;
-        const double vw0 = (x0[u] > 0.0 && x0[u] < INFINITY) ? x0[u] : 0.0;
         const double unit_sig = sg[u] == sg[u] ? sg[u] : 0.02;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          if (q >= nq) break;
+          const double vw0 = (x0[u][q] > 0.0 && x0[u][q] < INFINITY) ? x0[u][q] : 0.0;
+          const int K = ks.K[q];
+#pragma unroll
+          for (int li = 0; li < 2; ++li) {
+            const int d = li == 0 ? n_bins - 1 : 0;
+            const double w1 = (l1[u] == d ? vw1 : 0.0) * inv[li][0];
+            const double w0 = (l0[u][q] == d ? vw0 : 0.0) * inv[li][K];
+            charge(q, fabs(w1 - w0) * sk[q][li][0], adv[u], unit_sig);
+          }
+        }
+      }
+    }
+  } else {
+    for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
+      double unit_sig = 0.02, adv = 0.0;
+      if (impact) {
+        adv = ADV[rt + a];
+        if (SIG) { const double sg = SIG[rt + a]; unit_sig = (sg == sg) ? sg : 0.02; }
+      }
+      for (int q = 0; q < nq; ++q) {
+        const int K = ks.K[q];
 #pragma unroll
         for (int li = 0; li < 2; ++li) {
           const int d = li == 0 ? n_bins - 1 : 0;
-          const double w1 = (l1[u] == d ? vw1 : 0.0) * inv[li][0];
-          const double w0 = (l0[u] == d ? vw0 : 0.0) * inv[li][K];
-          const double dw = fabs(w1 - w0) * sk[li][0];
-          turn += dw;
-          double unit = half_spread;
-          if (impact && adv[u] > 0.0) {
-            const double im = k_impact * unit_sig * sqrt(dw * aum / adv[u]);
-            unit = unit + ((im == im) ? im : 0.0);
+          double dw;
+          if (full[q][li]) {
+            const int64_t o1 = rt + a, o0 = ((int64_t)(t - K) * B + b) * N + a;
+            const double w1 = member_w(L[o1], d, W, o1) * inv[li][0];
+            const double w0 = member_w(L[o0], d, W, o0) * inv[li][K];
+            dw = fabs(w1 - w0) * sk[q][li][0];
+          } else {
+            double x1 = 0.0, x0 = 0.0;
+            for (int j = 0; j <= K; ++j) {
+              const double iv = inv[li][j];
+              if (iv == 0.0) continue;
+              const int64_t o = ((int64_t)(t - j) * B + b) * N + a;
+              const double w = member_w(L[o], d, W, o) * iv;
+              if (j < K) x1 += w;
+              if (j >= 1) x0 += w;
+            }
+            dw = fabs(x1 * sk[q][li][0] - x0 * sk[q][li][1]);
           }
-          cost += dw * unit;
+          charge(q, dw, adv, unit_sig);
         }
       }
     }
-    a_tail = a1;  // nothing left for the general loop
   }
-  for (int64_t a = a_tail; a < a1; a += PF_THREADS) {
-    double unit_sig = 0.02, adv = 0.0;
-    if (impact) {
-      adv = ADV[rt + a];
-      if (SIG) { const double sg = SIG[rt + a]; unit_sig = (sg == sg) ? sg : 0.02; }
-    }
+  __shared__ double red[PF_WAVES][2 * TO_MAXQ];
 #pragma unroll
-    for (int li = 0; li < 2; ++li) {
-      const int d = li == 0 ? n_bins - 1 : 0;
-      double dw;
-      if (full[li]) {
-        const int64_t o1 = rt + a, o0 = rk + a;
-        const double w1 = member_w(L[o1], d, W, o1) * inv[li][0];
-        const double w0 = member_w(L[o0], d, W, o0) * inv[li][K];
-        dw = fabs(w1 - w0) * sk[li][0];
-      } else {
-        double x1 = 0.0, x0 = 0.0;
-        for (int j = 0; j <= K; ++j) {
-          const double iv = inv[li][j];
-          if (iv == 0.0) continue;
-          const int64_t o = ((int64_t)(t - j) * B + b) * N + a;
-          const double w = member_w(L[o], d, W, o) * iv;
-          if (j < K) x1 += w;
-          if (j >= 1) x0 += w;
-        }
-        dw = fabs(x1 * sk[li][0] - x0 * sk[li][1]);
-      }
-      turn += dw;
-      double unit = half_spread;
-      if (impact && adv > 0.0) {
-        const double im = k_impact * unit_sig * sqrt(dw * aum / adv);
-        unit = unit + ((im == im) ? im : 0.0);
-      }
-      cost += dw * unit;
-    }
+  for (int q = 0; q < TO_MAXQ; ++q) {
+    if (q >= nq) break;
+    const double x1 = wave_sum(turn[q]), y1 = wave_sum(cost[q]);
+    if (lane == 0) { red[wid][2 * q] = x1; red[wid][2 * q + 1] = y1; }
   }
-  __shared__ double red[PF_WAVES][2];
-  const double x1 = wave_sum(turn), y1 = wave_sum(cost);
-  if (lane == 0) { red[wid][0] = x1; red[wid][1] = y1; }
   __syncthreads();
-  if (tid == 0) {
+  if (tid < nq) {
+    const int q = tid;
     double x = 0.0, y = 0.0;
-    for (int w2 = 0; w2 < PF_WAVES; ++w2) { x += red[w2][0]; y += red[w2][1]; }
-    TURNp[(int64_t)tb * Ct + c] = 0.5 * x;
-    COSTp[(int64_t)tb * Ct + c] = y;
+    for (int w2 = 0; w2 < PF_WAVES; ++w2) { x += red[w2][2 * q]; y += red[w2][2 * q + 1]; }
+    TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.5 * x;
+    COSTp[((int64_t)q * rows + tb) * Ct + c] = y;
   }
 }
 
@@ -452,9 +477,9 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   l.swr = 0;
   l.sw = cs;
   l.fw = 2 * cs;
-  l.turn = l.fw + l.rows * l.p.C * 2;
-  l.cost = l.turn + l.rows * l.p.Ct;
-  l.bytes = (l.cost + l.rows * l.p.Ct) * 8 + 256;
+  l.turn = l.fw + l.rows * l.p.C * 2;                      // [TO_MAXQ][rows][Ct]
+  l.cost = l.turn + (int64_t)TO_MAXQ * l.rows * l.p.Ct;
+  l.bytes = (l.cost + (int64_t)TO_MAXQ * l.rows * l.p.Ct) * 8 + 256;
   return l;
 }
 
@@ -488,18 +513,21 @@ int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const doubl
   return CSM_OK;
 }
 
-int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, int32_t T_m,
-                               int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, int32_t K,
-                               double half_spread, double k_impact, double aum, const double* ADV,
-                               const double* SIG, double* PR, double* LS, double* TURN,
-                               double* COST, double* NET, void* workspace) {
+int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double* W,
+                                     int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
+                                     int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                     double half_spread, double k_impact, double aum,
+                                     const double* ADV, const double* SIG, double* PR, double* LS,
+                                     double* TURN, double* COST, double* NET, void* workspace) {
   int r = prep(ctx);
   if (r) return r;
-  if (!L || !PR || !LS || !workspace || T_m < 0 || B < 1 || N <= 0 || K < 1 || K > Kmax ||
+  bool ks_ok = Ks && nK >= 1;
+  for (int q = 0; ks_ok && q < nK; ++q) ks_ok = Ks[q] >= 1 && Ks[q] <= Kmax;
+  if (!L || !PR || !LS || !workspace || T_m < 0 || B < 1 || N <= 0 || !ks_ok ||
       Kmax > TO_MAXK || n_bins < 2 || n_bins > 30 || !(half_spread >= 0.0) ||
       !(k_impact >= 0.0) || !(aum >= 0.0) || (int64_t)T_m * B > 0x7FFFFFFF)
-    return set_err(ctx, CSM_E_INVAL, "csm_portfolio_from_cohorts: bad arguments (T_m=%d B=%d N=%lld K=%d Kmax=%d)",
-                   T_m, B, (long long)N, K, Kmax);
+    return set_err(ctx, CSM_E_INVAL, "csm_portfolio_from_cohorts: bad arguments (T_m=%d B=%d N=%lld nK=%d Kmax=%d)",
+                   T_m, B, (long long)N, nK, Kmax);
   if (NET && !COST)
     return set_err(ctx, CSM_E_INVAL, "csm_portfolio: NET needs COST");
   if (T_m == 0) return CSM_OK;
@@ -507,22 +535,47 @@ int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, i
   double* ws = (double*)workspace;
   hipStream_t st = ctx->stream;
   const bool costs = TURN || COST;
-  if (costs) {
-    hipLaunchKernelGGL(k_turnover, dim3((unsigned)lay.p.Ct, (unsigned)lay.rows), dim3(PF_THREADS),
-                       0, st, L, W, (const double*)(ws + lay.fw), T_m, B, N, K, n_bins, lay.p.C,
-                       lay.p.CHt, half_spread, k_impact, aum, ADV, SIG, ws + lay.turn,
-                       ws + lay.cost);
-    LAUNCH_CHECK(ctx, "k_turnover");
+  const int64_t rb = (int64_t)T_m * B;   // cells of one [T_m][B] output
+  for (int q0 = 0; q0 < nK; q0 += TO_MAXQ) {
+    KSet ks;
+    ks.n = nK - q0 < TO_MAXQ ? nK - q0 : TO_MAXQ;
+    for (int q = 0; q < TO_MAXQ; ++q) ks.K[q] = q < ks.n ? Ks[q0 + q] : 1;
+    if (costs) {
+      hipLaunchKernelGGL(k_turnover, dim3((unsigned)lay.p.Ct, (unsigned)lay.rows),
+                         dim3(PF_THREADS), 0, st, L, W, (const double*)(ws + lay.fw), T_m, B, N,
+                         ks, Kmax, n_bins, lay.p.C, lay.p.CHt, half_spread, k_impact, aum, ADV,
+                         SIG, ws + lay.turn, ws + lay.cost);
+      LAUNCH_CHECK(ctx, "k_turnover");
+    }
+    for (int q = 0; q < ks.n; ++q) {
+      const int qq = q0 + q;
+      const int64_t tq = (int64_t)q * lay.rows * lay.p.Ct;
+      double* TURNq = TURN ? TURN + qq * rb : nullptr;
+      double* COSTq = COST ? COST + qq * rb : nullptr;
+      double* NETq = NET ? NET + qq * rb : nullptr;
+      double* PRq = PR + qq * rb * n_bins;
+      hipLaunchKernelGGL(k_overlap, dim3((unsigned)lay.rows), dim3(64), 0, st,
+                         (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks.K[q],
+                         Kmax, lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn + tq) : nullptr,
+                         (const double*)(ws + lay.cost + tq), lay.p.Ct, PRq, TURNq, COSTq);
+      LAUNCH_CHECK(ctx, "k_overlap");
+      hipLaunchKernelGGL(k_ls, dim3((unsigned)B), dim3(256), 0, st, (const double*)PRq, T_m, B,
+                         n_bins, LS + qq * rb, (const double*)COSTq, NETq);
+      LAUNCH_CHECK(ctx, "k_ls");
+    }
   }
-  hipLaunchKernelGGL(k_overlap, dim3((unsigned)lay.rows), dim3(64), 0, st,
-                     (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), K, Kmax,
-                     lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
-                     (const double*)(ws + lay.cost), lay.p.Ct, PR, TURN, COST);
-  LAUNCH_CHECK(ctx, "k_overlap");
-  hipLaunchKernelGGL(k_ls, dim3((unsigned)B), dim3(256), 0, st, (const double*)PR, T_m, B, n_bins,
-                     LS, (const double*)COST, NET);
-  LAUNCH_CHECK(ctx, "k_ls");
   return CSM_OK;
+}
+
+int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, int32_t T_m,
+                               int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, int32_t K,
+                               double half_spread, double k_impact, double aum, const double* ADV,
+                               const double* SIG, double* PR, double* LS, double* TURN,
+                               double* COST, double* NET, void* workspace) {
+  const int32_t ks[1] = {K};
+  return csm_portfolio_from_cohorts_multi(ctx, L, W, T_m, B, N, n_bins, Kmax, 1, ks, half_spread,
+                                          k_impact, aum, ADV, SIG, PR, LS, TURN, COST, NET,
+                                          workspace);
 }
 
 int csm_portfolio(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,

@@ -402,18 +402,19 @@ class Engine:
             workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
         self._call("csm_cohort_sums", _ptr(L), _ptr(NR), _ptr(W), T_m, int(B), N, int(n_bins),
                    Kmax, _ptr(workspace))
-        res = {}
-        for K in Ks:
-            PR, LS = self.empty((T_m, B, n_bins)), self.empty((T_m, B))
-            TURN = self.empty((T_m, B)) if with_costs else None
-            COST = self.empty((T_m, B)) if with_costs else None
-            NET = self.empty((T_m, B)) if with_costs else None
-            self._call("csm_portfolio_from_cohorts", _ptr(L), _ptr(W), T_m, int(B), N,
-                       int(n_bins), Kmax, K, float(half_spread), float(k_impact), float(aum),
-                       _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS), _ptr(TURN), _ptr(COST),
-                       _ptr(NET), _ptr(workspace))
-            res[K] = PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET)
-        return res
+        nK = len(Ks)
+        PR, LS = self.empty((nK, T_m, B, n_bins)), self.empty((nK, T_m, B))
+        TURN = self.empty((nK, T_m, B)) if with_costs else None
+        COST = self.empty((nK, T_m, B)) if with_costs else None
+        NET = self.empty((nK, T_m, B)) if with_costs else None
+        ks = (ctypes.c_int32 * nK)(*Ks)
+        self._call("csm_portfolio_from_cohorts_multi", _ptr(L), _ptr(W), T_m, int(B), N,
+                   int(n_bins), Kmax, nK, ctypes.cast(ks, ctypes.c_void_p), float(half_spread),
+                   float(k_impact), float(aum), _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS),
+                   _ptr(TURN), _ptr(COST), _ptr(NET), _ptr(workspace))
+        pick = lambda x, q: None if x is None else x[q]
+        return {K: PortfolioOut(PR=PR[q], LS=LS[q], TURN=pick(TURN, q), COST=pick(COST, q),
+                                NET=pick(NET, q)) for q, K in enumerate(Ks)}
 
     def turnover_features(self, PM, VOL, so, mcap, lookback=3):
         """csm_turnover_features (src/features.py:60-107, rule T1): (ADV, SH, TURN, TAVG)."""

@@ -221,6 +221,15 @@ int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, i
                                double half_spread, double k_impact, double aum, const double* ADV,
                                const double* SIG, double* PR, double* LS, double* TURN,
                                double* COST, double* NET, void* workspace);
+/* Several holding periods at once (Ks: HOST array of nK values <= Kmax): outputs stacked
+ * over K -- PR [nK][T_m][B][n_bins], LS / TURN / COST / NET [nK][T_m][B]; the turnover pass
+ * loads each cell's labels once for up to 4 K values. */
+int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double* W,
+                                     int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
+                                     int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                     double half_spread, double k_impact, double aum,
+                                     const double* ADV, const double* SIG, double* PR, double* LS,
+                                     double* TURN, double* COST, double* NET, void* workspace);
 
 /*
  * Stationary month bootstrap (BASELINE config C5; rule E6): panels b0 .. b0+B-1 of the base

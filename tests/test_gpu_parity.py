@@ -130,6 +130,9 @@ def test_decile_stress(engine, case):
     row = x[None, :]
     L, _, _, _ = engine.deciles(_up(row), None, 10)
     assert np.array_equal(L.cpu().numpy()[0], _oracle_labels(x))
+    xs = x[:12_000]  # the narrow-row kernel (1024 buckets) on the same pathologies
+    Ls, _, _, _ = engine.deciles(_up(xs[None, :]), None, 10)
+    assert np.array_equal(Ls.cpu().numpy()[0], _oracle_labels(xs))
 
 
 @pytest.mark.parametrize("n_bins", [2, 3, 4, 5, 10, 20])
@@ -321,3 +324,22 @@ def test_segmented_overlapped_pass_bit_identical(engine, segments):
         assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
     assert torch.equal(L, ref.L) and torch.equal(CNT, ref.CNT)
     assert np.array_equal(L.cpu().numpy(), z["J12s1_L"])
+
+
+@pytest.mark.parametrize("name", ["edge", "c1", "small", "real_data"])
+def test_narrow_and_wide_decile_kernels_agree(engine, name):
+    """Rows of <= 16384 assets take the narrow-row kernel (256 threads, 1024 buckets); forcing
+    the wide kernel gives the same labels and counts, means equal to rounding."""
+    z = load_golden(name)
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    _, M, NR = engine.momentum(PM, 12, 1)
+    lib = engine.lib
+    a = engine.deciles(M, NR, 10, with_nv=True)
+    try:
+        assert lib.csm_tune(b"dec_narrow_max", 0) == 0
+        b = engine.deciles(M, NR, 10, with_nv=True)
+    finally:
+        lib.csm_tune(b"dec_narrow_max", 16384)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+    ea, eb = a[1].cpu().numpy(), b[1].cpu().numpy()
+    assert np.array_equal(np.isnan(ea), np.isnan(eb)) and max_rel(ea, eb) <= 1e-13
