@@ -611,7 +611,7 @@ __global__ __launch_bounds__(256) void k_last_present_month(const double* __rest
 // Kernel C: per-date qcut labels + fused decile means (csrc/deciles.inc, wide-row variant).
 // =====================================================================================
 #define DEC_THREADS 512
-#define HB 4096
+#define HB 8192
 #define CAP 4096
 namespace dec_wide {
 #include "deciles.inc"
