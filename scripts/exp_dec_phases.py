@@ -13,6 +13,7 @@ import csmom  # noqa: E402
 from csmom.synth import bday_calendar, make_device_panel  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+IDS = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 TD = 10_000
 days, ms, _ = bday_calendar("1985-01-01", TD)
 pan = make_device_panel(N, days, ms, seed=4, device="cuda:0")
@@ -23,6 +24,7 @@ M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
 L = eng.empty((T_m, N), torch.int8)
 EW, CNT = eng.empty((T_m, 10)), eng.empty((T_m, 10), torch.int32)
 eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
+eng.lib.csm_tune(b"dec_ids", IDS)
 for _ in range(3):
     eng.deciles(M, NR, 10, out=(L, EW, CNT, None))
 tim = torch.full((T_m, 9), -1, dtype=torch.int64, device="cuda:0")
@@ -39,7 +41,7 @@ t = t[ok]
 names = ["sample", "histogram", "targets", "refine", "gather", "select", "edges+table",
          "labels+sums", ]
 d = np.diff(t, axis=1)
-out = {"N": N, "rows_timed": int(ok.sum()), "kernel_ms": round(e0.elapsed_time(e1), 4),
+out = {"N": N, "ids": IDS, "rows_timed": int(ok.sum()), "kernel_ms": round(e0.elapsed_time(e1), 4),
        "phase_us_mean": {n: round(float(d[:, i].mean()), 2) for i, n in enumerate(names)},
        "phase_us_max": {n: round(float(d[:, i].max()), 2) for i, n in enumerate(names)},
        "row_us_mean": round(float((t[:, -1] - t[:, 0]).mean()), 2),
