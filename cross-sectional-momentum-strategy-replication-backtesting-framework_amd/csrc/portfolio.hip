@@ -24,6 +24,8 @@
 // deterministic run to run.
 #include "csm_common.h"
 
+#include <string.h>
+
 #define PF_THREADS 256
 #define PF_WAVES (PF_THREADS / 64)
 #define PF_CHUNK_MIN 256     // assets per chunk, at least one per thread
@@ -138,6 +140,85 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
       FWp[((int64_t)tb * C + c) * 2 + tid] = x;   // leg 0 = top, 1 = bottom
     }
     __syncthreads();  // red is reused by the next cohort
+  }
+}
+
+// Cohort sums with per-wave LDS accumulators: cells in the outer loop, the K cohort ages in
+// the inner loop, and one LDS float atomic per (cell, age) into the wave's own [age][decile]
+// slot instead of n_bins predicated fmas.  The slots are private to a wave, so only lanes of
+// one instruction ever meet at an address, and the waves' slots are combined in wave order.
+// Used when Kmax * n_bins fits (<= AC_MAXKD slots).
+#define AC_MAXKD 384
+template <int NB, bool VW>
+__global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
+    const int8_t* __restrict__ L, const double* __restrict__ NR, const double* __restrict__ W,
+    int T_m, int B, int64_t N, int K, int C, int64_t CH, double* __restrict__ SWRp,
+    double* __restrict__ SWp, double* __restrict__ FWp) {
+  __shared__ double acc_r[PF_WAVES][AC_MAXKD];   // sum of w * r per (age, decile)
+  __shared__ double acc_w[PF_WAVES][AC_MAXKD];   // sum of w (equal weight: the count)
+  __shared__ double red[PF_WAVES][2];
+  const int c = blockIdx.x;
+  const int tb = blockIdx.y;
+  const int t = tb / B, b = tb - t * B;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int KD = K * NB;
+  for (int i = lane; i < KD; i += 64) { acc_r[wid][i] = 0.0; acc_w[wid][i] = 0.0; }
+  const int64_t a0 = (int64_t)c * CH;
+  const int64_t a1 = a0 + CH < N ? a0 + CH : N;
+  const int64_t rt = ((int64_t)t * B + b) * N;
+  const int kmax = t + 1 < K ? t + 1 : K;   // ages with a formation month s = t - k >= 0
+  double ft = 0.0, fb = 0.0;
+  double* ar = acc_r[wid];
+  double* aw = acc_w[wid];
+  __syncthreads();
+  const int64_t rowstep = (int64_t)B * N;   // one month back
+  for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
+    const double r = NR[rt + a];
+    const bool rv = r == r;
+    // ages in groups of KU: the group's label (and weight) loads are issued before use
+    constexpr int KU = 4;
+    for (int k0 = 0; k0 < kmax; k0 += KU) {
+      int lab[KU];
+      double wx[KU];
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int k = k0 + u;
+        const int64_t o = rt - (int64_t)k * rowstep + a;
+        lab[u] = k < kmax ? (int)L[o] : -1;
+        if (VW) wx[u] = k < kmax ? W[o] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int k = k0 + u;
+        double w = 1.0;
+        if (VW) w = (wx[u] > 0.0 && wx[u] < INFINITY) ? wx[u] : 0.0;
+        if (k == 0) {
+          ft += lab[u] == NB - 1 ? w : 0.0;
+          fb += lab[u] == 0 ? w : 0.0;
+        }
+        if (lab[u] >= 0 && rv && (!VW || w > 0.0)) {
+          const int slot = k * NB + lab[u];
+          atomicAdd(ar + slot, VW ? w * r : r);
+          atomicAdd(aw + slot, w);
+        }
+      }
+    }
+  }
+  const double x1 = wave_sum(ft), y1 = wave_sum(fb);
+  if (lane == 0) { red[wid][0] = x1; red[wid][1] = y1; }
+  __syncthreads();
+  for (int i = tid; i < K * NB; i += PF_THREADS) {
+    const int k = i / NB, d = i - k * NB;
+    double x = 0.0, y = 0.0;
+    for (int w2 = 0; w2 < PF_WAVES; ++w2) { x += acc_r[w2][i]; y += acc_w[w2][i]; }
+    const int64_t ob = (((int64_t)tb * K + k) * C + c) * NB + d;
+    SWRp[ob] = k < kmax ? x : 0.0;
+    SWp[ob] = k < kmax ? y : 0.0;
+  }
+  if (tid < 2) {
+    double x = 0.0;
+    for (int w2 = 0; w2 < PF_WAVES; ++w2) x += red[w2][tid];
+    FWp[((int64_t)tb * C + c) * 2 + tid] = x;
   }
 }
 
@@ -422,6 +503,9 @@ __global__ __launch_bounds__(256) void k_bootstrap_panel(const double* __restric
 }
 
 // ------------------------------------------------------------------------------- C ABI
+// 1: cohort sums through per-wave LDS atomics (k_cohort_lds) where they fit; 0: registers
+static int g_tune_cohort_lds = 1;
+
 struct PfPlan {
   int C, kpar, Ct;
   int64_t CH, CHt;
@@ -455,6 +539,16 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                           const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
                           double* SWp, double* FWp) {
   const dim3 g((unsigned)pl.C, (unsigned)(T_m * B), pl.kpar ? (unsigned)K : 1u);
+  if (g_tune_cohort_lds && !pl.kpar && K * NB <= AC_MAXKD) {
+    const dim3 g2((unsigned)pl.C, (unsigned)(T_m * B));
+    if (W)
+      hipLaunchKernelGGL((k_cohort_lds<NB, true>), g2, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B,
+                         N, K, pl.C, pl.CH, SWRp, SWp, FWp);
+    else
+      hipLaunchKernelGGL((k_cohort_lds<NB, false>), g2, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B,
+                         N, K, pl.C, pl.CH, SWRp, SWp, FWp);
+    return;
+  }
   if (W)
     hipLaunchKernelGGL((k_cohort<NB, true>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
                        pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp);
@@ -484,6 +578,14 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
 }
 
 extern "C" {
+
+int csm_tune_portfolio(const char* key, int value) {
+  if (key && !strcmp(key, "cohort_lds") && (value == 0 || value == 1)) {
+    g_tune_cohort_lds = value;
+    return CSM_OK;
+  }
+  return CSM_E_INVAL;
+}
 
 int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t K) {
   if (T_m < 0 || B < 1 || N <= 0 || n_bins < 1 || K < 1) return 0;

@@ -199,3 +199,25 @@ def test_portfolio_multi_shares_cohort_pass(engine):
         one = engine.portfolio(L, NR, 10, K=K, W=W)
         for f in ("PR", "LS", "TURN", "COST", "NET"):
             assert bits_equal(getattr(got, f).cpu().numpy(), getattr(one, f).cpu().numpy()), (K, f)
+
+
+@pytest.mark.parametrize("vw", [False, True])
+def test_cohort_lds_variant_deterministic_and_equal(engine, vw):
+    """The LDS-atomic cohort kernel: identical bits on repeated runs, and within 1e-10 of the
+    register-accumulator kernel (different summation order)."""
+    L, NR, _, PM = _labels(engine, "c1")
+    W = _up(np.abs(PM.cpu().numpy()) * 1e6) if vw else None
+    lib = engine.lib
+    try:
+        assert lib.csm_tune(b"cohort_lds", 1) == 0
+        a = engine.portfolio_multi(L, NR, 10, Ks=(3, 12), W=W)
+        b = engine.portfolio_multi(L, NR, 10, Ks=(3, 12), W=W)
+        assert lib.csm_tune(b"cohort_lds", 0) == 0
+        c = engine.portfolio_multi(L, NR, 10, Ks=(3, 12), W=W)
+    finally:
+        lib.csm_tune(b"cohort_lds", 1)
+    for K in (3, 12):
+        for f in ("PR", "LS", "TURN", "NET"):
+            x, y, z = (getattr(o[K], f).cpu().numpy() for o in (a, b, c))
+            assert bits_equal(x, y), (K, f)
+            assert np.array_equal(np.isnan(x), np.isnan(z)) and max_rel(x, z) <= 1e-10, (K, f)
