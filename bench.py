@@ -364,12 +364,16 @@ class TimedStages:
         return self._wrap("portfolio(k_cohort+k_turnover+k_overlap+k_ls)", per * T_m * BN,
                           self.eng.portfolio_multi, L, NR, n_bins, **k)
 
+    def summary(self, LS, TURN=None, COST=None, NET=None, **k):
+        return self._wrap("summary(k_summary)", 8.0 * LS.numel() * (4 if TURN is not None else 1),
+                          self.eng.summary, LS, TURN, COST, NET, **k)
+
     def bootstrap(self, R, B, **k):
         T_m, N = R.shape
         return self._wrap("bootstrap(k_bootstrap_*)", 16.0 * T_m * B * N, self.eng.bootstrap,
                           R, B, **k)
 
-    def summary(self, steps):
+    def stage_report(self, steps):
         agg = {}
         for name, e0, e1, nb in self.rec:
             ms, tot = agg.get(name, (0.0, 0.0))
@@ -454,7 +458,7 @@ def sweep_main(args):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    stages = ts.summary(args.steps)
+    stages = ts.stage_report(args.steps)
     if rank == 0:
         dom = max(stages.items(), key=lambda kv: kv[1][0])
         dname, (dms, dbytes) = dom

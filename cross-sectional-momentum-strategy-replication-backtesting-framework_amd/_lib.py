@@ -25,7 +25,7 @@ EXPORTS = (
     "csm_tiled_size", "csm_portfolio", "csm_portfolio_workspace", "csm_bootstrap",
     "csm_cohort_sums", "csm_portfolio_from_cohorts", "csm_turnover_features",
     "csm_double_sort_labels", "csm_tune_ptr", "csm_next_present",
-    "csm_last_present_month", "csm_portfolio_from_cohorts_multi",
+    "csm_last_present_month", "csm_portfolio_from_cohorts_multi", "csm_summary",
 )
 
 
@@ -83,6 +83,7 @@ def _declare(lib):
         "csm_portfolio_from_cohorts_multi": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
                                                             _i32, _i32, _p, _f64, _f64, _f64, _p,
                                                             _p, _p, _p, _p, _p, _p, _p]),
+        "csm_summary": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _f64, _p]),
         "csm_bootstrap": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64,
                                          _f64, _p, _p]),
         "csm_tile_panel": (ctypes.c_int, [_p, _p, _i64, _i64, _p]),

@@ -383,13 +383,16 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
 }
 
 // ------------------------------------------------------------------------------ E2, E3
-// one 64-lane workgroup per (t, b): lane d < nb combines decile d over the chunks and the
-// cohorts; lane 0 also totals the turnover / cost partials.
+// one 64-lane workgroup per (t, b, holding period q of the K set): lane d < nb combines decile
+// d over the chunks and the cohorts; lane 0 also totals the turnover / cost partials.  Output
+// q lands at offset q * rows of the [nK][T_m][B] stacks (PR: [nK][T_m][B][nb]).
 __global__ __launch_bounds__(64) void k_overlap(
-    const double* __restrict__ SWRp, const double* __restrict__ SWp, int K, int Kmax, int C, int nb,
-    const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
-    double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST) {
+    const double* __restrict__ SWRp, const double* __restrict__ SWp, KSet ks, int Kmax, int C,
+    int nb, const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
+    int64_t rows, double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST) {
   const int64_t tb = blockIdx.x;
+  const int q = blockIdx.y;
+  const int K = ks.K[q];
   const int d = threadIdx.x;
   if (d < nb) {
     double acc = 0.0;
@@ -403,21 +406,27 @@ __global__ __launch_bounds__(64) void k_overlap(
       }
       if (y > 0.0) { acc += x / y; ++n; }
     }
-    PR[tb * nb + d] = n > 0 ? acc / (double)n : qnan();
+    PR[(q * rows + tb) * nb + d] = n > 0 ? acc / (double)n : qnan();
   }
   if (d == 0 && TURNp) {
+    const int64_t to = (q * rows + tb) * Ct;
     double x = 0.0, y = 0.0;
-    for (int c = 0; c < Ct; ++c) { x += TURNp[tb * Ct + c]; y += COSTp[tb * Ct + c]; }
-    if (TURN) TURN[tb] = x;
-    if (COST) COST[tb] = y;
+    for (int c = 0; c < Ct; ++c) { x += TURNp[to + c]; y += COSTp[to + c]; }
+    if (TURN) TURN[q * rows + tb] = x;
+    if (COST) COST[q * rows + tb] = y;
   }
 }
 
+// one workgroup per (panel b, holding period q): the reference's long-short rule on PR[q].
 __global__ __launch_bounds__(256) void k_ls(const double* __restrict__ PR, int T_m, int B, int nb,
                                             double* __restrict__ LS,
                                             const double* __restrict__ COST,
                                             double* __restrict__ NET) {
   const int b = blockIdx.x;
+  const int64_t qo = (int64_t)blockIdx.y * T_m * B;
+  PR += qo * nb;
+  LS += qo;
+  if (NET) { NET += qo; COST += qo; }
   __shared__ int has_lo, has_hi;
   if (threadIdx.x == 0) { has_lo = 0; has_hi = 0; }
   __syncthreads();
@@ -649,22 +658,20 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
                          SIG, ws + lay.turn, ws + lay.cost);
       LAUNCH_CHECK(ctx, "k_turnover");
     }
-    for (int q = 0; q < ks.n; ++q) {
-      const int qq = q0 + q;
-      const int64_t tq = (int64_t)q * lay.rows * lay.p.Ct;
-      double* TURNq = TURN ? TURN + qq * rb : nullptr;
-      double* COSTq = COST ? COST + qq * rb : nullptr;
-      double* NETq = NET ? NET + qq * rb : nullptr;
-      double* PRq = PR + qq * rb * n_bins;
-      hipLaunchKernelGGL(k_overlap, dim3((unsigned)lay.rows), dim3(64), 0, st,
-                         (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks.K[q],
-                         Kmax, lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn + tq) : nullptr,
-                         (const double*)(ws + lay.cost + tq), lay.p.Ct, PRq, TURNq, COSTq);
-      LAUNCH_CHECK(ctx, "k_overlap");
-      hipLaunchKernelGGL(k_ls, dim3((unsigned)B), dim3(256), 0, st, (const double*)PRq, T_m, B,
-                         n_bins, LS + qq * rb, (const double*)COSTq, NETq);
-      LAUNCH_CHECK(ctx, "k_ls");
-    }
+    double* TURNq = TURN ? TURN + q0 * rb : nullptr;
+    double* COSTq = COST ? COST + q0 * rb : nullptr;
+    double* NETq = NET ? NET + q0 * rb : nullptr;
+    double* PRq = PR + q0 * rb * n_bins;
+    hipLaunchKernelGGL(k_overlap, dim3((unsigned)lay.rows, (unsigned)ks.n), dim3(64), 0, st,
+                       (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks, Kmax,
+                       lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
+                       (const double*)(ws + lay.cost), lay.p.Ct, (int64_t)lay.rows, PRq, TURNq,
+                       COSTq);
+    LAUNCH_CHECK(ctx, "k_overlap");
+    hipLaunchKernelGGL(k_ls, dim3((unsigned)B, (unsigned)ks.n), dim3(256), 0, st,
+                       (const double*)PRq, T_m, B, n_bins, LS + q0 * rb, (const double*)COSTq,
+                       NETq);
+    LAUNCH_CHECK(ctx, "k_ls");
   }
   return CSM_OK;
 }
@@ -849,6 +856,92 @@ int csm_double_sort_labels(csm_ctx* ctx, const double* M, const double* X, const
     hipLaunchKernelGGL(k_combine_labels, dim3(g), dim3(256), 0, ctx->stream, Lm, Lv, n, n_vol, Lc);
     LAUNCH_CHECK(ctx, "k_combine_labels");
   }
+  return CSM_OK;
+}
+
+}  // extern "C"
+
+// =====================================================================================
+// Per-(strategy, panel) performance summary of the long-short series, the sweep's last step
+// (src/utils.py:8-16 Sharpe at `freq` periods a year; NaN months dropped, run_demo.py:67):
+// months, mean, Sharpe (ddof = 1), mean turnover, mean cost, mean and Sharpe of net.  One
+// workgroup per (panel, strategy); fixed-order reductions (mean first, then squared
+// deviations, as NumPy's std does).
+// =====================================================================================
+#define SUM_FIELDS 7
+__device__ __forceinline__ double block_sum256(double v, double* scr) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) scr[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < PF_WAVES; ++w) s += scr[w];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(PF_THREADS) void k_summary(const double* __restrict__ LS,
+                                                        const double* __restrict__ TURN,
+                                                        const double* __restrict__ COST,
+                                                        const double* __restrict__ NET, int T_m,
+                                                        int B, double freq,
+                                                        double* __restrict__ out) {
+  __shared__ double scr[PF_WAVES];
+  const int b = blockIdx.x, q = blockIdx.y;
+  const int64_t base = (int64_t)q * T_m * B;
+  double n = 0.0, s = 0.0, st = 0.0, sc = 0.0, sn = 0.0;
+  for (int t = threadIdx.x; t < T_m; t += PF_THREADS) {
+    const int64_t o = base + (int64_t)t * B + b;
+    const double x = LS[o];
+    if (x == x) {
+      n += 1.0;
+      s += x;
+      if (TURN) { st += TURN[o]; sc += COST[o]; sn += NET[o]; }
+    }
+  }
+  n = block_sum256(n, scr);
+  s = block_sum256(s, scr);
+  st = block_sum256(st, scr);
+  sc = block_sum256(sc, scr);
+  sn = block_sum256(sn, scr);
+  const double mean = s / n, nmean = sn / n;
+  double v = 0.0, vn = 0.0;
+  for (int t = threadIdx.x; t < T_m; t += PF_THREADS) {
+    const int64_t o = base + (int64_t)t * B + b;
+    const double x = LS[o];
+    if (x == x) {
+      v += (x - mean) * (x - mean);
+      if (NET) vn += (NET[o] - nmean) * (NET[o] - nmean);
+    }
+  }
+  v = block_sum256(v, scr);
+  vn = block_sum256(vn, scr);
+  if (threadIdx.x == 0) {
+    const double sd = sqrt(v / (n - 1.0)), sdn = sqrt(vn / (n - 1.0));
+    const double rf = sqrt(freq);
+    double* o = out + ((int64_t)q * B + b) * SUM_FIELDS;
+    o[0] = n;
+    o[1] = mean;
+    o[2] = sd > 0.0 ? mean * freq / (sd * rf) : qnan();
+    o[3] = TURN ? st / n : qnan();
+    o[4] = TURN ? sc / n : qnan();
+    o[5] = TURN ? nmean : qnan();
+    o[6] = (TURN && sdn > 0.0) ? nmean * freq / (sdn * rf) : qnan();
+  }
+}
+
+extern "C" {
+
+int csm_summary(csm_ctx* ctx, const double* LS, const double* TURN, const double* COST,
+                const double* NET, int32_t nS, int32_t T_m, int32_t B, double freq,
+                double* out) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!LS || !out || nS < 1 || T_m < 0 || B < 1 || !(freq > 0.0) ||
+      ((TURN != nullptr) != (COST != nullptr)) || ((TURN != nullptr) != (NET != nullptr)))
+    return set_err(ctx, CSM_E_INVAL, "csm_summary: bad arguments (nS=%d T_m=%d B=%d)", nS, T_m, B);
+  hipLaunchKernelGGL(k_summary, dim3((unsigned)B, (unsigned)nS), dim3(PF_THREADS), 0, ctx->stream,
+                     LS, TURN, COST, NET, T_m, B, freq, out);
+  LAUNCH_CHECK(ctx, "k_summary");
   return CSM_OK;
 }
 

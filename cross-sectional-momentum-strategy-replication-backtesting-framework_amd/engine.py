@@ -383,7 +383,7 @@ class Engine:
 
     def portfolio_multi(self, L, NR, n_bins=10, Ks=(1,), W=None, B=1, half_spread=0.0005,
                         k_impact=0.1, aum=0.0, ADV=None, SIG=None, with_costs=True,
-                        workspace=None):
+                        workspace=None, return_stacked=False):
         """One cohort-sum pass (csm_cohort_sums, Kmax = max(Ks)) shared by the accounting of
         every holding period K in Ks (csm_portfolio_from_cohorts).  Returns {K: PortfolioOut}."""
         T_m, BN = L.shape
@@ -413,8 +413,26 @@ class Engine:
                    float(k_impact), float(aum), _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS),
                    _ptr(TURN), _ptr(COST), _ptr(NET), _ptr(workspace))
         pick = lambda x, q: None if x is None else x[q]
-        return {K: PortfolioOut(PR=PR[q], LS=LS[q], TURN=pick(TURN, q), COST=pick(COST, q),
-                                NET=pick(NET, q)) for q, K in enumerate(Ks)}
+        res = {K: PortfolioOut(PR=PR[q], LS=LS[q], TURN=pick(TURN, q), COST=pick(COST, q),
+                               NET=pick(NET, q)) for q, K in enumerate(Ks)}
+        if return_stacked:
+            return res, PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET)
+        return res
+
+    def summary(self, LS, TURN=None, COST=None, NET=None, freq=12.0):
+        """csm_summary: [nS][B][7] (months, mean, Sharpe, turnover, cost, net mean, net
+        Sharpe) from stacked [nS][T_m][B] series (or one [T_m][B] series: nS = 1)."""
+        if LS.dim() == 2:
+            LS = LS.unsqueeze(0)
+            TURN, COST, NET = (None if x is None else x.unsqueeze(0) for x in (TURN, COST, NET))
+        nS, T_m, B = LS.shape
+        for t, nm in ((LS, "LS"), (TURN, "TURN"), (COST, "COST"), (NET, "NET")):
+            if t is not None:
+                _need(t, nm, torch.float64, (nS, T_m, B), self.device)
+        out = self.empty((nS, B, 7))
+        self._call("csm_summary", _ptr(LS), _ptr(TURN), _ptr(COST), _ptr(NET), nS, T_m, B,
+                   float(freq), _ptr(out))
+        return out
 
     def turnover_features(self, PM, VOL, so, mcap, lookback=3):
         """csm_turnover_features (src/features.py:60-107, rule T1): (ADV, SH, TURN, TAVG)."""

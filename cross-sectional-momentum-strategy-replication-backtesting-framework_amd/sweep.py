@@ -108,7 +108,7 @@ class SweepRunner:
         c, st = self.cfg, self.st
         T_m, BN = PMb.shape
         N = BN // B
-        rows, series = [], {}
+        rows, series, summ = [], {}, {}
         kw = dict(W=W, B=B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum, ADV=ADV,
                   SIG=SIG, with_costs=c.costs)
         for J in c.Js:   # one J's monthly panels live at a time
@@ -116,7 +116,12 @@ class SweepRunner:
             L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M
             L = L.reshape(T_m, BN)
-            if hasattr(st, "portfolio_multi"):   # one cohort pass serves every K of this J
+            if hasattr(st, "summary"):   # device path: one cohort pass for every K of this J,
+                outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)
+                summ_j = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # summaries on device
+                for q, K in enumerate(c.Ks):
+                    summ[(J, K)] = summ_j[q]
+            elif hasattr(st, "portfolio_multi"):
                 outs = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, **kw)
             else:
                 outs = {K: st.portfolio(L, NR, c.n_bins, K=K, **kw) for K in c.Ks}
@@ -124,8 +129,11 @@ class SweepRunner:
                 series[(J, K)] = outs[K]
             del L, NR
         for (J, K) in c.strategies:
-            out = series[(J, K)]
-            rows.append(summarize(out.LS, out.TURN, out.COST, out.NET))
+            if (J, K) in summ:
+                rows.append(summ[(J, K)])
+            else:
+                out = series[(J, K)]
+                rows.append(summarize(out.LS, out.TURN, out.COST, out.NET))
         return torch.stack(rows, dim=1), series                  # [B][S][F]
 
     def run_bootstrap(self, R_base: torch.Tensor, n_panels: int, seed: int = 5000,

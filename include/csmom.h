@@ -232,6 +232,16 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
                                      double* TURN, double* COST, double* NET, void* workspace);
 
 /*
+ * Performance summary per (strategy, panel) of stacked long-short series (LS, and the
+ * nullable-together TURN / COST / NET, each [nS][T_m][B]): out [nS][B][7] = months, mean,
+ * Sharpe (src/utils.py:8-16 at `freq` periods a year, ddof = 1), mean turnover, mean cost,
+ * net mean, net Sharpe; NaN months dropped (run_demo.py:67).
+ */
+int csm_summary(csm_ctx* ctx, const double* LS, const double* TURN, const double* COST,
+                const double* NET, int32_t nS, int32_t T_m, int32_t B, double freq,
+                double* out);
+
+/*
  * Stationary month bootstrap (BASELINE config C5; rule E6): panels b0 .. b0+B-1 of the base
  * month-return panel R[T_m][N] (csm_momentum's R; NaN = no row).  src[B][T_m] int32 out: the
  * source months; PMb[T_m][B][N] out: month prices p0 * prod(1 + r) over the resampled months,

@@ -221,3 +221,53 @@ def test_cohort_lds_variant_deterministic_and_equal(engine, vw):
             x, y, z = (getattr(o[K], f).cpu().numpy() for o in (a, b, c))
             assert bits_equal(x, y), (K, f)
             assert np.array_equal(np.isnan(x), np.isnan(z)) and max_rel(x, z) <= 1e-10, (K, f)
+
+
+def _summary_ref(LS, TURN, COST, NET, freq=12.0):
+    """NumPy restatement of sweep.summarize per (strategy, panel) (src/utils.py:8-16)."""
+    nS, T_m, B = LS.shape
+    out = np.full((nS, B, 7), np.nan)
+    for q in range(nS):
+        for b in range(B):
+            x = LS[q, :, b]
+            ok = ~np.isnan(x)
+            n = ok.sum()
+            out[q, b, 0] = n
+
+            def sh(v):
+                if n < 2:
+                    return np.mean(v) if n else np.nan, np.nan
+                m, sd = np.mean(v), np.std(v, ddof=1)
+                return m, (m * freq / (sd * np.sqrt(freq)) if sd > 0 else np.nan)
+            out[q, b, 1], out[q, b, 2] = sh(x[ok])
+            if TURN is not None and n:
+                out[q, b, 3] = TURN[q, ok, b].mean()
+                out[q, b, 4] = COST[q, ok, b].mean()
+                out[q, b, 5], out[q, b, 6] = sh(NET[q, ok, b])
+    return out
+
+
+@pytest.mark.parametrize("costs", [True, False])
+def test_summary_kernel(engine, costs):
+    """csm_summary against a NumPy restatement: NaN months dropped, an all-NaN panel, a
+    one-month panel and a constant panel (Sharpe NaN), several strategies in one launch."""
+    rng = np.random.default_rng(3)
+    nS, T_m, B = 3, 500, 7
+    LS = rng.normal(0.01, 0.05, (nS, T_m, B))
+    LS[rng.random(LS.shape) < 0.1] = np.nan
+    LS[:, :, 2] = np.nan
+    LS[:, :, 3] = np.nan
+    LS[:, 17, 3] = 0.02
+    LS[:, :, 4] = 0.25          # exact sums: sd == 0 -> Sharpe NaN
+    TURN = np.abs(rng.normal(0.3, 0.1, LS.shape))
+    COST = TURN * 0.001
+    NET = LS - COST
+    args = (LS, TURN, COST, NET) if costs else (LS, None, None, None)
+    got = engine.summary(*[None if a is None else _up(a) for a in args]).cpu().numpy()
+    ref = _summary_ref(*args)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    m = ~np.isnan(ref)
+    assert np.allclose(got[m], ref[m], rtol=1e-12, atol=1e-15)
+    # one [T_m][B] series is nS = 1
+    one = engine.summary(*[None if a is None else _up(a[1]) for a in args]).cpu().numpy()
+    assert bits_equal(one[0], got[1])
