@@ -59,8 +59,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
     int T_m, int B, int64_t N, int K, int C, int64_t CH, int kpar, double* __restrict__ SWRp,
     double* __restrict__ SWp, double* __restrict__ FWp) {
   __shared__ double red[PF_WAVES][2 * NB + 2];
-  const int c = blockIdx.x;
-  const int tb = blockIdx.y;
+  const int c = (int)(blockIdx.x % (unsigned)C);
+  const int tb = (int)(blockIdx.x / (unsigned)C);
   const int t = tb / B, b = tb - t * B;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t a0 = (int64_t)c * CH;
@@ -157,8 +157,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
   __shared__ double acc_r[PF_WAVES][AC_MAXKD];   // sum of w * r per (age, decile)
   __shared__ double acc_w[PF_WAVES][AC_MAXKD];   // sum of w (equal weight: the count)
   __shared__ double red[PF_WAVES][2];
-  const int c = blockIdx.x;
-  const int tb = blockIdx.y;
+  const int c = (int)(blockIdx.x % (unsigned)C);
+  const int tb = (int)(blockIdx.x / (unsigned)C);
   const int t = tb / B, b = tb - t * B;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int KD = K * NB;
@@ -222,6 +222,247 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
   }
 }
 
+// Cohort sums from label-sorted formation rows.  k_label_sort turns each formation row (s, b)
+// into a stable counting sort of its members by decile (asset ids as uint16, segment offsets,
+// and for value weights the sanitised weights in the same order), plus the row's formation
+// leg totals.  k_cohort_seg then holds the return row of month t in LDS and, per (age k,
+// decile d) segment of the row formed at t - k, gathers the members' returns: no per-decile
+// selects and no atomics, one LDS read per (cell, age).  A row's sort is read by the K months
+// that hold it (from L2 / MALL).  Chunks split every segment by position, and the partials are
+// combined in chunk order like the other cohort kernels'.  Used for N <= SEG_MAXN.
+#define SEG_MAXN 7168   // VW sort stages 9 bytes per cell in LDS: <= 64 KB per workgroup
+template <int NB, bool VW>
+__global__ __launch_bounds__(PF_THREADS) void k_label_sort(
+    const int8_t* __restrict__ L, const double* __restrict__ W, int64_t N, int C,
+    uint16_t* __restrict__ PERM, int32_t* __restrict__ OFF, double* __restrict__ WSRT,
+    double* __restrict__ FWp) {
+  // the row is staged in LDS first (all loads in flight at once), then both passes read LDS
+  extern __shared__ double wl[];                  // VW: weights [N], then labels [N]
+  int8_t* ll = VW ? (int8_t*)(wl + N) : (int8_t*)wl;
+  __shared__ int cnts[PF_WAVES][NB];
+  __shared__ double red[PF_WAVES][2];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int8_t* Lr = L + row * N;
+  const double* Wr = VW ? W + row * N : nullptr;
+  if (!VW && (N & 3) == 0) {   // 4-byte aligned rows: word loads
+    const uint32_t* L4 = (const uint32_t*)Lr;
+    uint32_t* l4 = (uint32_t*)ll;
+    const int nw = (int)(N >> 2);
+#pragma unroll 4
+    for (int i = tid; i < nw; i += PF_THREADS) l4[i] = L4[i];
+  } else {
+#pragma unroll 4
+    for (int a = tid; a < (int)N; a += PF_THREADS) {
+      int lab = (int)Lr[a];
+      if (VW) {
+        const double w = Wr[a];
+        wl[a] = w;
+        if (!(w > 0.0 && w < INFINITY)) lab = -1;   // no valid weight: not a member
+      }
+      ll[a] = (int8_t)lab;
+    }
+  }
+  __syncthreads();
+  const int64_t Q = ((N + PF_WAVES - 1) / PF_WAVES + 63) / 64 * 64;   // wave quarter, whole tiles
+  const int64_t q0 = wid * Q, q1 = q0 + Q < N ? q0 + Q : N;
+  int cnt[NB];
+#pragma unroll
+  for (int d = 0; d < NB; ++d) cnt[d] = 0;
+  for (int64_t a0 = q0; a0 < q1; a0 += 64) {
+    const int64_t a = a0 + lane;
+    const int lab = a < q1 ? (int)ll[a] : -1;
+#pragma unroll
+    for (int d = 0; d < NB; ++d) cnt[d] += __popcll(__ballot(lab == d));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < NB; ++d) cnts[wid][d] = cnt[d];
+  }
+  __syncthreads();
+  int base[NB];
+  int run = 0;
+#pragma unroll
+  for (int d = 0; d < NB; ++d) {
+    int before = 0, tot = 0;
+    for (int w2 = 0; w2 < PF_WAVES; ++w2) {
+      const int v = cnts[w2][d];
+      before += w2 < wid ? v : 0;
+      tot += v;
+    }
+    base[d] = run + before;
+    if (tid == 0) OFF[row * (NB + 1) + d] = run;
+    run += tot;
+  }
+  if (tid == 0) OFF[row * (NB + 1) + NB] = run;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  double ft = 0.0, fb = 0.0;
+  for (int64_t a0 = q0; a0 < q1; a0 += 64) {
+    const int64_t a = a0 + lane;
+    const int lab = a < q1 ? (int)ll[a] : -1;
+    int pos = -1;
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+      const uint64_t m = __ballot(lab == d);
+      if (lab == d) pos = base[d] + __popcll(m & lt);
+      base[d] += __popcll(m);
+    }
+    if (pos >= 0) {
+      PERM[row * N + pos] = (uint16_t)a;
+      if (VW) {
+        const double w = wl[a];
+        WSRT[row * N + pos] = w;
+        ft += lab == NB - 1 ? w : 0.0;
+        fb += lab == 0 ? w : 0.0;
+      }
+    }
+  }
+  if (VW) {
+    const double x = wave_sum(ft), y = wave_sum(fb);
+    if (lane == 0) { red[wid][0] = x; red[wid][1] = y; }
+    __syncthreads();
+  }
+  for (int i = tid; i < 2 * C; i += PF_THREADS) {   // leg totals in chunk 0, zeros elsewhere
+    const int c = i >> 1, leg = i & 1;
+    double v = 0.0;
+    if (c == 0) {
+      if (VW) {
+        for (int w2 = 0; w2 < PF_WAVES; ++w2) v += red[w2][leg];
+      } else {
+        const int d = leg == 0 ? NB - 1 : 0;
+        for (int w2 = 0; w2 < PF_WAVES; ++w2) v += (double)cnts[w2][d];
+      }
+    }
+    FWp[(row * C + c) * 2 + leg] = v;
+  }
+}
+
+// 16-lane groups, one (age, decile) segment per group at a time: a short reduction (4 steps)
+// per segment instead of a 64-lane one, and four segments per wave instruction.  The segment
+// offsets of all K formation rows are fetched into LDS with the return row, and a group reads
+// its segment's ids as 8-byte words (4 ids), up to 8 words per lane in flight, so one round
+// trip to L2 covers a typical segment.
+#define SEG_G 16
+#define SEG_MAXKD 512   // K * (n_bins + 1) offsets staged in LDS
+template <int NB, bool VW>
+__global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
+    const double* __restrict__ NR, const uint16_t* __restrict__ PERM,
+    const int32_t* __restrict__ OFF, const double* __restrict__ WSRT, int T_m, int B, int64_t N,
+    int K, int C, int xcd, double* __restrict__ SWRp, double* __restrict__ SWp) {
+  extern __shared__ double rl[];   // the return row of month t (N values)
+  __shared__ int32_t offs[SEG_MAXKD];
+  int c = 0;
+  int64_t tb;
+  int t;
+  if (xcd) {   // C == 1
+    // XCD-aware order: workgroups go round-robin to the 8 XCDs, so workgroup id -> (t, b)
+    // keeps panel b on XCD b % 8 with t advancing slowly; the K formation rows a panel's
+    // months re-read then stay in that XCD's L2.
+    const int id = (int)blockIdx.x, x = id & 7, j = id >> 3;
+    const int Bx = (B + 7) >> 3;
+    t = j / Bx;
+    const int b = x + 8 * (j - t * Bx);
+    if (b >= B || t >= T_m) return;
+    tb = (int64_t)t * B + b;
+  } else {
+    c = (int)(blockIdx.x % (unsigned)C);
+    tb = blockIdx.x / (unsigned)C;
+    t = (int)(tb / B);
+  }
+  const int tid = threadIdx.x;
+  const int grp = tid / SEG_G, sl = tid % SEG_G;
+  const int kmax = t + 1 < K ? t + 1 : K;
+  const double* NRr = NR + tb * N;
+  for (int i = tid; i < kmax * (NB + 1); i += PF_THREADS) {
+    const int k = i / (NB + 1), e = i - k * (NB + 1);
+    offs[i] = OFF[(tb - (int64_t)k * B) * (NB + 1) + e];
+  }
+#pragma unroll 8
+  for (int a = tid; a < (int)N; a += PF_THREADS) rl[a] = NRr[a];
+  __syncthreads();
+  const bool vec = (N & 3) == 0;   // id rows 8-byte aligned
+  // chunk c owns the segments g = c (mod C) whole and writes zeros for the others (exact
+  // under the chunk-order sum of k_overlap)
+  for (int g = tid; g < K * NB && C > 1; g += PF_THREADS) {
+    if (g % C == c) continue;
+    const int k = g / NB, d = g - k * NB;
+    const int64_t ob = ((tb * K + k) * C + c) * NB + d;
+    SWRp[ob] = 0.0;
+    SWp[ob] = 0.0;
+  }
+  for (int g = c + grp * C; g < K * NB; g += (PF_THREADS / SEG_G) * C) {
+    const int k = g / NB, d = g - k * NB;
+    const int64_t ob = ((tb * K + k) * C + c) * NB + d;
+    if (k >= kmax) {
+      if (sl == 0) { SWRp[ob] = 0.0; SWp[ob] = 0.0; }
+      continue;
+    }
+    const int64_t srow = tb - (int64_t)k * B;
+    const int64_t lo = offs[k * (NB + 1) + d], hi = offs[k * (NB + 1) + d + 1];
+    const uint16_t* P = PERM + srow * N;
+    const double* Ws = VW ? WSRT + srow * N : nullptr;
+    double sr = 0.0, sw = 0.0;
+    int n = 0;
+    auto take = [&](int64_t j, int id) {
+      const double x = rl[id];
+      if (x == x) {
+        if (VW) {
+          const double w = Ws[j];
+          sr += w * x;
+          sw += w;
+        } else {
+          sr += x;
+          ++n;
+        }
+      }
+    };
+    if (vec) {
+      const uint64_t* P8 = (const uint64_t*)P;
+      constexpr int U = 8;
+      for (int64_t q0 = (lo >> 2) + sl; q0 * 4 < hi; q0 += U * SEG_G) {
+        uint64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t q = q0 + u * SEG_G;
+          v[u] = q * 4 < hi ? P8[q] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j0 = (q0 + u * SEG_G) * 4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t j = j0 + e;
+            if (j >= lo && j < hi) take(j, (int)((v[u] >> (16 * e)) & 0xffffu));
+          }
+        }
+      }
+    } else {
+      constexpr int U = 8;
+      for (int64_t j0 = lo + sl; j0 < hi; j0 += U * SEG_G) {
+        int idx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j = j0 + u * SEG_G;
+          idx[u] = j < hi ? (int)P[j] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (idx[u] >= 0) take(j0 + u * SEG_G, idx[u]);
+      }
+    }
+#pragma unroll
+    for (int o = SEG_G / 2; o > 0; o >>= 1) {
+      sr += __shfl_xor(sr, o, SEG_G);
+      if (VW) sw += __shfl_xor(sw, o, SEG_G);
+      else n += __shfl_xor(n, o, SEG_G);
+    }
+    if (sl == 0) {
+      SWRp[ob] = sr;
+      SWp[ob] = VW ? sw : (double)n;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ E4, E5
 // w_u = (1/K_u) sum over the non-empty cohorts s in (u-K, u] of omega_s, omega_s[a] =
 // W[s][a] / total_s.  When both windows of months t and t-1 are full (K non-empty cohorts
@@ -236,14 +477,29 @@ struct KSet {
   int K[TO_MAXQ];
 };
 
+// labels of CW consecutive cells (CW = 4: one 4-byte load, the row offset being 4-aligned)
+template <int CW>
+__device__ __forceinline__ void load_labels(const int8_t* __restrict__ p, int* lab) {
+  if constexpr (CW == 4) {
+    const uint32_t v = *(const uint32_t*)p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lab[e] = (int)(int8_t)(v >> (8 * e));
+  } else {
+    lab[0] = (int)*p;
+  }
+}
+
+__device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INFINITY) ? x : 0.0; }
+
+template <bool VW, bool IMP>
 __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
     int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
-    double half_spread, double k_impact, double aum, const double* __restrict__ ADV,
+    int Ct, double half_spread, double k_impact, double aum, const double* __restrict__ ADV,
     const double* __restrict__ SIG, double* __restrict__ TURNp, double* __restrict__ COSTp) {
-  const int c = blockIdx.x, Ct = gridDim.x;
-  const int tb = blockIdx.y;
-  const int rows = gridDim.y;
+  const int c = (int)(blockIdx.x % (unsigned)Ct);
+  const int tb = (int)(blockIdx.x / (unsigned)Ct);
+  const int rows = T_m * B;
   const int t = tb / B, b = tb - t * B;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ double inv[2][TO_MAXK + 1];      // [leg][j]: 1/total of cohort s = t - j (0 = empty)
@@ -273,112 +529,284 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
   const int64_t rt = ((int64_t)t * B + b) * N;
-  const bool impact = ADV && aum > 0.0;
+  const int64_t rowstep = (int64_t)B * N;
   const int nq = ks.n;
+  const int dtop = n_bins - 1;
+  // Equal weight (any cost model without impact): |w_t - w_{t-1}| of a cell in a full leg is
+  // inv0 (member at t only), invK (at t - K only), |inv0 - invK| (both) or 0, so a full leg's
+  // turnover is three member counts.  Counts are exact integers (both legs packed in one
+  // 32-bit word: a chunk holds < 65536 cells); f64 sums only for legs that are not full (the
+  // first months) and for value weights.  Every path gives a (K, leg) the same value, so a
+  // K's result does not depend on the other K of the set.
+  constexpr bool CNT = !VW && !IMP;
   double turn[TO_MAXQ], cost[TO_MAXQ];
+  uint32_t s1 = 0, s0[TO_MAXQ], sb[TO_MAXQ];   // packed counts: leg 0 (top) low half, leg 1 high
 #pragma unroll
-  for (int q = 0; q < TO_MAXQ; ++q) { turn[q] = 0.0; cost[q] = 0.0; }
+  for (int q = 0; q < TO_MAXQ; ++q) { turn[q] = 0.0; cost[q] = 0.0; s0[q] = 0; sb[q] = 0; }
   auto charge = [&](int q, double dw, double adv, double unit_sig) {
     turn[q] += dw;
-    double unit = half_spread;
-    if (impact && adv > 0.0) {
-      const double im = k_impact * unit_sig * sqrt(dw * aum / adv);
-      unit = unit + ((im == im) ? im : 0.0);
+    if (IMP) {
+      double unit = half_spread;
+      if (adv > 0.0) {
+        const double im = k_impact * unit_sig * sqrt(dw * aum / adv);
+        unit = unit + ((im == im) ? im : 0.0);
+      }
+      cost[q] += dw * unit;
     }
-    cost[q] += dw * unit;
   };
   bool all_full = true;
   for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
-  if (all_full) {
-    // steady state: 2 cells per lane per trip, every load issued before use
+  if (CNT && all_full && (N & 3) == 0) {
+    // steady state, 4 cells per lane per word (SWAR byte compares on the label words)
+    const uint32_t topw = (uint32_t)dtop * 0x01010101u;
+    auto beq = [](uint32_t z) {   // 0x80 in each byte of z that is zero
+      return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+    };
     constexpr int TU = 2;
-    for (int64_t i0 = a0 + tid; i0 < a1; i0 += TU * PF_THREADS) {
-      int l1[TU], l0[TU][TO_MAXQ];
-      double x1[TU], x0[TU][TO_MAXQ], adv[TU], sg[TU];
+    for (int64_t a = a0 + 4 * tid; a < a1; a += 4 * TU * PF_THREADS) {
+      uint32_t w1[TU], w0[TU][TO_MAXQ];
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        const int64_t a = i0 + (int64_t)u * PF_THREADS;
-        const bool in = a < a1;
-        l1[u] = in ? (int)L[rt + a] : -1;
-        x1[u] = (W && in) ? W[rt + a] : 1.0;
+        const int64_t x = a + (int64_t)u * 4 * PF_THREADS;
+        const bool in = x < a1;
+        w1[u] = in ? *(const uint32_t*)(L + rt + x) : 0xFFFFFFFFu;
 #pragma unroll
-        for (int q = 0; q < TO_MAXQ; ++q) {
-          const bool use = in && q < nq;
-          const int64_t rk = ((int64_t)(t - (use ? ks.K[q] : 0)) * B + b) * N;
-          l0[u][q] = use ? (int)L[rk + a] : -1;
-          x0[u][q] = (W && use) ? W[rk + a] : 1.0;
-        }
-        adv[u] = (impact && in) ? ADV[rt + a] : 0.0;
-        sg[u] = (impact && SIG && in) ? SIG[rt + a] : 0.02;
+        for (int q = 0; q < TO_MAXQ; ++q)
+          w0[u][q] = (in && q < nq) ? *(const uint32_t*)(L + rt - (int64_t)ks.K[q] * rowstep + x)
+                                    : 0xFFFFFFFFu;
       }
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        const double vw1 = (x1[u] > 0.0 && x1[u] < INFINITY) ? x1[u] : 0.0;
-        const double unit_sig = sg[u] == sg[u] ? sg[u] : 0.02;
+        const uint32_t e1t = beq(w1[u] ^ topw), e10 = beq(w1[u]);
+        s1 += __popc(e1t) + (__popc(e10) << 16);
 #pragma unroll
         for (int q = 0; q < TO_MAXQ; ++q) {
           if (q >= nq) break;
-          const double vw0 = (x0[u][q] > 0.0 && x0[u][q] < INFINITY) ? x0[u][q] : 0.0;
+          const uint32_t e0t = beq(w0[u][q] ^ topw), e00 = beq(w0[u][q]);
+          s0[q] += __popc(e0t) + (__popc(e00) << 16);
+          sb[q] += __popc(e1t & e0t) + (__popc(e10 & e00) << 16);
+        }
+      }
+    }
+  } else if (all_full && (N & 3) == 0) {
+    // steady state, 4 cells per lane (4-byte label loads; chunk bounds are multiples of 64):
+    // w_t - w_{t-1} needs the month-t and month t-K_q labels only
+    constexpr int CW = 4;
+    for (int64_t a = a0 + CW * tid; a < a1; a += CW * PF_THREADS) {
+      int l1[CW], l0[TO_MAXQ][CW];
+      double x1[CW], x0[TO_MAXQ][CW], adv[CW], sg[CW];
+      load_labels<CW>(L + rt + a, l1);
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q) {
+        if (q < nq) {
+          load_labels<CW>(L + rt - (int64_t)ks.K[q] * rowstep + a, l0[q]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < CW; ++e) l0[q][e] = -1;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < CW; ++e) {
+        x1[e] = VW ? W[rt + a + e] : 1.0;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q)
+          x0[q][e] = (VW && q < nq) ? W[rt - (int64_t)ks.K[q] * rowstep + a + e] : 1.0;
+        adv[e] = IMP ? ADV[rt + a + e] : 0.0;
+        sg[e] = (IMP && SIG) ? SIG[rt + a + e] : 0.02;
+      }
+#pragma unroll
+      for (int e = 0; e < CW; ++e) {
+        const double vw1 = VW ? valid_w(x1[e]) : 1.0;
+        const double unit_sig = sg[e] == sg[e] ? sg[e] : 0.02;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          if (q >= nq) break;
+          const double vw0 = VW ? valid_w(x0[q][e]) : 1.0;
           const int K = ks.K[q];
 #pragma unroll
           for (int li = 0; li < 2; ++li) {
-            const int d = li == 0 ? n_bins - 1 : 0;
-            const double w1 = (l1[u] == d ? vw1 : 0.0) * inv[li][0];
-            const double w0 = (l0[u][q] == d ? vw0 : 0.0) * inv[li][K];
-            charge(q, fabs(w1 - w0) * sk[q][li][0], adv[u], unit_sig);
+            const int d = li == 0 ? dtop : 0;
+            const double w1 = (l1[e] == d ? vw1 : 0.0) * inv[li][0];
+            const double w0 = (l0[q][e] == d ? vw0 : 0.0) * inv[li][K];
+            charge(q, fabs(w1 - w0) * sk[q][li][0], adv[e], unit_sig);
           }
         }
       }
     }
   } else {
-    for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
-      double unit_sig = 0.02, adv = 0.0;
-      if (impact) {
+    // general rows: one pass over the ages j <= max K_q per cell, the age loads unrolled so
+    // they are in flight together; w_t and w_{t-1} sums for every (q, leg) at once.  Cells go
+    // to lanes as in the steady paths (4 consecutive per lane when N % 4 == 0), so a row's
+    // sums have the same order whichever path it takes.
+    int kq = 0;
+    for (int q = 0; q < nq; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;
+    const int cw = (N & 3) == 0 ? 4 : 1;
+    if (CNT && kq <= 31) {
+      // equal weight: a cell's leg memberships over the ages are two bit masks; the sums of
+      // inverse totals run over the set bits only (ascending age, the same order and values
+      // as the dense loop below)
+      const int jmax = kq < t ? kq : t;   // ages with a formation month s = t - j >= 0
+      const uint32_t topw = (uint32_t)dtop * 0x01010101u;
+      auto beq = [](uint32_t z) { return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u; };
+      for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS) {
+        uint32_t mt4[4] = {0, 0, 0, 0}, mb4[4] = {0, 0, 0, 0};
+        if (cw == 4) {
+          // the 4 cells' labels of 8 ages per trip as label words, all loads in flight
+          for (int j0 = 0; j0 <= jmax; j0 += 8) {
+            uint32_t wv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              wv[u] = j0 + u <= jmax ? *(const uint32_t*)(L + rt - (int64_t)(j0 + u) * rowstep + a4)
+                                     : 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const uint32_t et = beq(wv[u] ^ topw) >> 7, eb = beq(wv[u]) >> 7;   // bits 0,8,16,24
+              const int j = j0 + u;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                mt4[e] |= ((et >> (8 * e)) & 1u) << (j & 31);
+                mb4[e] |= ((eb >> (8 * e)) & 1u) << (j & 31);
+              }
+            }
+          }
+        } else {
+          for (int j = 0; j <= jmax; ++j) {
+            const int lab = (int)L[rt - (int64_t)j * rowstep + a4];
+            mt4[0] |= (lab == dtop ? 1u : 0u) << j;
+            mb4[0] |= (lab == 0 ? 1u : 0u) << j;
+          }
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (e >= cw || a4 + e >= a1) break;
+        const uint32_t mt = mt4[e], mb = mb4[e];
+        // (an age whose cohort is empty on a leg has inv 0 there: its bit adds 0.0)
+        const uint32_t e1 = (mt & 1u) | ((mb & 1u) << 16);
+        s1 += e1;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          if (q >= nq) break;
+          const int K = ks.K[q];
+          const uint32_t e0 = ((mt >> K) & 1u) | (((mb >> K) & 1u) << 16);
+          s0[q] += e0;
+          sb[q] += e1 & e0;
+#pragma unroll
+          for (int li = 0; li < 2; ++li) {
+            if (full[q][li]) continue;
+            const uint32_t mm = li == 0 ? mt : mb;
+            double x1 = 0.0, x0 = 0.0;
+            for (uint32_t r = mm & ((1u << K) - 1u); r; r &= r - 1u) x1 += inv[li][__ffs(r) - 1];
+            for (uint32_t r = mm & (((2u << K) - 1u) & ~1u); r; r &= r - 1u) x0 += inv[li][__ffs(r) - 1];
+            charge(q, fabs(x1 * sk[q][li][0] - x0 * sk[q][li][1]), 0.0, 0.02);
+          }
+        }
+      }
+      }
+    } else
+    for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS)
+    for (int64_t a = a4; a < a4 + cw && a < a1; ++a) {
+      double adv = 0.0, unit_sig = 0.02;
+      if (IMP) {
         adv = ADV[rt + a];
         if (SIG) { const double sg = SIG[rt + a]; unit_sig = (sg == sg) ? sg : 0.02; }
       }
-      for (int q = 0; q < nq; ++q) {
-        const int K = ks.K[q];
+      double x1[TO_MAXQ][2], x0[TO_MAXQ][2], mK[TO_MAXQ][2], m0[2] = {0.0, 0.0};
+      int lab0 = -1, labK[TO_MAXQ];
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q) {
+        labK[q] = -1;
+#pragma unroll
+        for (int li = 0; li < 2; ++li) { x1[q][li] = 0.0; x0[q][li] = 0.0; mK[q][li] = 0.0; }
+      }
+#pragma unroll 4
+      for (int j = 0; j <= kq; ++j) {
+        const double i0 = inv[0][j], i1 = inv[1][j];
+        if (i0 == 0.0 && i1 == 0.0) continue;
+        const int64_t o = rt - (int64_t)j * rowstep + a;
+        const int lab = (int)L[o];
+        const double w = VW ? valid_w(W[o]) : 1.0;
+        const double m[2] = {lab == dtop ? w * i0 : 0.0, lab == 0 ? w * i1 : 0.0};
+        if (j == 0) { m0[0] = m[0]; m0[1] = m[1]; lab0 = lab; }
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          if (q >= nq) break;
+          const int K = ks.K[q];
+          if (j == K) labK[q] = lab;
+#pragma unroll
+          for (int li = 0; li < 2; ++li) {
+            if (j < K) x1[q][li] += m[li];
+            if (j >= 1 && j <= K) x0[q][li] += m[li];
+            if (j == K) mK[q][li] = m[li];
+          }
+        }
+      }
+      if (CNT) {
+        const uint32_t e1 = (lab0 == dtop ? 1u : 0u) | (lab0 == 0 ? 0x10000u : 0u);
+        s1 += e1;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          if (q >= nq) break;
+          const uint32_t e0 = (labK[q] == dtop ? 1u : 0u) | (labK[q] == 0 ? 0x10000u : 0u);
+          s0[q] += e0;
+          sb[q] += e1 & e0;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q) {
+        if (q >= nq) break;
 #pragma unroll
         for (int li = 0; li < 2; ++li) {
-          const int d = li == 0 ? n_bins - 1 : 0;
-          double dw;
           if (full[q][li]) {
-            const int64_t o1 = rt + a, o0 = ((int64_t)(t - K) * B + b) * N + a;
-            const double w1 = member_w(L[o1], d, W, o1) * inv[li][0];
-            const double w0 = member_w(L[o0], d, W, o0) * inv[li][K];
-            dw = fabs(w1 - w0) * sk[q][li][0];
+            if (!CNT) charge(q, fabs(m0[li] - mK[q][li]) * sk[q][li][0], adv, unit_sig);
           } else {
-            double x1 = 0.0, x0 = 0.0;
-            for (int j = 0; j <= K; ++j) {
-              const double iv = inv[li][j];
-              if (iv == 0.0) continue;
-              const int64_t o = ((int64_t)(t - j) * B + b) * N + a;
-              const double w = member_w(L[o], d, W, o) * iv;
-              if (j < K) x1 += w;
-              if (j >= 1) x0 += w;
-            }
-            dw = fabs(x1 * sk[q][li][0] - x0 * sk[q][li][1]);
+            charge(q, fabs(x1[q][li] * sk[q][li][0] - x0[q][li] * sk[q][li][1]), adv,
+                   unit_sig);
           }
-          charge(q, dw, adv, unit_sig);
         }
       }
     }
   }
   __shared__ double red[PF_WAVES][2 * TO_MAXQ];
+  __shared__ uint32_t cred[PF_WAVES][1 + 2 * TO_MAXQ];
+  if (CNT) {
+    const uint32_t x = (uint32_t)wave_sumi((int)s1);
+    if (lane == 0) cred[wid][0] = x;
+  }
 #pragma unroll
   for (int q = 0; q < TO_MAXQ; ++q) {
     if (q >= nq) break;
-    const double x1 = wave_sum(turn[q]), y1 = wave_sum(cost[q]);
+    const double x1 = wave_sum(turn[q]);
+    const double y1 = IMP ? wave_sum(cost[q]) : 0.0;
     if (lane == 0) { red[wid][2 * q] = x1; red[wid][2 * q + 1] = y1; }
+    if (CNT) {
+      const uint32_t x = (uint32_t)wave_sumi((int)s0[q]), y = (uint32_t)wave_sumi((int)sb[q]);
+      if (lane == 0) { cred[wid][1 + 2 * q] = x; cred[wid][2 + 2 * q] = y; }
+    }
   }
   __syncthreads();
   if (tid < nq) {
-    const int q = tid;
+    const int q = tid, K = ks.K[q];
     double x = 0.0, y = 0.0;
     for (int w2 = 0; w2 < PF_WAVES; ++w2) { x += red[w2][2 * q]; y += red[w2][2 * q + 1]; }
+    if (CNT) {
+      uint32_t S1 = 0, S0 = 0, SB = 0;
+      for (int w2 = 0; w2 < PF_WAVES; ++w2) {
+        S1 += cred[w2][0];
+        S0 += cred[w2][1 + 2 * q];
+        SB += cred[w2][2 + 2 * q];
+      }
+#pragma unroll
+      for (int li = 0; li < 2; ++li) {
+        if (!full[q][li]) continue;
+        const uint32_t n1 = (S1 >> (16 * li)) & 0xFFFFu, n0 = (S0 >> (16 * li)) & 0xFFFFu,
+                       nb = (SB >> (16 * li)) & 0xFFFFu;
+        const double i1 = inv[li][0], i0 = inv[li][K];
+        x += ((double)(n1 - nb) * i1 + (double)(n0 - nb) * i0 + (double)nb * fabs(i1 - i0)) *
+             sk[q][li][0];
+      }
+    }
     TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.5 * x;
-    COSTp[((int64_t)q * rows + tb) * Ct + c] = y;
+    COSTp[((int64_t)q * rows + tb) * Ct + c] = IMP ? y : x * half_spread;
   }
 }
 
@@ -514,6 +942,8 @@ __global__ __launch_bounds__(256) void k_bootstrap_panel(const double* __restric
 // ------------------------------------------------------------------------------- C ABI
 // 1: cohort sums through per-wave LDS atomics (k_cohort_lds) where they fit; 0: registers
 static int g_tune_cohort_lds = 1;
+// 1: label-sorted segment gathers (k_label_sort + k_cohort_seg) where N <= SEG_MAXN
+static int g_tune_cohort_seg = 1;
 
 struct PfPlan {
   int C, kpar, Ct;
@@ -538,18 +968,44 @@ static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
   p.CH = (N + C - 1) / C;
   int64_t Ct = (want + rows - 1) / rows;
   Ct = Ct < 1 ? 1 : (Ct > cmax ? cmax : Ct);
-  p.Ct = (int)Ct;
-  p.CHt = (N + Ct - 1) / Ct;
+  const int64_t cmin = (N + 65471) / 65472;       // < 65536 cells per chunk (packed counts)
+  Ct = Ct < cmin ? cmin : Ct;
+  p.CHt = ((N + Ct - 1) / Ct + 63) / 64 * 64;   // chunk bounds on 64-cell (4-byte) boundaries
+  p.Ct = (int)((N + p.CHt - 1) / p.CHt);
   return p;
 }
 
 template <int NB>
 static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
                           const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
-                          double* SWp, double* FWp) {
-  const dim3 g((unsigned)pl.C, (unsigned)(T_m * B), pl.kpar ? (unsigned)K : 1u);
+                          double* SWp, double* FWp, char* segws, int64_t perm_b, int64_t off_b,
+                          int64_t wsrt_b) {
+  const dim3 g((unsigned)(pl.C * T_m * B), 1u, pl.kpar ? (unsigned)K : 1u);
+  if (g_tune_cohort_seg && segws && !pl.kpar && K * (NB + 1) <= SEG_MAXKD) {
+    uint16_t* PERM = (uint16_t*)(segws + perm_b);
+    int32_t* OFF = (int32_t*)(segws + off_b);
+    double* WSRT = (double*)(segws + wsrt_b);
+    const int xcd = pl.C == 1 && B >= 8;
+    const dim3 g1((unsigned)(T_m * B)),
+        g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(pl.C * T_m * B));
+    const size_t lds = (size_t)N * sizeof(double);
+    if (W) {
+      hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
+                         PERM, OFF, WSRT, FWp);
+      hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR,
+                         (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
+                         K, pl.C, xcd, SWRp, SWp);
+    } else {
+      hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N, pl.C,
+                         PERM, OFF, WSRT, FWp);
+      hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR,
+                         (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
+                         K, pl.C, xcd, SWRp, SWp);
+    }
+    return;
+  }
   if (g_tune_cohort_lds && !pl.kpar && K * NB <= AC_MAXKD) {
-    const dim3 g2((unsigned)pl.C, (unsigned)(T_m * B));
+    const dim3 g2((unsigned)(pl.C * T_m * B));
     if (W)
       hipLaunchKernelGGL((k_cohort_lds<NB, true>), g2, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B,
                          N, K, pl.C, pl.CH, SWRp, SWp, FWp);
@@ -571,6 +1027,8 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
 struct PfLayout {
   PfPlan p;
   int64_t rows, swr, sw, fw, turn, cost, bytes;
+  bool seg;                          // label-sort buffers present (N <= SEG_MAXN)
+  int64_t perm_b, off_b, wsrt_b;     // byte offsets: uint16 [rows][N], int32 [rows][nb+1], f64 [rows][N]
 };
 static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax) {
   PfLayout l;
@@ -583,6 +1041,15 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   l.turn = l.fw + l.rows * l.p.C * 2;                      // [TO_MAXQ][rows][Ct]
   l.cost = l.turn + (int64_t)TO_MAXQ * l.rows * l.p.Ct;
   l.bytes = (l.cost + (int64_t)TO_MAXQ * l.rows * l.p.Ct) * 8 + 256;
+  l.seg = N <= SEG_MAXN;
+  l.perm_b = l.off_b = l.wsrt_b = 0;
+  if (l.seg) {
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    l.perm_b = al(l.bytes);
+    l.off_b = al(l.perm_b + l.rows * N * 2);
+    l.wsrt_b = al(l.off_b + l.rows * (n_bins + 1) * 4);
+    l.bytes = al(l.wsrt_b + l.rows * N * 8);
+  }
   return l;
 }
 
@@ -591,6 +1058,10 @@ extern "C" {
 int csm_tune_portfolio(const char* key, int value) {
   if (key && !strcmp(key, "cohort_lds") && (value == 0 || value == 1)) {
     g_tune_cohort_lds = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "cohort_seg") && (value == 0 || value == 1)) {
+    g_tune_cohort_seg = value;
     return CSM_OK;
   }
   return CSM_E_INVAL;
@@ -614,7 +1085,7 @@ int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const doubl
   double* ws = (double*)workspace;
   hipStream_t st = ctx->stream;
   switch (n_bins) {
-#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw); break;
+#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b); break;
     PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20) PF_CASE(30)
 #undef PF_CASE
     default:
@@ -652,10 +1123,13 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
     ks.n = nK - q0 < TO_MAXQ ? nK - q0 : TO_MAXQ;
     for (int q = 0; q < TO_MAXQ; ++q) ks.K[q] = q < ks.n ? Ks[q0 + q] : 1;
     if (costs) {
-      hipLaunchKernelGGL(k_turnover, dim3((unsigned)lay.p.Ct, (unsigned)lay.rows),
-                         dim3(PF_THREADS), 0, st, L, W, (const double*)(ws + lay.fw), T_m, B, N,
-                         ks, Kmax, n_bins, lay.p.C, lay.p.CHt, half_spread, k_impact, aum, ADV,
-                         SIG, ws + lay.turn, ws + lay.cost);
+      const bool imp = ADV && aum > 0.0;
+      auto kern = W ? (imp ? k_turnover<true, true> : k_turnover<true, false>)
+                    : (imp ? k_turnover<false, true> : k_turnover<false, false>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(lay.p.Ct * lay.rows)), dim3(PF_THREADS), 0, st, L,
+                         W, (const double*)(ws + lay.fw), T_m, B, N, ks, Kmax, n_bins, lay.p.C,
+                         lay.p.CHt, lay.p.Ct, half_spread, k_impact, aum, ADV, SIG, ws + lay.turn,
+                         ws + lay.cost);
       LAUNCH_CHECK(ctx, "k_turnover");
     }
     double* TURNq = TURN ? TURN + q0 * rb : nullptr;

@@ -190,10 +190,13 @@ def test_portfolio_wide_panel_single_chunk(engine):
     _close(out.NET, ref["NET"], "NET")
 
 
-def test_portfolio_multi_shares_cohort_pass(engine):
-    """One cohort-sum pass with Kmax serves every K <= Kmax: identical to per-K calls."""
+@pytest.mark.parametrize("vw", [True, False])
+def test_portfolio_multi_shares_cohort_pass(engine, vw):
+    """One cohort-sum pass with Kmax serves every K <= Kmax, and one turnover pass every K of
+    the set: identical to per-K calls (value weights: f64 path; equal weights: member counts
+    in full legs, f64 sums in the first months)."""
     L, NR, _, PM = _labels(engine, "c1")
-    W = _up(np.abs(PM.cpu().numpy()) * 1e6)
+    W = _up(np.abs(PM.cpu().numpy()) * 1e6) if vw else None
     multi = engine.portfolio_multi(L, NR, 10, Ks=(3, 6, 9, 12), W=W)
     for K, got in multi.items():
         one = engine.portfolio(L, NR, 10, K=K, W=W)
@@ -201,26 +204,73 @@ def test_portfolio_multi_shares_cohort_pass(engine):
             assert bits_equal(getattr(got, f).cpu().numpy(), getattr(one, f).cpu().numpy()), (K, f)
 
 
+_COHORT_MODES = {"seg": (1, 1), "lds": (0, 1), "reg": (0, 0)}   # (cohort_seg, cohort_lds)
+
+
+def _with_cohort_mode(engine, mode, fn):
+    lib = engine.lib
+    seg, lds = _COHORT_MODES[mode]
+    try:
+        assert lib.csm_tune(b"cohort_seg", seg) == 0 and lib.csm_tune(b"cohort_lds", lds) == 0
+        return fn()
+    finally:
+        lib.csm_tune(b"cohort_seg", 1)
+        lib.csm_tune(b"cohort_lds", 1)
+
+
 @pytest.mark.parametrize("vw", [False, True])
-def test_cohort_lds_variant_deterministic_and_equal(engine, vw):
-    """The LDS-atomic cohort kernel: identical bits on repeated runs, and within 1e-10 of the
-    register-accumulator kernel (different summation order)."""
+@pytest.mark.parametrize("B", [1, 6])
+def test_cohort_variants_deterministic_and_equal(engine, vw, B):
+    """The three cohort-sum kernels (label-sorted segment gathers, per-wave LDS atomics,
+    register one-hot accumulators): each gives identical bits on repeated runs, and they agree
+    within 1e-10 (different summation orders).  B = 6 panels takes the one-chunk plan."""
     L, NR, _, PM = _labels(engine, "c1")
     W = _up(np.abs(PM.cpu().numpy()) * 1e6) if vw else None
-    lib = engine.lib
-    try:
-        assert lib.csm_tune(b"cohort_lds", 1) == 0
-        a = engine.portfolio_multi(L, NR, 10, Ks=(3, 12), W=W)
-        b = engine.portfolio_multi(L, NR, 10, Ks=(3, 12), W=W)
-        assert lib.csm_tune(b"cohort_lds", 0) == 0
-        c = engine.portfolio_multi(L, NR, 10, Ks=(3, 12), W=W)
-    finally:
-        lib.csm_tune(b"cohort_lds", 1)
+    if B > 1:
+        T_m, N = L.shape
+        rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 7 * i, axis=1) for i in range(B)],
+                                     axis=1).reshape(T_m, B * N))
+        L, NR = rep(L), rep(NR)
+        W = rep(W) if vw else None
+    run = lambda: engine.portfolio_multi(L, NR, 10, Ks=(3, 12), W=W, B=B)
+    res = {m: (_with_cohort_mode(engine, m, run), _with_cohort_mode(engine, m, run))
+           for m in _COHORT_MODES}
     for K in (3, 12):
         for f in ("PR", "LS", "TURN", "NET"):
-            x, y, z = (getattr(o[K], f).cpu().numpy() for o in (a, b, c))
-            assert bits_equal(x, y), (K, f)
-            assert np.array_equal(np.isnan(x), np.isnan(z)) and max_rel(x, z) <= 1e-10, (K, f)
+            z = getattr(res["reg"][0][K], f).cpu().numpy()
+            for m, (a, b) in res.items():
+                x, y = getattr(a[K], f).cpu().numpy(), getattr(b[K], f).cpu().numpy()
+                assert bits_equal(x, y), (m, K, f)
+                assert np.array_equal(np.isnan(x), np.isnan(z)) and max_rel(x, z) <= 1e-10, (m, K, f)
+
+
+@pytest.mark.parametrize("n_bins,ncols", [(3, 500), (20, 500), (30, 500), (10, 497), (5, 498)])
+@pytest.mark.parametrize("vw", [False, True])
+def test_cohort_seg_vs_oracle_nbins(engine, n_bins, ncols, vw):
+    """Segment-gather cohort sums (EW, and VW with invalid weights) with NaN returns against
+    the portfolio oracle, for several bin counts (ballot loops unrolled per n_bins) and row
+    widths that are not a multiple of 4 (scalar id loads, byte label staging)."""
+    z = load_golden("c1")
+    PM, _ = engine.month_end(_up(np.ascontiguousarray(z["P"][:, :ncols])),
+                             _up(z["month_start"].astype(np.int64)))
+    _, M, NR = engine.momentum(PM, 6, 1)
+    if n_bins <= 20:
+        L, _, _, _ = engine.deciles(M, None, n_bins)
+    else:   # beyond csm_deciles' range: random labels with gaps
+        Lh = np.random.default_rng(n_bins).integers(-1, n_bins, M.shape).astype(np.int8)
+        L = _up(Lh)
+    Wh = np.abs(PM.cpu().numpy()) * 1e6
+    Wh[::7, ::5] = -1.0   # invalid weights: not members
+    Wh[::11, ::3] = np.nan
+    if not vw:
+        Wh = None
+    ref = PO.portfolio(L.cpu().numpy(), NR.cpu().numpy(), n_bins, K=5, W=Wh)
+    out = _with_cohort_mode(engine, "seg", lambda: engine.portfolio(
+        L, NR, n_bins, K=5, W=None if Wh is None else _up(Wh)))
+    _close(out.PR, ref["PR"], "PR")
+    _close(out.LS, ref["LS"], "LS")
+    _close(out.TURN, ref["TURN"], "TURN")
+    _close(out.COST, ref["COST"], "COST")
 
 
 def _summary_ref(LS, TURN, COST, NET, freq=12.0):
@@ -271,3 +321,21 @@ def test_summary_kernel(engine, costs):
     # one [T_m][B] series is nS = 1
     one = engine.summary(*[None if a is None else _up(a[1]) for a in args]).cpu().numpy()
     assert bits_equal(one[0], got[1])
+
+
+@pytest.mark.parametrize("mode", ["seg", "lds"])
+def test_portfolio_many_rows(engine, mode):
+    """More (t, b) rows than a grid's y dimension holds (360 x 203 = 73080 > 65535): the
+    flattened grids, and the XCD-ordered segment kernel with a panel count that is not a
+    multiple of 8, against the oracle."""
+    rng = np.random.default_rng(11)
+    T_m, B, N = 360, 203, 48
+    Lh = rng.integers(-1, 10, (T_m, B, N)).astype(np.int8)
+    NRh = rng.normal(0.0, 0.05, (T_m, B, N))
+    NRh[rng.random(NRh.shape) < 0.05] = np.nan
+    ref = PO.portfolio(Lh, NRh, 10, K=4)
+    out = _with_cohort_mode(engine, mode, lambda: engine.portfolio(
+        _up(Lh.reshape(T_m, B * N)), _up(NRh.reshape(T_m, B * N)), 10, K=4, B=B))
+    _close(out.PR, ref["PR"], "PR")
+    _close(out.TURN, ref["TURN"], "TURN")
+    _close(out.NET, ref["NET"], "NET")
