@@ -26,6 +26,8 @@
 
 #include <string.h>
 
+#include <algorithm>
+
 #define PF_THREADS 256
 #define PF_WAVES (PF_THREADS / 64)
 #define PF_CHUNK_MIN 256     // assets per chunk, at least one per thread
@@ -348,7 +350,7 @@ template <int NB, bool VW>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const double* __restrict__ NR, const uint16_t* __restrict__ PERM,
     const int32_t* __restrict__ OFF, const double* __restrict__ WSRT, int T_m, int B, int64_t N,
-    int K, int C, int xcd, double* __restrict__ SWRp, double* __restrict__ SWp) {
+    int K, int C, int Cs, int xcd, double* __restrict__ SWRp, double* __restrict__ SWp) {
   extern __shared__ double rl[];   // the return row of month t (N values)
   __shared__ int32_t offs[SEG_MAXKD];
   int c = 0;
@@ -372,6 +374,15 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   const int tid = threadIdx.x;
   const int grp = tid / SEG_G, sl = tid % SEG_G;
   const int kmax = t + 1 < K ? t + 1 : K;
+  if (c >= Cs) {   // chunks beyond the Cs working ones only hold zeros
+    for (int g = tid; g < K * NB; g += PF_THREADS) {
+      const int k = g / NB, d = g - k * NB;
+      const int64_t ob = ((tb * K + k) * C + c) * NB + d;
+      SWRp[ob] = 0.0;
+      SWp[ob] = 0.0;
+    }
+    return;
+  }
   const double* NRr = NR + tb * N;
   for (int i = tid; i < kmax * (NB + 1); i += PF_THREADS) {
     const int k = i / (NB + 1), e = i - k * (NB + 1);
@@ -381,16 +392,17 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   for (int a = tid; a < (int)N; a += PF_THREADS) rl[a] = NRr[a];
   __syncthreads();
   const bool vec = (N & 3) == 0;   // id rows 8-byte aligned
-  // chunk c owns the segments g = c (mod C) whole and writes zeros for the others (exact
-  // under the chunk-order sum of k_overlap)
-  for (int g = tid; g < K * NB && C > 1; g += PF_THREADS) {
-    if (g % C == c) continue;
+  // working chunk c < Cs owns the segments g = c (mod Cs) whole and writes zeros for the
+  // others (exact under the chunk-order sum of k_overlap); each working chunk stages the
+  // whole return row, so Cs stays small
+  for (int g = tid; g < K * NB && Cs > 1; g += PF_THREADS) {
+    if (g % Cs == c) continue;
     const int k = g / NB, d = g - k * NB;
     const int64_t ob = ((tb * K + k) * C + c) * NB + d;
     SWRp[ob] = 0.0;
     SWp[ob] = 0.0;
   }
-  for (int g = c + grp * C; g < K * NB; g += (PF_THREADS / SEG_G) * C) {
+  for (int g = c + grp * Cs; g < K * NB; g += (PF_THREADS / SEG_G) * Cs) {
     const int k = g / NB, d = g - k * NB;
     const int64_t ob = ((tb * K + k) * C + c) * NB + d;
     if (k >= kmax) {
@@ -491,7 +503,9 @@ __device__ __forceinline__ void load_labels(const int8_t* __restrict__ p, int* l
 
 __device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INFINITY) ? x : 0.0; }
 
-template <bool VW, bool IMP>
+// GEN = false: the steady rows only (every (K, leg) window full), GEN = true: the others (the
+// first months, empty cohorts); two launches so the steady kernel keeps few registers.
+template <bool VW, bool IMP, bool GEN>
 __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
     int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
@@ -512,6 +526,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
       double tot = 0.0;
       if (s >= 0)
         for (int cc = 0; cc < Cf; ++cc) tot += FWp[(((int64_t)s * B + b) * Cf + cc) * 2 + li];
+      // (called with the folded totals, Cf = 1)
       inv[li][j] = tot > 0.0 ? 1.0 / tot : 0.0;
     }
   }
@@ -556,7 +571,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
   };
   bool all_full = true;
   for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
-  if (CNT && all_full && (N & 3) == 0) {
+  if (all_full == GEN) return;   // the other launch's row
+  if (!GEN && CNT && (N & 3) == 0) {
     // steady state, 4 cells per lane per word (SWAR byte compares on the label words)
     const uint32_t topw = (uint32_t)dtop * 0x01010101u;
     auto beq = [](uint32_t z) {   // 0x80 in each byte of z that is zero
@@ -588,64 +604,61 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
         }
       }
     }
-  } else if (all_full && (N & 3) == 0) {
-    // steady state, 4 cells per lane (4-byte label loads; chunk bounds are multiples of 64):
-    // w_t - w_{t-1} needs the month-t and month t-K_q labels only
-    constexpr int CW = 4;
-    for (int64_t a = a0 + CW * tid; a < a1; a += CW * PF_THREADS) {
-      int l1[CW], l0[TO_MAXQ][CW];
-      double x1[CW], x0[TO_MAXQ][CW], adv[CW], sg[CW];
-      load_labels<CW>(L + rt + a, l1);
+  } else if (!GEN) {
+    // steady state (value weights or impact costs): w_t - w_{t-1} needs the month-t and month
+    // t-K_q labels only; TU cells per lane per trip (stride PF_THREADS), all loads in flight
+    constexpr int TU = 2;
+    for (int64_t i0 = a0 + tid; i0 < a1; i0 += TU * PF_THREADS) {
+      int l1[TU], l0[TU][TO_MAXQ];
+      double x1[TU], x0[TU][TO_MAXQ], adv[TU], sg[TU];
 #pragma unroll
-      for (int q = 0; q < TO_MAXQ; ++q) {
-        if (q < nq) {
-          load_labels<CW>(L + rt - (int64_t)ks.K[q] * rowstep + a, l0[q]);
-        } else {
+      for (int u = 0; u < TU; ++u) {
+        const int64_t a = i0 + (int64_t)u * PF_THREADS;
+        const bool in = a < a1;
+        l1[u] = in ? (int)L[rt + a] : -1;
+        x1[u] = (VW && in) ? W[rt + a] : 1.0;
 #pragma unroll
-          for (int e = 0; e < CW; ++e) l0[q][e] = -1;
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          const bool use = in && q < nq;
+          const int64_t o = rt - (use ? (int64_t)ks.K[q] * rowstep : 0) + a;
+          l0[u][q] = use ? (int)L[o] : -1;
+          x0[u][q] = (VW && use) ? W[o] : 1.0;
         }
+        adv[u] = (IMP && in) ? ADV[rt + a] : 0.0;
+        sg[u] = (IMP && SIG && in) ? SIG[rt + a] : 0.02;
       }
 #pragma unroll
-      for (int e = 0; e < CW; ++e) {
-        x1[e] = VW ? W[rt + a + e] : 1.0;
-#pragma unroll
-        for (int q = 0; q < TO_MAXQ; ++q)
-          x0[q][e] = (VW && q < nq) ? W[rt - (int64_t)ks.K[q] * rowstep + a + e] : 1.0;
-        adv[e] = IMP ? ADV[rt + a + e] : 0.0;
-        sg[e] = (IMP && SIG) ? SIG[rt + a + e] : 0.02;
-      }
-#pragma unroll
-      for (int e = 0; e < CW; ++e) {
-        const double vw1 = VW ? valid_w(x1[e]) : 1.0;
-        const double unit_sig = sg[e] == sg[e] ? sg[e] : 0.02;
+      for (int u = 0; u < TU; ++u) {
+        const double vw1 = VW ? valid_w(x1[u]) : 1.0;
+        const double unit_sig = sg[u] == sg[u] ? sg[u] : 0.02;
 #pragma unroll
         for (int q = 0; q < TO_MAXQ; ++q) {
           if (q >= nq) break;
-          const double vw0 = VW ? valid_w(x0[q][e]) : 1.0;
+          const double vw0 = VW ? valid_w(x0[u][q]) : 1.0;
           const int K = ks.K[q];
 #pragma unroll
           for (int li = 0; li < 2; ++li) {
             const int d = li == 0 ? dtop : 0;
-            const double w1 = (l1[e] == d ? vw1 : 0.0) * inv[li][0];
-            const double w0 = (l0[q][e] == d ? vw0 : 0.0) * inv[li][K];
-            charge(q, fabs(w1 - w0) * sk[q][li][0], adv[e], unit_sig);
+            const double w1 = (l1[u] == d ? vw1 : 0.0) * inv[li][0];
+            const double w0 = (l0[u][q] == d ? vw0 : 0.0) * inv[li][K];
+            charge(q, fabs(w1 - w0) * sk[q][li][0], adv[u], unit_sig);
           }
         }
       }
     }
-  } else {
+  } else if (GEN) {
     // general rows: one pass over the ages j <= max K_q per cell, the age loads unrolled so
     // they are in flight together; w_t and w_{t-1} sums for every (q, leg) at once.  Cells go
     // to lanes as in the steady paths (4 consecutive per lane when N % 4 == 0), so a row's
     // sums have the same order whichever path it takes.
     int kq = 0;
     for (int q = 0; q < nq; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;
-    const int cw = (N & 3) == 0 ? 4 : 1;
+    const int cw = (CNT && (N & 3) == 0) ? 4 : 1;   // the steady paths' cells per lane
+    const int jmax = kq < t ? kq : t;   // ages with a formation month s = t - j >= 0
     if (CNT && kq <= 31) {
       // equal weight: a cell's leg memberships over the ages are two bit masks; the sums of
       // inverse totals run over the set bits only (ascending age, the same order and values
       // as the dense loop below)
-      const int jmax = kq < t ? kq : t;   // ages with a formation month s = t - j >= 0
       const uint32_t topw = (uint32_t)dtop * 0x01010101u;
       auto beq = [](uint32_t z) { return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u; };
       for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS) {
@@ -718,13 +731,25 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
 #pragma unroll
         for (int li = 0; li < 2; ++li) { x1[q][li] = 0.0; x0[q][li] = 0.0; mK[q][li] = 0.0; }
       }
-#pragma unroll 4
-      for (int j = 0; j <= kq; ++j) {
+      // ages in trips of 8: the trip's label and weight loads are all in flight before use
+      for (int j0 = 0; j0 <= jmax; j0 += 8) {
+      int labv[8];
+      double wv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool ok = j0 + u <= jmax;
+        const int64_t o = rt - (int64_t)(ok ? j0 + u : 0) * rowstep + a;
+        labv[u] = ok ? (int)L[o] : -1;
+        wv[u] = (VW && ok) ? W[o] : 1.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u;
+        if (j > jmax) break;
         const double i0 = inv[0][j], i1 = inv[1][j];
         if (i0 == 0.0 && i1 == 0.0) continue;
-        const int64_t o = rt - (int64_t)j * rowstep + a;
-        const int lab = (int)L[o];
-        const double w = VW ? valid_w(W[o]) : 1.0;
+        const int lab = labv[u];
+        const double w = VW ? valid_w(wv[u]) : 1.0;
         const double m[2] = {lab == dtop ? w * i0 : 0.0, lab == 0 ? w * i1 : 0.0};
         if (j == 0) { m0[0] = m[0]; m0[1] = m[1]; lab0 = lab; }
 #pragma unroll
@@ -739,6 +764,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
             if (j == K) mK[q][li] = m[li];
           }
         }
+      }
       }
       if (CNT) {
         const uint32_t e1 = (lab0 == dtop ? 1u : 0u) | (lab0 == 0 ? 0x10000u : 0u);
@@ -827,10 +853,21 @@ __global__ __launch_bounds__(64) void k_overlap(
     int n = 0;
     for (int k = 0; k < K; ++k) {
       double x = 0.0, y = 0.0;
-      for (int c = 0; c < C; ++c) {
-        const int64_t o = ((tb * Kmax + k) * C + c) * nb + d;
-        x += SWRp[o];
-        y += SWp[o];
+      // chunk partials in trips of 8, loads first, then summed in chunk order
+      for (int c0 = 0; c0 < C; c0 += 8) {
+        double xr[8], yr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int64_t o = ((tb * Kmax + k) * C + (c0 + u < C ? c0 + u : 0)) * nb + d;
+          xr[u] = c0 + u < C ? SWRp[o] : 0.0;
+          yr[u] = c0 + u < C ? SWp[o] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (c0 + u >= C) break;
+          x += xr[u];
+          y += yr[u];
+        }
       }
       if (y > 0.0) { acc += x / y; ++n; }
     }
@@ -975,6 +1012,19 @@ static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
   return p;
 }
 
+// formation leg totals of each row: the chunk partials summed in chunk order, once per row
+// (k_turnover reads them for K + 1 formation months per block)
+__global__ __launch_bounds__(256) void k_fw_fold(const double* __restrict__ FWp, int64_t rows,
+                                                 int C, double* __restrict__ FWt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * rows) return;
+  const int64_t row = i >> 1;
+  const int leg = (int)(i & 1);
+  double tot = 0.0;
+  for (int c = 0; c < C; ++c) tot += FWp[(row * C + c) * 2 + leg];
+  FWt[i] = tot;
+}
+
 template <int NB>
 static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
                           const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
@@ -986,6 +1036,8 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     int32_t* OFF = (int32_t*)(segws + off_b);
     double* WSRT = (double*)(segws + wsrt_b);
     const int xcd = pl.C == 1 && B >= 8;
+    const int64_t rows = (int64_t)T_m * B;
+    const int Cs = (int)std::min<int64_t>(pl.C, std::max<int64_t>(1, (1024 + rows - 1) / rows));
     const dim3 g1((unsigned)(T_m * B)),
         g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(pl.C * T_m * B));
     const size_t lds = (size_t)N * sizeof(double);
@@ -994,13 +1046,13 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                          PERM, OFF, WSRT, FWp);
       hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR,
                          (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, xcd, SWRp, SWp);
+                         K, pl.C, Cs, xcd, SWRp, SWp);
     } else {
       hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
       hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR,
                          (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, xcd, SWRp, SWp);
+                         K, pl.C, Cs, xcd, SWRp, SWp);
     }
     return;
   }
@@ -1026,7 +1078,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
 // [rows][Kmax][C][n_bins], FWp [rows][C][2], then the turnover partials [rows][Ct] x 2.
 struct PfLayout {
   PfPlan p;
-  int64_t rows, swr, sw, fw, turn, cost, bytes;
+  int64_t rows, swr, sw, fw, fwt, turn, cost, bytes;
   bool seg;                          // label-sort buffers present (N <= SEG_MAXN)
   int64_t perm_b, off_b, wsrt_b;     // byte offsets: uint16 [rows][N], int32 [rows][nb+1], f64 [rows][N]
 };
@@ -1038,7 +1090,8 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   l.swr = 0;
   l.sw = cs;
   l.fw = 2 * cs;
-  l.turn = l.fw + l.rows * l.p.C * 2;                      // [TO_MAXQ][rows][Ct]
+  l.fwt = l.fw + l.rows * l.p.C * 2;                       // [rows][2] folded totals
+  l.turn = l.fwt + l.rows * 2;                              // [TO_MAXQ][rows][Ct]
   l.cost = l.turn + (int64_t)TO_MAXQ * l.rows * l.p.Ct;
   l.bytes = (l.cost + (int64_t)TO_MAXQ * l.rows * l.p.Ct) * 8 + 256;
   l.seg = N <= SEG_MAXN;
@@ -1092,6 +1145,9 @@ int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const doubl
       return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: n_bins=%d unsupported (2,3,4,5,10,20,30)", n_bins);
   }
   LAUNCH_CHECK(ctx, "k_cohort");
+  hipLaunchKernelGGL(k_fw_fold, dim3((unsigned)((2 * lay.rows + 255) / 256)), dim3(256), 0, st,
+                     (const double*)(ws + lay.fw), lay.rows, lay.p.C, ws + lay.fwt);
+  LAUNCH_CHECK(ctx, "k_fw_fold");
   return CSM_OK;
 }
 
@@ -1124,12 +1180,16 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
     for (int q = 0; q < TO_MAXQ; ++q) ks.K[q] = q < ks.n ? Ks[q0 + q] : 1;
     if (costs) {
       const bool imp = ADV && aum > 0.0;
-      auto kern = W ? (imp ? k_turnover<true, true> : k_turnover<true, false>)
-                    : (imp ? k_turnover<false, true> : k_turnover<false, false>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)(lay.p.Ct * lay.rows)), dim3(PF_THREADS), 0, st, L,
-                         W, (const double*)(ws + lay.fw), T_m, B, N, ks, Kmax, n_bins, lay.p.C,
-                         lay.p.CHt, lay.p.Ct, half_spread, k_impact, aum, ADV, SIG, ws + lay.turn,
-                         ws + lay.cost);
+      for (int gen = 0; gen < 2; ++gen) {
+        auto kern = gen ? (W ? (imp ? k_turnover<true, true, true> : k_turnover<true, false, true>)
+                             : (imp ? k_turnover<false, true, true> : k_turnover<false, false, true>))
+                        : (W ? (imp ? k_turnover<true, true, false> : k_turnover<true, false, false>)
+                             : (imp ? k_turnover<false, true, false> : k_turnover<false, false, false>));
+        hipLaunchKernelGGL(kern, dim3((unsigned)(lay.p.Ct * lay.rows)), dim3(PF_THREADS), 0, st,
+                           L, W, (const double*)(ws + lay.fwt), T_m, B, N, ks, Kmax, n_bins, 1,
+                           lay.p.CHt, lay.p.Ct, half_spread, k_impact, aum, ADV, SIG,
+                           ws + lay.turn, ws + lay.cost);
+      }
       LAUNCH_CHECK(ctx, "k_turnover");
     }
     double* TURNq = TURN ? TURN + q0 * rb : nullptr;
