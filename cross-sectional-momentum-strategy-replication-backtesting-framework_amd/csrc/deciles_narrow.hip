@@ -7,7 +7,8 @@
 
 #define DEC_THREADS 256
 #define HB 1024
-#define CAP 2048
+#define CAP 1024     // candidates of the target buckets (refinement splits beyond)
+#define DEC_MINB 6   // 6 workgroups per CU (8: register spills, slower)
 namespace dec_narrow {
 #include "deciles.inc"
 }  // namespace dec_narrow
