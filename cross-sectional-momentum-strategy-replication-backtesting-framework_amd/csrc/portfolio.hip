@@ -232,12 +232,17 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
 // selects and no atomics, one LDS read per (cell, age).  A row's sort is read by the K months
 // that hold it (from L2 / MALL).  Chunks split every segment by position, and the partials are
 // combined in chunk order like the other cohort kernels'.  Used for N <= SEG_MAXN.
+// id rows are padded: every segment starts on a 4-id (8-byte) boundary and its last word is
+// filled with the sentinel id N (LDS slot N of the staged return row holds NaN, so a sentinel
+// contributes nothing): the gather loop needs no per-element bounds test.  Row stride:
+__host__ __device__ __forceinline__ int64_t seg_stride(int64_t N) { return ((N + 3) & ~3LL) + 128; }
 #define SEG_MAXN 7168   // VW sort stages 9 bytes per cell in LDS: <= 64 KB per workgroup
 template <int NB, bool VW>
 __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
     const int8_t* __restrict__ L, const double* __restrict__ W, int64_t N, int C,
     uint16_t* __restrict__ PERM, int32_t* __restrict__ OFF, double* __restrict__ WSRT,
     double* __restrict__ FWp) {
+  const int64_t PS = seg_stride(N);
   // the row is staged in LDS first (all loads in flight at once), then both passes read LDS
   extern __shared__ double wl[];                  // VW: weights [N], then labels [N]
   int8_t* ll = VW ? (int8_t*)(wl + N) : (int8_t*)wl;
@@ -294,7 +299,13 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
     }
     base[d] = run + before;
     if (tid == 0) OFF[row * (NB + 1) + d] = run;
-    run += tot;
+    const int r4 = (tot + 3) & ~3;
+    if (tid == d)   // sentinel ids in the segment's last word
+      for (int p = run + tot; p < run + r4; ++p) {
+        PERM[row * PS + p] = (uint16_t)N;
+        if (VW) WSRT[row * PS + p] = 0.0;
+      }
+    run += r4;
   }
   if (tid == 0) OFF[row * (NB + 1) + NB] = run;
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -310,10 +321,10 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
       base[d] += __popcll(m);
     }
     if (pos >= 0) {
-      PERM[row * N + pos] = (uint16_t)a;
+      PERM[row * PS + pos] = (uint16_t)a;
       if (VW) {
         const double w = wl[a];
-        WSRT[row * N + pos] = w;
+        WSRT[row * PS + pos] = w;
         ft += lab == NB - 1 ? w : 0.0;
         fb += lab == 0 ? w : 0.0;
       }
@@ -351,7 +362,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const double* __restrict__ NR, const uint16_t* __restrict__ PERM,
     const int32_t* __restrict__ OFF, const double* __restrict__ WSRT, int T_m, int B, int64_t N,
     int K, int C, int Cs, int xcd, double* __restrict__ SWRp, double* __restrict__ SWp) {
-  extern __shared__ double rl[];   // the return row of month t (N values)
+  extern __shared__ double rl[];   // the return row of month t (N values), NaN at slot N
   __shared__ int32_t offs[SEG_MAXKD];
   int c = 0;
   int64_t tb;
@@ -390,8 +401,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   }
 #pragma unroll 8
   for (int a = tid; a < (int)N; a += PF_THREADS) rl[a] = NRr[a];
+  if (tid == 0) rl[N] = qnan();
   __syncthreads();
-  const bool vec = (N & 3) == 0;   // id rows 8-byte aligned
   // working chunk c < Cs owns the segments g = c (mod Cs) whole and writes zeros for the
   // others (exact under the chunk-order sum of k_overlap); each working chunk stages the
   // whole return row, so Cs stays small
@@ -402,66 +413,58 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     SWRp[ob] = 0.0;
     SWp[ob] = 0.0;
   }
-  for (int g = c + grp * Cs; g < K * NB; g += (PF_THREADS / SEG_G) * Cs) {
+  const int64_t PS = seg_stride(N);
+  const uint64_t SENT = (uint64_t)N * 0x0001000100010001ull;   // four sentinel ids
+  const int gstep = (PF_THREADS / SEG_G) * Cs;
+  // one segment: its row's id words [w0, w1), its sorted weights; zeros when its cohort is
+  // not formed
+  struct Seg {
+    int64_t w0, w1, ob;
+    const uint64_t* P8;
+    const double* Ws;
+    bool live;
+  };
+  auto seg_at = [&](int g) {
+    Seg q;
     const int k = g / NB, d = g - k * NB;
-    const int64_t ob = ((tb * K + k) * C + c) * NB + d;
-    if (k >= kmax) {
-      if (sl == 0) { SWRp[ob] = 0.0; SWp[ob] = 0.0; }
-      continue;
+    q.ob = ((tb * K + k) * C + c) * NB + d;
+    q.live = k < kmax;
+    const int64_t srow = tb - (int64_t)(q.live ? k : 0) * B;
+    q.w0 = q.live ? offs[k * (NB + 1) + d] >> 2 : 0;
+    q.w1 = q.live ? offs[k * (NB + 1) + d + 1] >> 2 : 0;
+    q.P8 = (const uint64_t*)(PERM + srow * PS);
+    q.Ws = VW ? WSRT + srow * PS : nullptr;
+    return q;
+  };
+  constexpr int U = 8;
+  // ids of one trip (U words of 4 ids per lane) of a segment, from word w on
+  auto load_trip = [&](const Seg& q, int64_t w, uint64_t* v) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t x = w + u * SEG_G;
+      v[u] = x < q.w1 ? q.P8[x] : SENT;
     }
-    const int64_t srow = tb - (int64_t)k * B;
-    const int64_t lo = offs[k * (NB + 1) + d], hi = offs[k * (NB + 1) + d + 1];
-    const uint16_t* P = PERM + srow * N;
-    const double* Ws = VW ? WSRT + srow * N : nullptr;
-    double sr = 0.0, sw = 0.0;
-    int n = 0;
-    auto take = [&](int64_t j, int id) {
-      const double x = rl[id];
-      if (x == x) {
-        if (VW) {
-          const double w = Ws[j];
-          sr += w * x;
-          sw += w;
-        } else {
-          sr += x;
-          ++n;
-        }
-      }
-    };
-    if (vec) {
-      const uint64_t* P8 = (const uint64_t*)P;
-      constexpr int U = 8;
-      for (int64_t q0 = (lo >> 2) + sl; q0 * 4 < hi; q0 += U * SEG_G) {
-        uint64_t v[U];
+  };
+  auto use_trip = [&](const Seg& q, int64_t w, const uint64_t* v, double& sr, double& sw, int& n) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int64_t q = q0 + u * SEG_G;
-          v[u] = q * 4 < hi ? P8[q] : 0ull;
-        }
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int64_t j0 = (q0 + u * SEG_G) * 4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int64_t j = j0 + e;
-            if (j >= lo && j < hi) take(j, (int)((v[u] >> (16 * e)) & 0xffffu));
+      for (int e = 0; e < 4; ++e) {
+        const double x = rl[(v[u] >> (16 * e)) & 0xffffu];
+        if (x == x) {
+          if (VW) {
+            const double wt = q.Ws[(w + u * SEG_G) * 4 + e];
+            sr += wt * x;
+            sw += wt;
+          } else {
+            sr += x;
+            ++n;
           }
         }
       }
-    } else {
-      constexpr int U = 8;
-      for (int64_t j0 = lo + sl; j0 < hi; j0 += U * SEG_G) {
-        int idx[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int64_t j = j0 + u * SEG_G;
-          idx[u] = j < hi ? (int)P[j] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (idx[u] >= 0) take(j0 + u * SEG_G, idx[u]);
-      }
     }
+  };
+  auto finish = [&](const Seg& q, double sr, double sw, int n) {
 #pragma unroll
     for (int o = SEG_G / 2; o > 0; o >>= 1) {
       sr += __shfl_xor(sr, o, SEG_G);
@@ -469,9 +472,35 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
       else n += __shfl_xor(n, o, SEG_G);
     }
     if (sl == 0) {
-      SWRp[ob] = sr;
-      SWp[ob] = VW ? sw : (double)n;
+      SWRp[q.ob] = q.live ? sr : 0.0;
+      SWp[q.ob] = q.live ? (VW ? sw : (double)n) : 0.0;
     }
+  };
+  // two segments per group at a time: both segments' first trips of ids are in flight
+  // together (a typical segment is one trip), then any further trips one by one
+  for (int g = c + grp * Cs; g < K * NB; g += 2 * gstep) {
+    const bool two = g + gstep < K * NB;
+    const Seg q1 = seg_at(g), q2 = seg_at(two ? g + gstep : g);
+    const int64_t a1 = q1.w0 + sl, a2 = q2.w0 + sl;
+    uint64_t v1[U], v2[U];
+    load_trip(q1, a1, v1);
+    if (two) load_trip(q2, a2, v2);
+    double sr1 = 0.0, sw1 = 0.0, sr2 = 0.0, sw2 = 0.0;
+    int n1 = 0, n2 = 0;
+    use_trip(q1, a1, v1, sr1, sw1, n1);
+    for (int64_t w = a1 + U * SEG_G; w < q1.w1; w += U * SEG_G) {
+      load_trip(q1, w, v1);
+      use_trip(q1, w, v1, sr1, sw1, n1);
+    }
+    if (two) {
+      use_trip(q2, a2, v2, sr2, sw2, n2);
+      for (int64_t w = a2 + U * SEG_G; w < q2.w1; w += U * SEG_G) {
+        load_trip(q2, w, v2);
+        use_trip(q2, w, v2, sr2, sw2, n2);
+      }
+    }
+    finish(q1, sr1, sw1, n1);
+    if (two) finish(q2, sr2, sw2, n2);
   }
 }
 
@@ -1040,7 +1069,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     const int Cs = (int)std::min<int64_t>(pl.C, std::max<int64_t>(1, (1024 + rows - 1) / rows));
     const dim3 g1((unsigned)(T_m * B)),
         g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(pl.C * T_m * B));
-    const size_t lds = (size_t)N * sizeof(double);
+    const size_t lds = (size_t)(N + 1) * sizeof(double);
     if (W) {
       hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
@@ -1099,9 +1128,9 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   if (l.seg) {
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     l.perm_b = al(l.bytes);
-    l.off_b = al(l.perm_b + l.rows * N * 2);
+    l.off_b = al(l.perm_b + l.rows * seg_stride(N) * 2);
     l.wsrt_b = al(l.off_b + l.rows * (n_bins + 1) * 4);
-    l.bytes = al(l.wsrt_b + l.rows * N * 8);
+    l.bytes = al(l.wsrt_b + l.rows * seg_stride(N) * 8);
   }
   return l;
 }

@@ -1,4 +1,4 @@
-"""C5-shaped cohort sums: register-accumulator vs per-wave LDS-atomic k_cohort, interleaved.
+"""C5-shaped cohort sums (no costs): label sort + segment gathers vs per-wave LDS atomics, interleaved.
 100 bootstrap panels of a 5k x 300-month base, J=12, Ks (3,6,9,12).  Dev tool."""
 import json
 import sys
@@ -32,20 +32,22 @@ def timed(fn):
     return a.elapsed_time(b)
 
 
-res = {0: [], 1: []}
+MODES = {"seg": (1, 1), "lds": (0, 1)}   # (cohort_seg, cohort_lds)
+res = {m: [] for m in MODES}
 outs = {}
 for rnd in range(6):
-    for v in (0, 1):
-        eng.lib.csm_tune(b"cohort_lds", v)
-        t = timed(lambda: outs.__setitem__(v, eng.portfolio_multi(L, NR, 10, Ks=(3, 6, 9, 12), B=B,
-                                                                  workspace=ws)))
+    for m, (sg, ld) in MODES.items():
+        eng.lib.csm_tune(b"cohort_seg", sg)
+        eng.lib.csm_tune(b"cohort_lds", ld)
+        t = timed(lambda: outs.__setitem__(m, eng.portfolio_multi(L, NR, 10, Ks=(3, 6, 9, 12), B=B,
+                                                                  workspace=ws, with_costs=False)))
         if rnd:
-            res[v].append(t)
+            res[m].append(t)
+eng.lib.csm_tune(b"cohort_seg", 1)
 eng.lib.csm_tune(b"cohort_lds", 1)
-a, b = outs[0][12].PR.cpu().numpy(), outs[1][12].PR.cpu().numpy()
+a, b = outs["lds"][12].PR.cpu().numpy(), outs["seg"][12].PR.cpu().numpy()
 m = ~np.isnan(a)
 rel = float(np.max(np.abs(a[m] - b[m]) / np.maximum(np.abs(a[m]), 1e-300)))
 print(json.dumps({"B": B, "N": N, "T_m": T_m,
-                  "portfolio_multi_ms": {"registers": round(float(np.median(res[0])), 3),
-                                         "lds_atomics": round(float(np.median(res[1])), 3)},
+                  "cohort_plus_overlap_ms": {k: round(float(np.median(v)), 3) for k, v in res.items()},
                   "max_rel_PR": rel}), flush=True)
