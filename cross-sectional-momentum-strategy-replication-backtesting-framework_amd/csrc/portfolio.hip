@@ -308,17 +308,33 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
     run += r4;
   }
   if (tid == 0) OFF[row * (NB + 1) + NB] = run;
+  // pass 2: a lane's rank among the lanes of its tile with the same label from bit-sliced
+  // ballots (one per label bit, not one per label); the running segment positions live in
+  // this wave's LDS row, bumped by the last lane of each label group
+  __shared__ int wbase[PF_WAVES][NB];
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < NB; ++d) wbase[wid][d] = base[d];
+  }
+  constexpr int NBITS = NB <= 2 ? 1 : NB <= 4 ? 2 : NB <= 8 ? 3 : NB <= 16 ? 4 : 5;
   const uint64_t lt = (1ull << lane) - 1ull;
   double ft = 0.0, fb = 0.0;
   for (int64_t a0 = q0; a0 < q1; a0 += 64) {
     const int64_t a = a0 + lane;
     const int lab = a < q1 ? (int)ll[a] : -1;
-    int pos = -1;
+    uint64_t same = __ballot(lab >= 0);
 #pragma unroll
-    for (int d = 0; d < NB; ++d) {
-      const uint64_t m = __ballot(lab == d);
-      if (lab == d) pos = base[d] + __popcll(m & lt);
-      base[d] += __popcll(m);
+    for (int bb = 0; bb < NBITS; ++bb) {
+      const bool bit = (lab >> bb) & 1;
+      const uint64_t m = __ballot(bit);
+      same &= bit ? m : ~m;
+    }
+    int pos = -1;
+    if (lab >= 0) {
+      const int r = __popcll(same & lt);
+      const int b0 = wbase[wid][lab];
+      pos = b0 + r;
+      if (r == __popcll(same) - 1) wbase[wid][lab] = b0 + r + 1;   // last of its group
     }
     if (pos >= 0) {
       PERM[row * PS + pos] = (uint16_t)a;
