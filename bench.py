@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--days", type=int, default=None)
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-assets", type=int, default=50000)
+    ap.add_argument("--cpu-assets", type=int, default=150000)   # ~10-15 s of oracle time
     ap.add_argument("--seed", type=int, default=4)
     return ap.parse_args()
 
@@ -494,7 +494,7 @@ def sweep_main(args):
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline_sweep(args.config, 500 if args.config == "c3" else 300,
+            line["cpu_baseline"] = cpu_baseline_sweep(args.config, 1500 if args.config == "c3" else 1000,
                                                       T_d, cfg["start"])
         print(json.dumps(line), flush=True)
     if world > 1:

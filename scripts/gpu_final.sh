@@ -9,7 +9,7 @@ rc=$?; tail -2 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; tail -1 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
 bash scripts/profile.sh r01 c4 || exit $?
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-assets 20000 > gpurun_out/bench_c4.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench_c4.log 2>&1
 rc=$?; grep -o '"value": [0-9.e+]*\|"ms_per_step": [0-9.]*\|"frac": [0-9.]*' gpurun_out/bench_c4.log | tr '\n' ' '; echo; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_c2.log 2>&1
 rc=$?; grep -o '"value": [0-9.e+]*\|"ms_per_step": [0-9.]*' gpurun_out/bench_c2.log | tr '\n' ' '; echo; [ $rc -eq 0 ] || exit $rc

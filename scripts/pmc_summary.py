@@ -20,7 +20,8 @@ def short(name: str) -> str:
     n = name.strip().strip('"')
     n = re.sub(r"^void\s+", "", n)
     n = n.split("(")[0]
-    return n.split("<")[0].strip()
+    n = n.split("<")[0].strip()
+    return n.split("::")[-1]   # dec_wide::k_deciles -> k_deciles
 
 
 def read_stats(d):
