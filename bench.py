@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--assets", type=int, default=None)
     ap.add_argument("--days", type=int, default=None)
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--shard-mode", default="fused", choices=["fused", "unfused"],
+                    help="N>1 date shards: speculative fused signal + repair, or month-end + "
+                         "carried scan")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-assets", type=int, default=150000)   # ~10-15 s of oracle time
     ap.add_argument("--seed", type=int, default=4)
@@ -144,16 +147,18 @@ def main():
     days_per_rank = args.days or cfg["days"]
     total_days = days_per_rank * world if args.scaling == "weak" else days_per_rank
     days, ms_host, mend, months = shard_calendar(cfg["start"], total_days, world, rank)
-    panel = make_device_panel(N, days, ms_host, seed=args.seed * 1000 + rank, device=dev)
+    panel = make_device_panel(N, days, ms_host, seed=args.seed * 1000 + rank, device=dev,
+                              shard=(rank, world, args.seed, total_days / world))
     T_d, T_m = len(days), len(ms_host) - 1
 
     eng = csmom.Engine(local)
     J, skip, nb = 12, 1, 10
-    pipe = DateShardPipeline(eng, months, J, skip, nb) if world > 1 else None
-
     # preallocated outputs: the timed loop performs no allocation
     max_days = int(np.diff(ms_host).max())
     fused = eng.use_fused(panel.P, None, max_days)
+    pipe = (DateShardPipeline(eng, months, J, skip, nb,
+                              fused=fused and args.shard_mode == "fused")
+            if world > 1 else None)
     PM = None if fused else eng.empty((T_m, N))
     M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
     L = eng.empty((T_m, N), torch.int8)
@@ -174,7 +179,7 @@ def main():
 
     def step(ev=scratch_events):
         if pipe is not None:
-            r = pipe.run(panel.P, panel.month_start)
+            r = pipe.run(panel.P, panel.month_start, max_days)
             return r.LS
         i = 0
         ev[i].record()
@@ -228,7 +233,7 @@ def main():
     if rank == 0:
         from oracle import csmom_oracle as O
         if world > 1:
-            r = pipe.run(panel.P, panel.month_start)
+            r = pipe.run(panel.P, panel.month_start, max_days)
             Mh, Lh = r.M, r.L
         else:
             Mh, Lh = M, L
@@ -289,8 +294,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic seeded GBM panel generated in HBM (late listings, delistings, "
-                    "NaN days, absent and all-NaN months)",
-            "engine_path": ("fused k_signal" if fused else
+                    "NaN days, absent and all-NaN months); N>1: rank r holds date shard r of "
+                    "one global panel (prices continue across shards)",
+            "engine_path": (("speculative fused k_signal + k_shard_repair" if pipe.fused else
+                             "k_month_end + carried k_momentum") if pipe is not None else
+                            "fused k_signal" if fused else
                             f"k_month_end + scan ({chunks} month chunks)"),
             "config": {"workload": cfg["name"] if args.assets is None and args.days is None
                        else f"custom: {N} assets x {T_d} bdays per GPU",

@@ -26,6 +26,7 @@ EXPORTS = (
     "csm_cohort_sums", "csm_portfolio_from_cohorts", "csm_turnover_features",
     "csm_double_sort_labels", "csm_tune_ptr", "csm_next_present",
     "csm_last_present_month", "csm_portfolio_from_cohorts_multi", "csm_summary",
+    "csm_shard_repair", "csm_signal_shard", "csm_shard_summary_state",
 )
 
 
@@ -94,6 +95,12 @@ def _declare(lib):
         "csm_long_short": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p]),
         "csm_shard_summary": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p]),
         "csm_fold_carry": (ctypes.c_int, [_p, _p, _i32, _i32, _i64, _i32, _i32, _p, _p]),
+        "csm_shard_repair": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p,
+                                            _p, _p, _p]),
+        "csm_signal_shard": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p,
+                                            _p, _p, _p, _p]),
+        "csm_shard_summary_state": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p,
+                                                   _p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

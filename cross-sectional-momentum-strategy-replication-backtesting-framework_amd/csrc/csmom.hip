@@ -362,7 +362,20 @@ __device__ __forceinline__ double comp(double2 v, int k) { return k == 0 ? v.x :
 // otherwise P is row-major [T_d][N] and consecutive day rows of a wave are N * 8 B apart.
 // BW > 1 (row-major only): BW waves cover 64 * VEC * BW adjacent assets and meet at a
 // barrier every NBUF months, so a workgroup's day-row reads stay BW KiB contiguous in time.
-template <int MAXD, int VEC, int NBUF, bool TILED = false, int ST = 0, int BW = 1>
+// Speculative shards keep PM only for the first and last W + SHARD_PM_EDGE months (what the
+// summary walks and the repair read for a dense asset); other months are re-derived from the
+// daily panel for the rare asset that needs them (shard_pm_at).
+#define SHARD_PM_EDGE 8
+__device__ __forceinline__ bool shard_pm_kept(int m, int T_m, int W) {
+  return m < W + SHARD_PM_EDGE || m >= T_m - (W + SHARD_PM_EDGE);
+}
+
+// SH (speculative date shard): carry_out is instead a [5][N] end-state record -- present
+// months of the shard, the pending ranked row (month index, -1 none), its subset-ffilled
+// price, and the first / last present month (-1 none) -- for k_shard_summary_state and
+// k_shard_repair.
+template <int MAXD, int VEC, int NBUF, bool TILED = false, int ST = 0, int BW = 1,
+          bool SH = false>
 __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
@@ -377,8 +390,18 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   const bool live = a0 < N;
   const int RS = 64 * VEC * BW;
   ScanLane sl[VEC];
+  // SH counters live in LDS after the ring ([3][RS] ints: present months, first, last present
+  // month): the kernel already holds ~500 registers, and these are touched once per month
+  int* shc = reinterpret_cast<int*>(ring_lds + W * RS);
 #pragma unroll
-  for (int k = 0; k < VEC; ++k) scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, carry, N, a0 + k, live);
+  for (int k = 0; k < VEC; ++k) {
+    scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, carry, N, a0 + k, live);
+    if (SH) {
+      shc[VEC * tid + k] = 0;
+      shc[RS + VEC * tid + k] = -1;
+      shc[2 * RS + VEC * tid + k] = -1;
+    }
+  }
   const double* base = TILED ? P + (int64_t)blockIdx.x * T_d * (64 * VEC) + VEC * tid
                              : P + (live ? a0 : 0);
   const int64_t rstride = TILED ? 64 * VEC : N;
@@ -406,9 +429,15 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
         last = ok ? x : last;
       }
       pm[c] = p ? (v ? last : qnan()) : absent_val();
+      if (SH && p) {
+        int* q = shc + VEC * tid + c;
+        q[0] += 1;
+        if (q[RS] < 0) q[RS] = m;
+        q[2 * RS] = m;
+      }
     }
     if (live) {
-      if (PMo) {
+      if (PMo && (!SH || shard_pm_kept(m, T_m, W))) {
         if (VEC == 2) *reinterpret_cast<double2*>(PMo + (int64_t)m * N + a0) = make_double2(pm[0], pm[VEC - 1]);
         else PMo[(int64_t)m * N + a0] = pm[0];
       }
@@ -451,8 +480,18 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   }
   if (live) {
 #pragma unroll
-    for (int k = 0; k < VEC; ++k)
-      scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm, carry_out);
+    for (int k = 0; k < VEC; ++k) {
+      scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm,
+                  SH ? nullptr : carry_out);
+      if (SH) {
+        const int* q = shc + VEC * tid + k;
+        carry_out[a0 + k] = (double)q[0];
+        carry_out[N + a0 + k] = (double)sl[k].prev;
+        carry_out[2 * N + a0 + k] = sl[k].psff;
+        carry_out[3 * N + a0 + k] = (double)q[RS];
+        carry_out[4 * N + a0 + k] = (double)q[2 * RS];
+      }
+    }
   }
 }
 
@@ -813,6 +852,212 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 }
 
 // =====================================================================================
+// Speculative date shards (the fused multi-GPU pass).  A rank runs k_signal<SH>
+// on its month range from an EMPTY scan state (trajectory F) before the earlier shards' carry
+// is known, writing PM and a [5][N] end-state record (present months, pending row, its psff,
+// first / last present month).  k_shard_summary_state builds the exchange record from PM with
+// short walks from both ends (no full pass).  After the all-gather and k_fold_carry,
+// k_shard_repair replays each asset from the true carry (trajectory T) beside F, rewriting
+// R / M / NR, until the two states are bit-identical -- from then on every output k_signal
+// wrote is T's -- or the asset has no present month left; then it finishes the pending ranked
+// row with next_pm (k_signal ran without it).  A dense asset converges after its first
+// J + skip + 1 present months.  Bit-identical to the unfused k_month_end -> k_shard_summary ->
+// k_fold_carry -> k_momentum(carry) pass.
+// =====================================================================================
+#define REPAIR_THREADS 64
+#define REPAIR_CHUNK 8
+#define WALK_CHUNK 8
+
+// Month price of asset a in month m of a speculative shard: PM where k_signal<SH> kept it,
+// else the month-end of the daily rows (k_signal's reduction: last valid price, NaN if the
+// month has rows but no price, ABSENT if none).
+__device__ __forceinline__ double shard_pm_at(const double* __restrict__ PM,
+                                              const double* __restrict__ P,
+                                              const int64_t* __restrict__ ms, int m, int T_m,
+                                              int W, int64_t N, int64_t a) {
+  if (shard_pm_kept(m, T_m, W)) return PM[(int64_t)m * N + a];
+  // the month's day rows are loaded together (one latency per month, not one per day)
+  constexpr int KD = 24;
+  const int64_t d0 = ms[m], d1 = ms[m + 1];
+  double last = 0.0;
+  bool p = false, v = false;
+  double xs[KD];
+#pragma unroll
+  for (int k = 0; k < KD; ++k) xs[k] = (d0 + k < d1) ? P[(d0 + k) * N + a] : absent_val();
+#pragma unroll
+  for (int k = 0; k < KD; ++k) {
+    const double x = xs[k];
+    const bool ok = x == x;
+    p |= !is_absent(x);
+    v |= ok;
+    last = ok ? x : last;
+  }
+  for (int64_t d = d0 + KD; d < d1; ++d) {
+    const double x = P[d * N + a];
+    const bool ok = x == x;
+    p |= !is_absent(x);
+    v |= ok;
+    last = ok ? x : last;
+  }
+  return p ? (v ? last : qnan()) : absent_val();
+}
+
+// Same record as k_shard_summary (n, fv, lvi, lv, head, first; tail of the last T present
+// month prices, ABSENT-padded at the front) from the SH state's n / first / last month.
+__global__ __launch_bounds__(256) void k_shard_summary_state(const double* __restrict__ PM,
+                                                             const double* __restrict__ P,
+                                                             const int64_t* __restrict__ ms,
+                                                             int T_m, int64_t N, int T,
+                                                             const double* __restrict__ st,
+                                                             double* __restrict__ out) {
+  const int W = T - 1;
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  const int64_t n = (int64_t)st[a];
+  const int fm = (int)st[3 * N + a], lm = (int)st[4 * N + a];
+  int64_t fv = -1, lvi = -1;
+  double lv = qnan(), head = qnan(), first = absent_val();
+  const int k = (int)(n < T ? n : T);
+  for (int j = 0; j < T - k; ++j) out[(int64_t)(SUM_SCALARS + j) * N + a] = absent_val();
+  if (n > 0) {
+    // forward from the first present month: first price, index of the first valid row
+    first = shard_pm_at(PM, P, ms, fm, T_m, W, N, a);
+    int64_t idx = 0;
+    bool found = false;
+    for (int m0 = fm; m0 <= lm && !found; m0 += WALK_CHUNK) {
+      double buf[WALK_CHUNK];
+#pragma unroll
+      for (int j = 0; j < WALK_CHUNK; ++j)
+        buf[j] = (m0 + j <= lm) ? shard_pm_at(PM, P, ms, m0 + j, T_m, W, N, a) : absent_val();
+#pragma unroll
+      for (int j = 0; j < WALK_CHUNK; ++j) {
+        const double x = buf[j];
+        if (found || is_absent(x)) continue;
+        if (!isnan_d(x)) { fv = idx; found = true; }
+        ++idx;
+      }
+    }
+    // backward from the last present month: tail, last valid (lv, lvi), head
+    int got = 0;
+    int64_t seen = 0;          // present rows passed, newest first
+    bool have_lv = false, done = false;
+    for (int m0 = lm; m0 >= fm && !done; m0 -= WALK_CHUNK) {
+      double buf[WALK_CHUNK];
+#pragma unroll
+      for (int j = 0; j < WALK_CHUNK; ++j)
+        buf[j] = (m0 - j >= fm) ? shard_pm_at(PM, P, ms, m0 - j, T_m, W, N, a) : absent_val();
+#pragma unroll
+      for (int j = 0; j < WALK_CHUNK; ++j) {
+        const double x = buf[j];
+        if (done || is_absent(x)) continue;
+        const bool valid = !isnan_d(x);
+        if (valid && !have_lv) { lv = x; lvi = n - 1 - seen; have_lv = true; }
+        if (got < k) {
+          out[(int64_t)(SUM_SCALARS + T - 1 - got) * N + a] = x;
+          ++got;
+        } else if (valid) {
+          head = x;
+          done = true;
+        }
+        ++seen;
+      }
+    }
+  }
+  out[0 * N + a] = (double)n;
+  out[1 * N + a] = (double)fv;
+  out[2 * N + a] = (double)lvi;
+  out[3 * N + a] = lv;
+  out[4 * N + a] = head;
+  out[5 * N + a] = first;
+}
+
+// F's step: scan_step without outputs (the state transition only).
+__device__ __forceinline__ void scan_shadow(ScanLane& s, double x, int m, double* ring, int RS,
+                                            int W, int J) {
+  if (is_absent(x)) return;
+  const bool xv = !isnan_d(x);
+  const double pnew = xv ? x : s.pff;
+  const double ret = pnew / s.pff - 1.0;
+  s.pff = pnew;
+  ring[s.head * RS] = 1.0 + ret;
+  s.head = (s.head + 1 == W) ? 0 : s.head + 1;
+  double acc = ring[s.head * RS];
+  int idx = s.head;
+  for (int k = 1; k < J; ++k) {
+    idx = (idx + 1 == W) ? 0 : idx + 1;
+    acc = acc * ring[idx * RS];
+  }
+  const bool ranked = !isnan_d(acc - 1.0);
+  if (ranked) {
+    s.psff = xv ? x : s.psff;
+    s.prev = m;
+  } else {
+    s.prev = -1;
+  }
+}
+
+__device__ __forceinline__ bool same_bits(double x, double y) {
+  return __double_as_longlong(x) == __double_as_longlong(y);
+}
+
+__global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
+    const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
+    int T_m, int64_t N, int J, int skip,
+    const double* __restrict__ carry, const double* __restrict__ next_pm,
+    const double* __restrict__ st, double* __restrict__ R, double* __restrict__ M,
+    double* __restrict__ NR) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][W][REPAIR_THREADS]
+  const int W = J + skip, RS = REPAIR_THREADS;
+  const int tid = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * REPAIR_THREADS + tid;
+  if (a >= N) return;  // no barriers below
+  double* rt = lds + tid;
+  double* rf = lds + W * RS + tid;
+  ScanLane t, f;
+  scan_init(t, rt, RS, W, carry, N, a, true);
+  scan_init(f, rf, RS, W, nullptr, N, a, true);
+  auto same = [&]() -> bool {
+    if (!same_bits(t.pff, f.pff) || !same_bits(t.psff, f.psff) || t.prev != f.prev) return false;
+    for (int k = 0; k < W; ++k)
+      if (!same_bits(rt[k * RS], rf[k * RS])) return false;
+    return true;
+  };
+  const int64_t npres = (int64_t)st[a];
+  int64_t seen = 0;
+  bool conv = same();
+  bool done = conv || npres == 0;
+  for (int m0 = 0; m0 < T_m && !done; m0 += REPAIR_CHUNK) {
+    double buf[REPAIR_CHUNK];
+#pragma unroll
+    for (int j = 0; j < REPAIR_CHUNK; ++j)
+      buf[j] = (m0 + j < T_m) ? shard_pm_at(PM, P, ms, m0 + j, T_m, W, N, a) : absent_val();
+#pragma unroll
+    for (int j = 0; j < REPAIR_CHUNK; ++j) {
+      const int m = m0 + j;
+      if (m >= T_m || done) break;
+      const double x = buf[j];
+      scan_step(t, x, m, rt, RS, W, J, N, a, R, M, NR);
+      scan_shadow(f, x, m, rf, RS, W, J);
+      if (!is_absent(x)) ++seen;
+      conv = same();
+      done = conv || seen >= npres;
+    }
+  }
+  // the pending ranked row at the shard's end: F's (= T's once converged) or T's own
+  const int prev = conv ? (int)st[N + a] : t.prev;
+  const double psff = conv ? st[2 * N + a] : t.psff;
+  if (prev >= 0) {
+    double nr = qnan();
+    const double x = next_pm[a];
+    if (!is_absent(x)) {
+      const double ps_new = isnan_d(x) ? psff : x;
+      nr = ps_new / psff - 1.0;
+    }
+    NR[(int64_t)prev * N + a] = nr;
+  }
+}
+
+// =====================================================================================
 // Panel re-blocking [T_d][N] -> [ceil(N/128)][T_d][128] (csm_tile_panel).  Both sides are
 // contiguous 1 KiB (tile, day) rows; assets past N in the last tile are ABSENT.
 // =====================================================================================
@@ -977,9 +1222,12 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
                          int64_t N, const int64_t* month_start, int32_t T_m,
                          int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
                          double* M, double* NR, const double* carry, const double* next_pm,
-                         double* carry_out) {
+                         double* carry_out, bool sh = false) {
   int r = prep(ctx);
   if (r) return r;
+  if (sh && (tiled || !PM || carry || next_pm || !carry_out || T_m < 1))
+    return set_err(ctx, CSM_E_INVAL, "%s: a speculative shard pass needs PM and state, no carry / "
+                   "next_pm, and at least one month", who);
   if (!P || !month_start || !M || !NR || N <= 0 || T_d < 0 || T_m < 0 || J < 1 || skip < 0 ||
       J + skip > 256 || max_month_days < 1)
     return set_err(ctx, CSM_E_INVAL, "%s: bad arguments (N=%lld T_m=%d J=%d skip=%d)", who,
@@ -993,7 +1241,7 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   if (T_m == 0) return CSM_OK;
   const int W = J + skip;
   const bool can2 = (N % 2 == 0) && aligned16(P) && (!PM || aligned16(PM));
-  if (!tiled && can2 && g_tune_signal_mw != 0) {
+  if (!tiled && can2 && g_tune_signal_mw != 0 && !sh) {
     const int nw = g_tune_signal_mw / 10, nb = g_tune_signal_mw % 10;
     const void* fm = nullptr;
 #define SMW(MD, NW_, NB_) (const void*)k_signal_mw<MD, NW_, NB_>
@@ -1016,13 +1264,20 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   }
   const int vec = tiled ? 2 : ((g_tune_signal_vec == 1 || !can2) ? 1 : 2);
   const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : 4;
-  const int bw = (!tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
-  const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double);
+  const int bw = (!sh && !tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
+  const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double) +
+                     (sh ? (size_t)3 * 64 * vec * sizeof(int) : 0);
   const unsigned blocks = (unsigned)((N / vec + 64 * bw - 1) / (64 * bw));
   const void* fn = nullptr;
 #define SIG(MD, V, NB) (const void*)k_signal<MD, V, NB, false>
 #define SIGT(MD, NB) (const void*)k_signal<MD, 2, NB, true>
-  if (tiled)
+  if (sh)
+    fn = max_month_days <= 24
+             ? (vec == 2 ? (const void*)k_signal<24, 2, 4, false, 0, 1, true>
+                         : (const void*)k_signal<24, 1, 4, false, 0, 1, true>)
+             : (vec == 2 ? (const void*)k_signal<32, 2, 4, false, 0, 1, true>
+                         : (const void*)k_signal<32, 1, 4, false, 0, 1, true>);
+  else if (tiled)
     fn = max_month_days <= 24 ? (nbuf == 3 ? SIGT(24, 3) : SIGT(24, 4))
                               : (nbuf == 3 ? SIGT(32, 3) : SIGT(32, 4));
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_bw == 2)
@@ -1058,6 +1313,13 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
                double* carry_out) {
   return signal_launch(ctx, "csm_signal", false, P, T_d, N, month_start, T_m, max_month_days, J,
                        skip, PM, R, M, NR, carry, next_pm, carry_out);
+}
+
+int csm_signal_shard(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                     const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
+                     int32_t skip, double* PM, double* R, double* M, double* NR, double* state) {
+  return signal_launch(ctx, "csm_signal_shard", false, P, T_d, N, month_start, T_m,
+                       max_month_days, J, skip, PM, R, M, NR, nullptr, nullptr, state, true);
 }
 
 int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
@@ -1215,6 +1477,42 @@ int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, 
   hipLaunchKernelGGL(k_fold_carry, dim3(blocks), dim3(256), 0, ctx->stream, summaries, G, g, N, J,
                      skip, carry, next_pm, (const double*)nullptr);
   LAUNCH_CHECK(ctx, "k_fold_carry");
+  return CSM_OK;
+}
+
+int csm_shard_summary_state(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                            const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                            const double* state, double* out) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !PM || !state || !out || N <= 0 || T_m < 1 || J < 1 || skip < 0 ||
+      J + skip > 256)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_summary_state: bad arguments");
+  hipLaunchKernelGGL(k_shard_summary_state, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     ctx->stream, PM, P, month_start, T_m, N, J + skip + 1, state, out);
+  LAUNCH_CHECK(ctx, "k_shard_summary_state");
+  return CSM_OK;
+}
+
+int csm_shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_start, const double* PM,
+                     int32_t T_m, int64_t N, int32_t J, int32_t skip, const double* carry,
+                     const double* next_pm, const double* state, double* R, double* M,
+                     double* NR) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !PM || !carry || !next_pm || !state || !M || !NR || N <= 0 ||
+      T_m < 1 || J < 1 ||
+      skip < 0 || J + skip > 128)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_repair: bad arguments (J + skip <= 128)");
+  const int W = J + skip;
+  const size_t lds = (size_t)2 * W * REPAIR_THREADS * sizeof(double);
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_shard_repair,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_shard_repair, dim3((unsigned)((N + REPAIR_THREADS - 1) / REPAIR_THREADS)),
+                     dim3(REPAIR_THREADS), lds, ctx->stream, PM, P, month_start, T_m, N, J, skip,
+                     carry, next_pm, state, R, M, NR);
+  LAUNCH_CHECK(ctx, "k_shard_repair");
   return CSM_OK;
 }
 

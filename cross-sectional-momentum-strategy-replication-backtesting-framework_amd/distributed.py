@@ -59,27 +59,55 @@ class DateShardPipeline:
     """Runs one pass of the hot path on this rank's month range.
 
     stages: object with month_end, shard_summary, fold_carry, momentum, deciles, long_short
-    (the `Engine` method signatures).  months_per_rank: local month counts of all ranks
-    (fixed for a run, so no size exchange happens per pass).
+    (the `Engine` method signatures); with fused=True also signal and shard_repair.
+    months_per_rank: local month counts of all ranks (fixed for a run, so no size exchange
+    happens per pass).
+
+    fused=False: month-end, summary, collective 1, carry, scan from the carry (the carry is
+    needed before the scan starts, so month-end and scan are separate passes).
+    fused=True (speculative): the fused signal pass runs from an empty state at once (one
+    read of the daily panel; PM and a small end-state record written for the exchange), the
+    summary comes from short walks at both ends, collective 1 follows, and shard_repair
+    rewrites the outputs of the first months where the true carry changes them --
+    bit-identical to fused=False (tests/test_gpu_shards_api.py).
     """
 
-    def __init__(self, stages, months_per_rank, J=12, skip=1, n_bins=10, group=None):
+    def __init__(self, stages, months_per_rank, J=12, skip=1, n_bins=10, group=None,
+                 fused=False):
         self.st = stages
         self.months = list(months_per_rank)
         self.J, self.skip, self.n_bins = J, skip, n_bins
         self.group = group
+        self.fused = fused
         self.G = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         if len(self.months) != self.G:
             raise ValueError(f"months_per_rank has {len(self.months)} entries for {self.G} ranks")
         self.Tmax = max(self.months)
 
-    def run(self, P_local, month_start_local) -> ShardResult:
-        st, J, s, nb = self.st, self.J, self.skip, self.n_bins
-        PM, _ = st.month_end(P_local, month_start_local)
-        T_m, N = PM.shape
+    def _check_months(self, T_m):
         if T_m != self.months[self.rank]:
             raise ValueError(f"rank {self.rank}: {T_m} months, partition says {self.months[self.rank]}")
+
+    def run(self, P_local, month_start_local, max_month_days=None) -> ShardResult:
+        st, J, s = self.st, self.J, self.skip
+        if self.fused:
+            if max_month_days is None:
+                raise ValueError("the fused shard pass needs max_month_days")
+            T_m = month_start_local.numel() - 1
+            self._check_months(T_m)
+            if self.G == 1:
+                _, _, M, NR = st.signal(P_local, month_start_local, max_month_days, J, s)
+                return self._rank_and_gather(M, NR)
+            PM, _, M, NR, state = st.signal_shard(P_local, month_start_local, max_month_days,
+                                                  J, s)
+            summary = st.shard_summary(PM, J, s, state=state)
+            summaries = all_gather_stack(summary, self.group)          # collective 1
+            carry, next_pm = st.fold_carry(summaries, self.rank, J, s)
+            st.shard_repair(PM, carry, next_pm, state, M, NR, J, s)
+            return self._rank_and_gather(M, NR)
+        PM, _ = st.month_end(P_local, month_start_local)
+        self._check_months(PM.shape[0])
         summary = st.shard_summary(PM, J, s)
         if self.G > 1:
             summaries = all_gather_stack(summary, self.group)          # collective 1
@@ -87,6 +115,11 @@ class DateShardPipeline:
         else:
             carry, next_pm = None, None
         _, M, NR = st.momentum(PM, J, s, carry=carry, next_pm=next_pm)
+        return self._rank_and_gather(M, NR)
+
+    def _rank_and_gather(self, M, NR) -> ShardResult:
+        st, nb = self.st, self.n_bins
+        T_m = M.shape[0]
         L, EW, CNT, _ = st.deciles(M, NR, nb)
         if self.G > 1:
             pad_ew = torch.full((self.Tmax, nb), float("nan"), dtype=EW.dtype, device=EW.device)
@@ -104,27 +137,39 @@ class DateShardPipeline:
         return ShardResult(M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS)
 
 
-def virtual_shards(stages, P, month_start_host, G, J=12, skip=1, n_bins=10):
+def virtual_shards(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, fused=False):
     """Run the G-shard decomposition sequentially on ONE device (no collectives): the same
-    summary / fold / scan kernels as DateShardPipeline, for single-GPU verification that a
-    G-GPU run equals the 1-GPU run bit for bit.  Returns concatenated (M, NR, L, EW, CNT, LS)."""
+    summary / fold / scan kernels as DateShardPipeline (fused=True: the speculative signal +
+    shard_repair path), for single-GPU verification that a G-GPU run equals the 1-GPU run bit
+    for bit.  Returns concatenated (M, NR, L, EW, CNT, LS)."""
     import numpy as np
 
     ms = np.asarray(month_start_host, dtype=np.int64)
     T_m = len(ms) - 1
     dev = P.device
     parts = month_partition(T_m, G)
-    PMs = []
+    PMs, outs = [], []
     for (m0, m1) in parts:
         d0, d1 = ms[m0], ms[m1]
         msl = torch.from_numpy(ms[m0:m1 + 1] - d0).to(dev)
-        PM, _ = stages.month_end(P[d0:d1].contiguous(), msl)
+        if fused:
+            maxd = int(np.diff(ms[m0:m1 + 1]).max()) if m1 > m0 else 1
+            PM, _, M, NR, state = stages.signal_shard(P[d0:d1].contiguous(), msl, maxd, J, skip)
+            outs.append((M, NR, state))
+        else:
+            PM, _ = stages.month_end(P[d0:d1].contiguous(), msl)
+            outs.append((None, None, None))
         PMs.append(PM)
-    summaries = torch.stack([stages.shard_summary(PM, J, skip) for PM in PMs])
+    summaries = torch.stack([stages.shard_summary(PM, J, skip, state=outs[g][2])
+                             for g, PM in enumerate(PMs)])
     Ms, NRs, Ls, EWs, CNTs = [], [], [], [], []
     for g, PM in enumerate(PMs):
         carry, next_pm = stages.fold_carry(summaries, g, J, skip)
-        _, M, NR = stages.momentum(PM, J, skip, carry=carry, next_pm=next_pm)
+        if fused:
+            M, NR, state = outs[g]
+            stages.shard_repair(PM, carry, next_pm, state, M, NR, J, skip)
+        else:
+            _, M, NR = stages.momentum(PM, J, skip, carry=carry, next_pm=next_pm)
         L, EW, CNT, _ = stages.deciles(M, NR, n_bins)
         Ms.append(M); NRs.append(NR); Ls.append(L); EWs.append(EW); CNTs.append(CNT)
     EW = torch.cat(EWs).contiguous()

@@ -81,6 +81,16 @@ class PortfolioOut:
     NET: torch.Tensor | None = None   # [T_m][B] LS - COST
 
 
+@dataclass
+class ShardState:
+    """signal_shard's end-state record [5][N] (present months, pending ranked row, its
+    subset-ffilled price, first / last present month) with the daily panel it came from
+    (shard_summary / shard_repair re-derive months PM does not keep from it)."""
+    t: torch.Tensor
+    P: torch.Tensor
+    month_start: torch.Tensor
+
+
 class Engine:
     """Signal (J, skip) -> per-date n_bins labels -> equal-weight long-short, on one GPU."""
 
@@ -479,13 +489,20 @@ class Engine:
                    float(mean_block), float(p0), _ptr(src), _ptr(PMb))
         return src, PMb
 
-    def shard_summary(self, PM, J, skip, out=None):
+    def shard_summary(self, PM, J, skip, out=None, state=None):
+        """csm_shard_summary (one pass over PM), or csm_shard_summary_state (short walks,
+        the same record) when `state` from signal_shard is given."""
         T_m, N = PM.shape
         _need(PM, "PM", torch.float64, (T_m, N), self.device)
         S = 6 + J + skip + 1
         out = self.empty((S, N)) if out is None else out
         _need(out, "summary", torch.float64, (S, N), self.device)
-        self._call("csm_shard_summary", _ptr(PM), T_m, N, int(J), int(skip), _ptr(out))
+        if state is not None:
+            _need(state.t, "state", torch.float64, (5, N), self.device)
+            self._call("csm_shard_summary_state", _ptr(state.P), _ptr(state.month_start),
+                       _ptr(PM), T_m, N, int(J), int(skip), _ptr(state.t), _ptr(out))
+        else:
+            self._call("csm_shard_summary", _ptr(PM), T_m, N, int(J), int(skip), _ptr(out))
         return out
 
     def fold_carry(self, summaries, g, J, skip, carry=None, next_pm=None):
@@ -498,6 +515,45 @@ class Engine:
         self._call("csm_fold_carry", _ptr(summaries), G, int(g), N, int(J), int(skip),
                    _ptr(carry), _ptr(next_pm))
         return carry, next_pm
+
+    def signal_shard(self, P, month_start, max_month_days, J=12, skip=1, with_ret=False,
+                     out=None):
+        """csm_signal_shard: the fused pass over this date shard from an empty scan state
+        (speculative; shard_repair fixes it once the carry is known).  Returns
+        (PM, R, M, NR, ShardState); PM holds only the shard's first / last J + skip + 8
+        months (the rest are re-derived from P where needed)."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        if out is None:
+            PM, M, NR = self.empty((T_m, N)), self.empty((T_m, N)), self.empty((T_m, N))
+            R = self.empty((T_m, N)) if with_ret else None
+            state = self.empty((5, N))
+        else:
+            PM, R, M, NR, state = out
+        self._call("csm_signal_shard", _ptr(P), T_d, N, _ptr(month_start), T_m,
+                   int(max_month_days), int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR),
+                   _ptr(state))
+        return PM, R, M, NR, ShardState(state, P, month_start)
+
+    def shard_repair(self, PM, carry, next_pm, state, M, NR, J, skip, R=None):
+        """csm_shard_repair: turn the outputs of signal_shard (M, NR, R rewritten in place)
+        into those of the scan from `carry`, and finish the pending rows with `next_pm` (both
+        from fold_carry)."""
+        T_m, N = PM.shape
+        W = J + skip
+        _need(PM, "PM", torch.float64, (T_m, N), self.device)
+        _need(carry, "carry", torch.float64, (W + 2, N), self.device)
+        _need(next_pm, "next_pm", torch.float64, (N,), self.device)
+        _need(state.t, "state", torch.float64, (5, N), self.device)
+        for t, nm in ((M, "M"), (NR, "NR"), (R, "R")):
+            if t is not None:
+                _need(t, nm, torch.float64, (T_m, N), self.device)
+        self._call("csm_shard_repair", _ptr(state.P), _ptr(state.month_start), _ptr(PM), T_m, N,
+                   int(J), int(skip), _ptr(carry), _ptr(next_pm), _ptr(state.t), _ptr(R),
+                   _ptr(M), _ptr(NR))
+        return M, NR
 
     def sync(self):
         self._call("csm_sync")

@@ -52,22 +52,64 @@ def shard_calendar(start: str, periods_total: int, G: int, rank: int):
 
 def make_device_panel(N: int, days: pd.DatetimeIndex, month_start: np.ndarray, seed: int,
                       device, late=0.05, delist=0.05, nan_day=0.01, absent_month=0.002,
-                      nan_month=0.001, block_days: int = 512) -> DevicePanel:
+                      nan_month=0.001, block_days: int = 512, shard=None) -> DevicePanel:
+    """Seeded GBM panel built in HBM.  shard=(rank, world, base_seed, days_per_shard): this
+    panel is date shard `rank` of ONE global panel -- per-asset drift / volatility and the
+    log-price at every shard boundary come from base_seed (identical on every rank), and the
+    shard's path is a Brownian bridge between its two boundary levels, so prices continue
+    across shards (independent per-rank panels would jump by e^(sigma*sqrt(T)) at each
+    boundary: heavy-tailed momentum for a year after it)."""
     device = torch.device(device)
     T_d = len(days)
     T_m = len(month_start) - 1
     g = torch.Generator(device=device)
     g.manual_seed(int(seed))
     f64 = dict(dtype=torch.float64, device=device)
-    mu = torch.randn(N, generator=g, **f64) * 2e-4 + 3e-4
-    sig = torch.rand(N, generator=g, **f64) * 0.03 + 0.01
-    list_day = torch.where(torch.rand(N, generator=g, **f64) < late,
-                           torch.randint(1, max(2, T_d // 2), (N,), generator=g, device=device),
-                           torch.zeros(N, dtype=torch.int64, device=device))
-    delist_day = torch.where(torch.rand(N, generator=g, **f64) < delist,
-                             torch.randint(max(1, T_d // 2), max(2, T_d), (N,), generator=g,
-                                           device=device),
-                             torch.full((N,), T_d, dtype=torch.int64, device=device))
+    if shard is None:
+        mu = torch.randn(N, generator=g, **f64) * 2e-4 + 3e-4
+        sig = torch.rand(N, generator=g, **f64) * 0.03 + 0.01
+        lvl0, lvl1 = None, None
+    else:
+        rank, world, base_seed, dps = shard
+        gg = torch.Generator(device=device)
+        gg.manual_seed(int(base_seed) * 7919 + 17)
+        mu = torch.randn(N, generator=gg, **f64) * 2e-4 + 3e-4
+        sig = torch.rand(N, generator=gg, **f64) * 0.03 + 0.01
+        z = torch.randn(world, N, generator=gg, **f64)
+        steps = mu * dps + sig * float(np.sqrt(dps)) * z               # [world][N]
+        anchors = torch.cat([torch.zeros(1, N, **f64), torch.cumsum(steps, 0)], 0)
+        lvl0, lvl1 = anchors[rank], anchors[rank + 1]
+        # the bridge needs the shard's own walk total first: one extra pass of its stream
+        gn = torch.Generator(device=device)
+        gn.manual_seed(int(seed) * 104729 + 3)
+        tot = torch.zeros(N, **f64)
+        for d0 in range(0, T_d, block_days):
+            d1 = min(T_d, d0 + block_days)
+            tot += (torch.randn(d1 - d0, N, generator=gn, **f64) * sig + mu).sum(0)
+        gn.manual_seed(int(seed) * 104729 + 3)
+        slope = ((lvl1 - lvl0) - tot) / max(T_d, 1)
+    if shard is None:
+        list_day = torch.where(torch.rand(N, generator=g, **f64) < late,
+                               torch.randint(1, max(2, T_d // 2), (N,), generator=g, device=device),
+                               torch.zeros(N, dtype=torch.int64, device=device))
+        delist_day = torch.where(torch.rand(N, generator=g, **f64) < delist,
+                                 torch.randint(max(1, T_d // 2), max(2, T_d), (N,), generator=g,
+                                               device=device),
+                                 torch.full((N,), T_d, dtype=torch.int64, device=device))
+    else:
+        # listings and delistings belong to the global panel (an asset delisted in shard r
+        # stays delisted in shard r+1), drawn on the global day axis and shifted to this shard
+        Dg = int(round(dps * world))
+        day0 = int(round(dps * rank))
+        lg = torch.where(torch.rand(N, generator=gg, **f64) < late,
+                         torch.randint(1, max(2, Dg // 2), (N,), generator=gg, device=device),
+                         torch.zeros(N, dtype=torch.int64, device=device))
+        dg = torch.where(torch.rand(N, generator=gg, **f64) < delist,
+                         torch.randint(max(1, Dg // 2), max(2, Dg), (N,), generator=gg,
+                                       device=device),
+                         torch.full((N,), Dg, dtype=torch.int64, device=device))
+        list_day = lg - day0
+        delist_day = torch.where(dg >= Dg, torch.full_like(dg, T_d), dg - day0)
     am = torch.rand(T_m, N, generator=g, **f64) < absent_month      # absent (month, asset)
     nm = torch.rand(T_m, N, generator=g, **f64) < nan_month         # all-NaN (month, asset)
     day_month = torch.from_numpy(
@@ -78,9 +120,14 @@ def make_device_panel(N: int, days: pd.DatetimeIndex, month_start: np.ndarray, s
     qnan = torch.tensor(NAN_BITS, dtype=torch.int64, device=device)
     for d0 in range(0, T_d, block_days):
         d1 = min(T_d, d0 + block_days)
-        lr = torch.randn(d1 - d0, N, generator=g, **f64) * sig + mu
+        if lvl0 is None:
+            lr = torch.randn(d1 - d0, N, generator=g, **f64) * sig + mu
+        else:
+            lr = torch.randn(d1 - d0, N, generator=gn, **f64) * sig + mu + slope
         c = torch.cumsum(lr, 0) + run
         run = c[-1].clone()
+        if lvl0 is not None:
+            c = c + lvl0
         blk = (100.0 * torch.exp(c)).view(torch.int64)
         dd = torch.arange(d0, d1, device=device)[:, None]
         dm = day_month[d0:d1]

@@ -187,6 +187,31 @@ int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, 
                    int32_t J, int32_t skip, double* carry, double* next_pm);
 
 /*
+ * Speculative date shards (the fused multi-GPU pass; no reference counterpart).
+ * csm_signal_shard: csm_signal over this rank's months from an EMPTY scan state, before the
+ *   earlier shards' carry is known (no carry / next_pm).  PM [T_m][N] is required but only its
+ *   first and last J + skip + 8 months are written (the calls below re-derive other months
+ *   from P where an asset needs them); state [5][N] out: present months, pending ranked row
+ *   (-1 none), its subset-ffilled price, first and last present month (-1 none).  T_m >= 1.
+ * csm_shard_summary_state: the csm_shard_summary record of the shard's month prices, bit for
+ *   bit, from short walks at both ends of each asset's present months.
+ * csm_shard_repair: with carry / next_pm from csm_fold_carry, rewrites R (nullable) / M / NR
+ *   where the true carry changes them and finishes the pending rows, so the result equals
+ *   csm_momentum(month prices, carry, next_pm) bit for bit.  J + skip <= 128.
+ * P / month_start / PM / state are the csm_signal_shard call's.
+ */
+int csm_signal_shard(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                     const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
+                     int32_t skip, double* PM, double* R, double* M, double* NR, double* state);
+int csm_shard_summary_state(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                            const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                            const double* state, double* out);
+int csm_shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_start, const double* PM,
+                     int32_t T_m, int64_t N, int32_t J, int32_t skip, const double* carry,
+                     const double* next_pm, const double* state, double* R, double* M,
+                     double* NR);
+
+/*
  * Portfolio accounting beyond the reference's K = 1 equal-weight case (SURVEY 8(f) rank 2;
  * rules E1..E5 in DESIGN.md section 8 / oracle/portfolio_oracle.py).  The reference counterpart
  * is run_demo.py:49-67 (K = 1, equal weight, no costs), which this collapses to.

@@ -20,7 +20,7 @@ class OracleStages:
         PM, _ = O.month_end(P.numpy(), ms.numpy())
         return torch.from_numpy(PM), None
 
-    def shard_summary(self, PM, J, skip):
+    def shard_summary(self, PM, J, skip, state=None):
         return torch.from_numpy(O.shard_summary(PM.numpy(), J, skip))
 
     def fold_carry(self, summaries, g, J, skip):
@@ -39,6 +39,25 @@ class OracleStages:
     def long_short(self, EW, CNT):
         return torch.from_numpy(O.long_short(EW.numpy(), CNT.numpy()))
 
+    # fused (speculative) mode: the signal pass runs from an empty state; the repair stage
+    # stands in for csm_shard_repair by rescanning from the carry (orchestration test only --
+    # the kernel itself is checked on the GPU, tests/test_gpu_shards_api.py)
+    def signal(self, P, ms, max_month_days, J=12, skip=1, with_pm=False, **kw):
+        PM, _ = O.month_end(P.numpy(), ms.numpy())
+        R, M, NR, _ = O.momentum_scan(PM, J, skip)
+        return (torch.from_numpy(PM) if with_pm else None), torch.from_numpy(R), \
+            torch.from_numpy(M), torch.from_numpy(NR)
+
+    def signal_shard(self, P, ms, max_month_days, J=12, skip=1, **kw):
+        PM, R, M, NR = self.signal(P, ms, max_month_days, J, skip, with_pm=True)
+        return PM, R, M, NR, None
+
+    def shard_repair(self, PM, carry, next_pm, state, M, NR, J, skip, R=None):
+        _, M2, NR2, _ = O.momentum_scan(PM.numpy(), J, skip, state=carry, next_pm=next_pm)
+        M.copy_(torch.from_numpy(M2))
+        NR.copy_(torch.from_numpy(NR2))
+        return M, NR
+
 
 def _free_port():
     s = socket.socket()
@@ -48,7 +67,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, J, skip, q):
+def _worker(rank, world, port, J, skip, q, fused=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -62,16 +81,19 @@ def _worker(rank, world, port, J, skip, q):
         d0, d1 = ms[m0], ms[m1]
         P = torch.from_numpy(np.ascontiguousarray(z["P"][d0:d1]))
         msl = torch.from_numpy(ms[m0:m1 + 1] - d0)
-        pipe = DateShardPipeline(OracleStages(), [b - a for a, b in parts], J, skip, 10)
-        r = pipe.run(P, msl)
+        pipe = DateShardPipeline(OracleStages(), [b - a for a, b in parts], J, skip, 10,
+                                 fused=fused)
+        r = pipe.run(P, msl, int(np.diff(ms).max()))
         q.put((rank, r.M.numpy(), r.NR.numpy(), r.L.numpy(), r.EW.numpy(), r.CNT.numpy(),
                r.LS.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,J,skip", [(2, 12, 1), (3, 3, 0), (2, 9, 2)])
-def test_date_shards_gloo(world, J, skip):
+@pytest.mark.parametrize("world,J,skip,fused", [(2, 12, 1, False), (3, 3, 0, False),
+                                                (2, 9, 2, False), (2, 12, 1, True),
+                                                (3, 9, 2, True)])
+def test_date_shards_gloo(world, J, skip, fused):
     import sys
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parent))
@@ -79,7 +101,7 @@ def test_date_shards_gloo(world, J, skip):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, J, skip, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, J, skip, q, fused)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])

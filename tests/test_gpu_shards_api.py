@@ -34,6 +34,113 @@ def test_virtual_shards_equal_unsharded(engine, J, skip, G):
     assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
 
 
+@pytest.mark.parametrize("J,skip", [(12, 1), (3, 0), (9, 2)])
+@pytest.mark.parametrize("G", [2, 3, 5, 8])
+def test_fused_virtual_shards_equal_unsharded(engine, J, skip, G):
+    """Speculative fused shards (signal from an empty state + shard_repair) == one pass."""
+    from csmom.distributed import virtual_shards
+    z = load_golden("edge")
+    P, ms = _up(z["P"]), z["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), J, skip, 10)
+    M, NR, L, EW, CNT, LS = virtual_shards(engine, P, ms, G, J, skip, 10, fused=True)
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L)
+    assert torch.equal(CNT, out.CNT)
+    assert bits_equal(EW.cpu().numpy(), out.EW.cpu().numpy())
+    assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+
+
+@pytest.mark.parametrize("J,skip,G", [(24, 1, 3), (48, 1, 2), (48, 0, 4)])
+def test_fused_shards_long_windows(engine, J, skip, G):
+    from csmom.distributed import virtual_shards
+    z = load_golden("longwin")
+    P, ms = _up(z["P"]), z["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), J, skip, 10)
+    M, NR, L, EW, CNT, LS = virtual_shards(engine, P, ms, G, J, skip, 10, fused=True)
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L)
+    assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+
+
+@pytest.mark.parametrize("G", [2, 7])
+def test_fused_shards_sparse_panel(engine, G):
+    """Gappy synthetic panel: many absent months and NaN month prices, so repairs run long
+    (past several shard boundaries) and pending rows cross shards."""
+    from oracle.synth_np import make_panel
+    from csmom.distributed import virtual_shards
+    pan = make_panel(512, 2600, seed=11, nan_day=0.05, absent_month=0.25, nan_month=0.15,
+                     cents=True)
+    P, ms = _up(pan["P"]), pan["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), 12, 1, 10, with_ret=True)
+    M, NR, L, EW, CNT, LS = virtual_shards(engine, P, ms, G, 12, 1, 10, fused=True)
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L)
+    assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+
+
+def test_shard_repair_rewrites_ret(engine):
+    """With R requested, the repaired R of a shard equals the carried scan's R."""
+    z = load_golden("edge")
+    J, skip = 12, 1
+    P, ms = z["P"], z["month_start"].astype(np.int64)
+    PMd, _ = engine.month_end(_up(P), _up(ms))
+    T_m = PMd.shape[0]
+    m0 = T_m // 2
+    d0 = int(ms[m0])
+    sums = torch.stack([engine.shard_summary(PMd[:m0].contiguous(), J, skip),
+                        engine.shard_summary(PMd[m0:].contiguous(), J, skip)])
+    carry, npm = engine.fold_carry(sums, 1, J, skip)
+    R0, M0, NR0 = engine.momentum(PMd[m0:].contiguous(), J, skip, with_ret=True, carry=carry,
+                                  next_pm=npm)
+    maxd = int(np.diff(ms).max())
+    PM, R, M, NR, st = engine.signal_shard(_up(P[d0:]), _up(ms[m0:] - d0), maxd, J, skip,
+                                           with_ret=True)
+    engine.shard_repair(PM, carry, npm, st, M, NR, J, skip, R=R)
+    assert bits_equal(R.cpu().numpy(), R0.cpu().numpy())
+    assert bits_equal(M.cpu().numpy(), M0.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), NR0.cpu().numpy())
+
+
+@pytest.mark.parametrize("panel", ["edge", "longwin", "sparse"])
+@pytest.mark.parametrize("J,skip", [(12, 1), (24, 0)])
+def test_summary_from_state_equals_full_pass(engine, panel, J, skip):
+    """csm_shard_summary_state (walks from the shard's ends; months PM does not keep are
+    re-derived from P) == csm_shard_summary (full pass over the full PM), on every shard of a
+    2- and 3-way split, and signal_shard's kept PM rows / end state are right."""
+    from oracle.synth_np import make_panel
+    if panel == "sparse":   # ~240 months: shards longer than the kept edges, long walks
+        z = make_panel(300, 5000, seed=3, nan_day=0.05, absent_month=0.3, nan_month=0.3)
+    else:
+        z = load_golden(panel)
+    P, ms = z["P"], z["month_start"].astype(np.int64)
+    T_m = len(ms) - 1
+    H = J + skip + 8
+    for G in (2, 3):
+        for a, b in O.month_ranges(T_m, G):
+            d0, d1 = int(ms[a]), int(ms[b])
+            msl = ms[a:b + 1] - d0
+            maxd = int(np.diff(msl).max())
+            PM, _, M, NR, st = engine.signal_shard(_up(P[d0:d1]), _up(msl), maxd, J, skip)
+            PMref, _ = engine.month_end(_up(P[d0:d1]), _up(msl))
+            tm = b - a
+            kept = [m for m in range(tm) if m < H or m >= tm - H]
+            assert bits_equal(PM.cpu().numpy()[kept], PMref.cpu().numpy()[kept])
+            full = engine.shard_summary(PMref, J, skip)
+            fast = engine.shard_summary(PM, J, skip, state=st)
+            assert bits_equal(fast.cpu().numpy(), full.cpu().numpy()), (panel, G, a, b)
+            pres = ~O.is_absent(PMref.cpu().numpy())
+            s = st.t.cpu().numpy()
+            assert np.array_equal(s[0], pres.sum(0))
+            idx = np.arange(tm)[:, None]
+            assert np.array_equal(s[3], np.where(pres.any(0), np.where(pres, idx, 10**9).min(0),
+                                                 -1))
+            assert np.array_equal(s[4], np.where(pres.any(0), np.where(pres, idx, -1).max(0),
+                                                 -1))
+
+
 def test_summary_and_fold_match_oracle(engine):
     z = load_golden("edge")
     J, skip = 12, 1
