@@ -1023,10 +1023,11 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
     return true;
   };
   const int64_t npres = (int64_t)st[a];
+  const int fm = (int)st[3 * N + a];  // months before the first present one change no state
   int64_t seen = 0;
   bool conv = same();
   bool done = conv || npres == 0;
-  for (int m0 = 0; m0 < T_m && !done; m0 += REPAIR_CHUNK) {
+  for (int m0 = fm < 0 ? 0 : fm; m0 < T_m && !done; m0 += REPAIR_CHUNK) {
     double buf[REPAIR_CHUNK];
 #pragma unroll
     for (int j = 0; j < REPAIR_CHUNK; ++j)

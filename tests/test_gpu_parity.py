@@ -106,7 +106,7 @@ def _oracle_labels(row, n_bins=10):
 
 
 @pytest.mark.parametrize("case", ["outlier", "ties", "twoval", "dense_center", "huge_range",
-                                  "neg_zero", "odd_n"])
+                                  "neg_zero", "odd_n", "lognormal", "pareto"])
 def test_decile_stress(engine, case):
     """Cross-sections that overflow the candidate buffer and force key-space refinement."""
     rng = np.random.default_rng(hash(case) % 2**32)
@@ -123,6 +123,10 @@ def test_decile_stress(engine, case):
         x = rng.normal(0, 1, n) * 10.0 ** rng.integers(-300, 300, n)
     elif case == "neg_zero":
         x = rng.choice(np.array([-0.0, 0.0, 1.0, -1.0, 2.0]), n)
+    elif case == "lognormal":   # momentum after long gaps: the bulk squeezed by the tail
+        x = np.exp(rng.normal(0, 3, n)) - 1.0
+    elif case == "pareto":
+        x = rng.pareto(0.7, n) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
     else:
         n = 100_001
         x = rng.standard_normal(n)
