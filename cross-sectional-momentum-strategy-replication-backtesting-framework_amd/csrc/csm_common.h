@@ -27,6 +27,7 @@ struct csm_ctx {
   char err[512];
   void* scratch;          // context-owned device workspace (k_deciles bucket ids), grown lazily
   size_t scratch_bytes;
+  int n_cu;               // compute units of the device (decile kernel choice)
 };
 
 static inline int set_err(csm_ctx* c, int code, const char* fmt, ...) {
@@ -79,3 +80,13 @@ template <int NB>
 void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                            int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
+
+// wide-row decile launcher with register-resident bucket ids (deciles_reg.hip): rows with
+// N even and N <= deciles_reg_max_n(), 16-B aligned M / NR, 2-B aligned L.  The first
+// DEC_REG_RI x 2048 cells of a row keep their ids in registers; the rest are re-read.
+#define DEC_REG_RI 46   // 2 x 46 id VGPRs per lane (48: a few spills)
+int deciles_reg_max_n();
+template <int NB>
+void launch_deciles_reg(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
+                        int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
+                        int32_t* NV, int ablate, int64_t* tim);

@@ -652,6 +652,12 @@ __global__ __launch_bounds__(256) void k_last_present_month(const double* __rest
 #define DEC_THREADS 512
 #define HB 8192
 #define CAP 4096
+// label pass: 8 x 32 B of M / NR in flight per lane (128 VGPRs: still two 512-thread
+// workgroups per CU): labels 117 -> 110 us per row at C4.  Row sweeps keep ROW_U = 8 (10 made
+// the histogram pass 3 us slower; profiles/r01/experiments/dec_unroll_ab.log)
+#ifndef DEC_LU
+#define DEC_LU 8
+#endif
 namespace dec_wide {
 #include "deciles.inc"
 }  // namespace dec_wide
@@ -659,6 +665,7 @@ using dec_wide::k_deciles;
 #undef DEC_THREADS
 #undef HB
 #undef CAP
+#undef DEC_LU
 
 // =====================================================================================
 // Kernel E: long-short series (one workgroup; T_m * n_bins is tiny).
@@ -1096,6 +1103,12 @@ static int64_t* g_dec_timing = nullptr;
 // k_deciles bucket-id scratch path (N % 4 == 0): 1 on, 0 off.  Off by default: it moves
 // fewer bytes but measured slower at C4 (0.44 vs 0.40 ms, profiles/r01/experiments).
 static int g_tune_dec_ids = 0;
+// k_deciles register-resident bucket ids (deciles_reg.hip; V2 rows): 0 off (default), 1 when
+// every date row gets its own CU (T_m <= CUs), 2 always.  Off by default: it streams M once
+// instead of three times, but its ~250 VGPRs allow one 512-thread workgroup per CU (the plain
+// kernel fits two), so fewer loads are in flight per CU.  Measured C4 (461 dates): 0.57 vs
+// 0.33 ms; a 58-date shard: 0.235 vs 0.220 ms (profiles/r01/experiments/dec_reg_phases.log).
+static int g_tune_dec_reg = 0;
 // rows with at most this many assets take the narrow-row decile kernel (deciles_narrow.hip)
 static int64_t g_tune_dec_narrow_max = 16384;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
 
@@ -1112,6 +1125,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "signal_nbuf") && (value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
   if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
   if (!strcmp(key, "dec_ids") && (value == 0 || value == 1)) { g_tune_dec_ids = value; return CSM_OK; }
+  if (!strcmp(key, "dec_reg") && value >= 0 && value <= 2) { g_tune_dec_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
@@ -1137,6 +1151,8 @@ int csm_create(int device, csm_ctx** out) {
   if (!c) return CSM_E_INVAL;
   c->device = device;
   c->stream = nullptr;
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    c->n_cu = 256;
   *out = c;
   return CSM_OK;
 }
@@ -1384,11 +1400,16 @@ int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double
 template <int NB>
 static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                           int32_t* CNT, int32_t* NV, uint16_t* ids) {
+                           int32_t* CNT, int32_t* NV, uint16_t* ids, int n_cu) {
   const int ab = g_tune_dec_ablate;
   int64_t* tm = g_dec_timing;
   if (N <= g_tune_dec_narrow_max && !ids) {   // rows of a few thousand assets (C2/C3/C5)
     launch_deciles_narrow<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
+    return;
+  }
+  const bool reg_rows = g_tune_dec_reg == 2 || (g_tune_dec_reg == 1 && T_m <= n_cu);
+  if (!ids && v2 && reg_rows && N <= deciles_reg_max_n()) {   // ids in registers: one HBM read of M per row
+    launch_deciles_reg<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
     return;
   }
   if (ids) hipLaunchKernelGGL((k_deciles<NB, true, true>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
@@ -1425,15 +1446,15 @@ int csm_deciles(csm_ctx* ctx, const double* M, const double* NR, int32_t T_m, in
     ids = (uint16_t*)ctx->scratch;
   }
   if (!NR) {
-    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids);
+    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, ctx->n_cu);
   } else {
     switch (n_bins) {
-      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
-      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
-      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
-      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
-      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
-      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
       default:
         return set_err(ctx, CSM_E_INVAL, "csm_deciles: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", n_bins);
     }

@@ -14,6 +14,9 @@ from csmom.synth import bday_calendar, make_device_panel  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 IDS = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+REG = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+ABL = int(sys.argv[4]) if len(sys.argv) > 4 else 0   # dec_ablate bitmask (1: no decile sums)
+ROWS = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # >0: time only the first ROWS dates
 TD = 10_000
 days, ms, _ = bday_calendar("1985-01-01", TD)
 pan = make_device_panel(N, days, ms, seed=4, device="cuda:0")
@@ -25,6 +28,11 @@ L = eng.empty((T_m, N), torch.int8)
 EW, CNT = eng.empty((T_m, 10)), eng.empty((T_m, 10), torch.int32)
 eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
 eng.lib.csm_tune(b"dec_ids", IDS)
+eng.lib.csm_tune(b"dec_reg", REG)
+eng.lib.csm_tune(b"dec_ablate", ABL)
+if ROWS:
+    M, NR, L, EW, CNT = M[:ROWS], NR[:ROWS], L[:ROWS], EW[:ROWS], CNT[:ROWS]
+    T_m = ROWS
 for _ in range(3):
     eng.deciles(M, NR, 10, out=(L, EW, CNT, None))
 tim = torch.full((T_m, 9), -1, dtype=torch.int64, device="cuda:0")
@@ -41,7 +49,7 @@ t = t[ok]
 names = ["sample", "histogram", "targets", "refine", "gather", "select", "edges+table",
          "labels+sums", ]
 d = np.diff(t, axis=1)
-out = {"N": N, "ids": IDS, "rows_timed": int(ok.sum()), "kernel_ms": round(e0.elapsed_time(e1), 4),
+out = {"N": N, "ids": IDS, "reg": REG, "ablate": ABL, "rows": T_m, "rows_timed": int(ok.sum()), "kernel_ms": round(e0.elapsed_time(e1), 4),
        "phase_us_mean": {n: round(float(d[:, i].mean()), 2) for i, n in enumerate(names)},
        "phase_us_max": {n: round(float(d[:, i].max()), 2) for i, n in enumerate(names)},
        "row_us_mean": round(float((t[:, -1] - t[:, 0]).mean()), 2),

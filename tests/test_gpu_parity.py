@@ -105,12 +105,12 @@ def _oracle_labels(row, n_bins=10):
     return out
 
 
-@pytest.mark.parametrize("case", ["outlier", "ties", "twoval", "dense_center", "huge_range",
-                                  "neg_zero", "odd_n", "lognormal", "pareto"])
-def test_decile_stress(engine, case):
-    """Cross-sections that overflow the candidate buffer and force key-space refinement."""
+STRESS = ["outlier", "ties", "twoval", "dense_center", "huge_range", "neg_zero", "odd_n",
+          "lognormal", "pareto"]
+
+
+def _stress_row(case, n=200_000):
     rng = np.random.default_rng(hash(case) % 2**32)
-    n = 200_000
     if case == "outlier":
         x = rng.normal(0, 1e-3, n); x[7] = 1e6
     elif case == "ties":
@@ -131,6 +131,13 @@ def test_decile_stress(engine, case):
         n = 100_001
         x = rng.standard_normal(n)
     x[rng.random(n) < 0.05] = np.nan
+    return x
+
+
+@pytest.mark.parametrize("case", STRESS)
+def test_decile_stress(engine, case):
+    """Cross-sections that overflow the candidate buffer and force key-space refinement."""
+    x = _stress_row(case)
     row = x[None, :]
     L, _, _, _ = engine.deciles(_up(row), None, 10)
     assert np.array_equal(L.cpu().numpy()[0], _oracle_labels(x))
@@ -347,3 +354,46 @@ def test_narrow_and_wide_decile_kernels_agree(engine, name):
     assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
     ea, eb = a[1].cpu().numpy(), b[1].cpu().numpy()
     assert np.array_equal(np.isnan(ea), np.isnan(eb)) and max_rel(ea, eb) <= 1e-13
+
+
+@pytest.mark.parametrize("n", [100_000, 94_208, 40_002, 117_760])
+@pytest.mark.parametrize("case", [c for c in STRESS if c != "odd_n"])
+def test_register_id_decile_kernel_stress(engine, case, n):
+    """The register-resident bucket-id kernel (dec_reg=2; deciles_reg.hip: the first 94208
+    cells of an even row keep their ids in registers, the rest up to 117760 are re-read):
+    labels equal the oracle's qcut on the stress pathologies, with and without a tail."""
+    x = _stress_row(case, n)
+    lib = engine.lib
+    try:
+        assert lib.csm_tune(b"dec_reg", 2) == 0
+        L, _, _, _ = engine.deciles(_up(x[None, :]), None, 10)
+    finally:
+        lib.csm_tune(b"dec_reg", 0)
+    assert np.array_equal(L.cpu().numpy()[0], _oracle_labels(x))
+
+
+@pytest.mark.parametrize("n", [100_000, 65_536, 20_002, 117_760])
+@pytest.mark.parametrize("n_bins", [10, 3, 20])
+def test_register_id_kernel_equals_plain_wide_kernel(engine, n, n_bins):
+    """The register-id kernel and the plain wide kernel (three row sweeps) give bit-identical
+    labels, counts and decile means (lanes own the same cells and add them in the same order),
+    on multi-date panels with NaN cells."""
+    rng = np.random.default_rng(n + n_bins)
+    T = 5
+    M = rng.standard_normal((T, n)) * 0.3
+    M[rng.random((T, n)) < 0.03] = np.nan
+    M[1, : n // 3] = np.round(M[1, : n // 3], 2)        # ties
+    NR = rng.standard_normal((T, n)) * 0.05
+    NR[rng.random((T, n)) < 0.02] = np.nan
+    Md, NRd = _up(M), _up(NR)
+    lib = engine.lib
+    b = engine.deciles(Md, NRd, n_bins, with_nv=True)
+    try:
+        assert lib.csm_tune(b"dec_reg", 2) == 0
+        a = engine.deciles(Md, NRd, n_bins, with_nv=True)
+    finally:
+        lib.csm_tune(b"dec_reg", 0)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+    assert bits_equal(a[1].cpu().numpy(), b[1].cpu().numpy())
+    ref = np.stack([_oracle_labels(M[t], n_bins) for t in range(T)])
+    assert np.array_equal(a[0].cpu().numpy(), ref)
