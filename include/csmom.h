@@ -40,8 +40,10 @@ int csm_abi_version(void);
 
 /* Process-wide tuning knobs for A/B measurement: "signal_vec" (1|2 assets per lane in the
  * fused kernel), "signal_nbuf" (3|4 month buffers), "dec_ablate" (profiling-only bitmask
- * that SKIPS decile passes and so produces wrong results).  Returns CSM_E_INVAL for an
- * unknown key or value. */
+ * that SKIPS decile passes and so produces wrong results), "dec_ids" (0|1 bucket-id scratch
+ * path), "dec_reg" (0 off | 1 when T_m <= CUs | 2 always: register-resident bucket ids,
+ * bit-identical), "dec_narrow_max" (widest row for the narrow-row decile kernel).  Returns
+ * CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
  * wall-clock ticks (100 MHz) at its phase boundaries (NULL switches it off). */
