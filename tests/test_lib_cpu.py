@@ -61,3 +61,21 @@ def test_engine_requires_gpu():
     import csmom
     with pytest.raises(RuntimeError):
         csmom.Engine(0)
+
+
+def test_tune_keys_documented_in_header_are_accepted():
+    """csm_tune only sets process-wide knobs (no GPU call): every key include/csmom.h lists
+    takes its documented values and restores its default; unknown keys / values are rejected."""
+    import csmom
+    lib = csmom.load_library()
+    cases = {b"signal_vec": ([1, 2], 2), b"signal_nbuf": ([3, 4], 4), b"dec_ablate": ([0, 1], 0),
+             b"dec_ids": ([0, 1], 0), b"dec_reg": ([0, 1, 2], 0),
+             b"dec_narrow_max": ([0, 16384], 16384)}
+    for key, (vals, default) in cases.items():
+        for v in vals:
+            assert lib.csm_tune(key, v) == 0, (key, v)
+        assert lib.csm_tune(key, default) == 0
+    assert lib.csm_tune(b"dec_reg", 3) != 0
+    assert lib.csm_tune(b"signal_vec", 3) != 0
+    assert lib.csm_tune(b"no_such_knob", 1) != 0
+    assert lib.csm_tune(None, 1) != 0
