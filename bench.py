@@ -354,6 +354,14 @@ class TimedStages:
         T_m, N = PM.shape
         return self._wrap("scan(k_momentum*)", 24.0 * N * T_m, self.eng.momentum, PM, J, skip, **k)
 
+    def momentum_multi(self, PM, Js, skip=1):
+        T_m, N = PM.shape
+        return self._wrap("scan(k_momentum*)", (8.0 + 16.0 * len(Js)) * N * T_m,
+                          self.eng.momentum_multi, PM, Js, skip)
+
+    def default_chunks(self, *a, **k):
+        return self.eng.default_chunks(*a, **k)
+
     def deciles(self, M, NR=None, n_bins=10, **k):
         R_, N = M.shape
         return self._wrap("deciles(k_deciles)", 9.0 * N * R_, self.eng.deciles, M, NR, n_bins, **k)

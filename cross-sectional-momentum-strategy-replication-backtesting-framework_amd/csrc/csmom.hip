@@ -340,6 +340,89 @@ __device__ __forceinline__ void momentum_body(
   scan_finish(s, ring, RS, W, N, a, NR, next_pm, carry_out);
 }
 
+// Several look-backs in one scan (parameter sweeps, C3 / C5): one read of PM, one ring of
+// Jmax + skip factors fl(1 + ret), and per J the sequential product over the oldest J of its
+// last J + skip factors -- the same factors in the same order as k_momentum with a ring of
+// exactly J + skip, so M and NR are bit-identical to per-J k_momentum calls.  NR is kept per
+// J: the ranked subset (and so next_ret's subset-ffill, run_demo.py:48) starts J + skip
+// present months after the first price.  No carry / next_pm (whole panels only).
+#define MJ_MAX 4
+struct MJSet {
+  int J[MJ_MAX];
+  double* M[MJ_MAX];
+  double* NR[MJ_MAX];
+};
+
+__global__ __launch_bounds__(256) void k_momentum_multi(const double* __restrict__ PM, int T_m,
+                                                        int64_t N, int nJ, int skip, int W,
+                                                        MJSet mj) {
+  extern __shared__ __attribute__((aligned(16))) double ring_lds[];
+  const int tid = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + tid;
+  if (a >= N) return;   // no barriers below
+  const int RS = blockDim.x;
+  double* ring = ring_lds + tid;
+  const double NaN = qnan();
+  for (int k = 0; k < W; ++k) ring[k * RS] = NaN;
+  int head = 0;
+  double pff = NaN;
+  double psff[MJ_MAX];
+  int prev[MJ_MAX];
+#pragma unroll
+  for (int q = 0; q < MJ_MAX; ++q) { psff[q] = NaN; prev[q] = -1; }
+  for (int m0 = 0; m0 < T_m; m0 += SCAN_CHUNK) {
+    double buf[SCAN_CHUNK];
+#pragma unroll
+    for (int j = 0; j < SCAN_CHUNK; ++j)
+      buf[j] = (m0 + j < T_m) ? PM[(int64_t)(m0 + j) * N + a] : absent_val();
+#pragma unroll
+    for (int j = 0; j < SCAN_CHUNK; ++j) {
+      const int m = m0 + j;
+      if (m >= T_m) break;
+      const double x = buf[j];
+      const int64_t o = (int64_t)m * N + a;
+      if (is_absent(x)) {
+#pragma unroll
+        for (int q = 0; q < MJ_MAX; ++q)
+          if (q < nJ) { mj.M[q][o] = NaN; mj.NR[q][o] = NaN; }
+        continue;
+      }
+      const bool xv = !isnan_d(x);
+      const double pnew = xv ? x : pff;
+      const double ret = pnew / pff - 1.0;
+      pff = pnew;
+      ring[head * RS] = 1.0 + ret;          // push: overwrite the oldest, advance head
+      head = (head + 1 == W) ? 0 : head + 1;
+#pragma unroll
+      for (int q = 0; q < MJ_MAX; ++q) {
+        if (q >= nJ) break;
+        const int J = mj.J[q];
+        int idx = head + (W - J - skip);      // oldest of this J's window
+        if (idx >= W) idx -= W;
+        double acc = ring[idx * RS];
+        for (int k = 1; k < J; ++k) {
+          idx = (idx + 1 == W) ? 0 : idx + 1;
+          acc = acc * ring[idx * RS];
+        }
+        const double mom = acc - 1.0;
+        const double ps_new = xv ? x : psff[q];
+        if (prev[q] >= 0) mj.NR[q][(int64_t)prev[q] * N + a] = ps_new / psff[q] - 1.0;
+        if (!isnan_d(mom)) {
+          psff[q] = ps_new;
+          prev[q] = m;
+        } else {
+          mj.NR[q][o] = NaN;
+          prev[q] = -1;
+        }
+        mj.M[q][o] = mom;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MJ_MAX; ++q)
+    if (q < nJ && prev[q] >= 0) mj.NR[q][(int64_t)prev[q] * N + a] = NaN;
+}
+
 // =====================================================================================
 // Kernel AB (fused): month-end aggregation + scan in one stream over the daily panel, for
 // large N.  One wave per block, two assets per lane (16-B row loads, 1 KiB per wave-
@@ -1232,6 +1315,38 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
   hipLaunchKernelGGL(k_momentum, dim3(blocks), dim3(tpb), lds, ctx->stream, PM, T_m, N, J,
                      skip, R, M, NR, carry, next_pm, carry_out);
   LAUNCH_CHECK(ctx, "k_momentum");
+  return CSM_OK;
+}
+
+int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                       const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
+                       double* const* NR) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!PM || !Js || !M || !NR || N <= 0 || T_m < 0 || nJ < 1 || nJ > MJ_MAX || skip < 0)
+    return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi: bad arguments (N=%lld T_m=%d nJ=%d "
+                   "skip=%d; 1 <= nJ <= %d)", (long long)N, T_m, nJ, skip, MJ_MAX);
+  MJSet mj;
+  int Jmax = 0;
+  for (int q = 0; q < MJ_MAX; ++q) {
+    mj.J[q] = q < nJ ? Js[q] : 1;
+    mj.M[q] = q < nJ ? M[q] : nullptr;
+    mj.NR[q] = q < nJ ? NR[q] : nullptr;
+    if (q < nJ && (Js[q] < 1 || !M[q] || !NR[q]))
+      return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi: J[%d]=%d or its outputs invalid", q,
+                     q < nJ ? Js[q] : 0);
+    if (q < nJ && Js[q] > Jmax) Jmax = Js[q];
+  }
+  const int W = Jmax + skip;
+  if (W > 64)
+    return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi: max(J) + skip = %d > 64", W);
+  if (T_m == 0) return CSM_OK;
+  const int tpb = SCAN_THREADS;
+  const size_t lds = (size_t)W * tpb * sizeof(double);   // <= 64 KiB
+  const unsigned blocks = (unsigned)((N + tpb - 1) / tpb);
+  hipLaunchKernelGGL(k_momentum_multi, dim3(blocks), dim3(tpb), lds, ctx->stream, PM, T_m, N,
+                     nJ, skip, W, mj);
+  LAUNCH_CHECK(ctx, "k_momentum_multi");
   return CSM_OK;
 }
 

@@ -170,6 +170,25 @@ class Engine:
                    _ptr(NR), _ptr(carry), _ptr(next_pm), _ptr(carry_out))
         return R, M, NR
 
+    def momentum_multi(self, PM, Js, skip=1):
+        """csm_momentum_multi: one scan for several look-backs (up to 4 per launch).  Returns
+        [(M, NR)] in the order of Js, each equal bit for bit to momentum(PM, J, skip)."""
+        T_m, N = PM.shape
+        _need(PM, "PM", torch.float64, (T_m, N), self.device)
+        Js = [int(J) for J in Js]
+        outs = []
+        for q0 in range(0, len(Js), 4):
+            grp = Js[q0:q0 + 4]
+            Ms = [self.empty((T_m, N)) for _ in grp]
+            NRs = [self.empty((T_m, N)) for _ in grp]
+            jarr = (ctypes.c_int32 * len(grp))(*grp)
+            marr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in Ms])
+            narr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in NRs])
+            self._call("csm_momentum_multi", _ptr(PM), T_m, N, jarr, len(grp), int(skip), marr,
+                       narr)
+            outs.extend(zip(Ms, NRs))
+        return outs
+
     @staticmethod
     def default_chunks(T_m, N, J=12, skip=1):
         """Chunks for the time-chunked scan: enough (chunk, asset) lanes to fill the chip

@@ -89,6 +89,17 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
                  const double* next_pm, double* carry_out);
 
 /*
+ * Several look-backs in one scan (parameter sweeps): Js[nJ] (1 <= nJ <= 4, host array),
+ * M[q] / NR[q] host arrays of device [T_m][N] outputs.  One read of PM; each (M[q], NR[q])
+ * equals csm_momentum(PM, Js[q], skip) bit for bit.  max(J) + skip <= 64; no carry.
+ * Replaces, per sweep batch, the per-J `compute_monthly_momentum_from_daily(...,
+ * lookback_months=J)` calls (src/features.py:47-52, run_demo.py:48).
+ */
+int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                       const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
+                       double* const* NR);
+
+/*
  * Time-chunked scan for panels with few assets: the months are split into C contiguous
  * chunks that are scanned concurrently from exactly rebuilt boundary states (the date-shard
  * summary/fold of csm_shard_summary / csm_fold_carry, inside one GPU).  Same outputs as

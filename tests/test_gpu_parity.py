@@ -397,3 +397,45 @@ def test_register_id_kernel_equals_plain_wide_kernel(engine, n, n_bins):
     assert bits_equal(a[1].cpu().numpy(), b[1].cpu().numpy())
     ref = np.stack([_oracle_labels(M[t], n_bins) for t in range(T)])
     assert np.array_equal(a[0].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("name", ["edge", "c1", "longwin"])
+@pytest.mark.parametrize("Js,skip", [((3, 6, 9, 12), 1), ((12,), 1), ((1, 2), 0),
+                                     ((24, 48, 12, 5, 7), 2)])
+def test_momentum_multi_equals_per_J_scans(engine, name, Js, skip):
+    """csm_momentum_multi (one scan, one ring of max(J) + skip factors) equals csm_momentum per
+    J bit for bit -- M and the J-dependent NR -- including > 4 look-backs (two launches)."""
+    z = load_golden(name)
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    outs = engine.momentum_multi(PM, Js, skip)
+    assert len(outs) == len(Js)
+    for J, (M, NR) in zip(Js, outs):
+        _, M1, NR1 = engine.momentum(PM, J, skip, chunked=False)
+        assert bits_equal(M.cpu().numpy(), M1.cpu().numpy()), J
+        assert bits_equal(NR.cpu().numpy(), NR1.cpu().numpy()), J
+
+
+def test_sweep_batch_multi_J_scan_equals_per_J(engine):
+    """A wide sweep batch (B x N lanes fill the chip) with multi_j_scan takes the multi-J scan;
+    its summary table equals the per-J scan path bit for bit."""
+    from csmom.sweep import SweepConfig, SweepRunner
+    z = load_golden("edge")
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    T_m, N = PM.shape
+    B = max(1, -(-140_000 // N))
+    PMb = PM.repeat(1, B).contiguous()
+    cfg = SweepConfig(multi_j_scan=True)
+    run = SweepRunner(engine, cfg)
+    a, _ = run.run_batch(PMb, B)
+
+    class PerJ:   # the engine without momentum_multi
+        def __init__(self, e):
+            self._e = e
+
+        def __getattr__(self, k):
+            if k == "momentum_multi":
+                raise AttributeError(k)
+            return getattr(self._e, k)
+
+    b, _ = SweepRunner(PerJ(engine), cfg).run_batch(PMb, B)
+    assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
