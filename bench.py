@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-assets", type=int, default=150000)   # ~10-15 s of oracle time
     ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--per-j-scan", action="store_true",
+                    help="C5: one scan per J instead of every J of a wide batch from one scan "
+                         "(csm_momentum_multi, the default)")
     return ap.parse_args()
 
 
@@ -422,7 +425,8 @@ def sweep_main(args):
     T_m = len(ms_host) - 1
     eng = csmom.Engine(local)
     ts = TimedStages(eng)
-    scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
+                             multi_j_scan=not args.per_j_scan)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":

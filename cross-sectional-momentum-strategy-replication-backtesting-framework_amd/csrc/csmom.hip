@@ -423,6 +423,79 @@ __global__ __launch_bounds__(256) void k_momentum_multi(const double* __restrict
     if (q < nJ && prev[q] >= 0) mj.NR[q][(int64_t)prev[q] * N + a] = NaN;
 }
 
+// Register-ring variant for max(J) + skip <= RW: the last RW factors live in registers as a
+// shift register (f[RW-1] newest), and J's product runs over all RW slots with the slots
+// outside its window predicated off.  acc starts at 1.0 and 1.0 * x == x exactly, so the
+// product is still oldest-first over the same factors: bit-identical, no LDS round trips.
+template <int RW>
+__global__ __launch_bounds__(256) void k_momentum_multi_reg(const double* __restrict__ PM,
+                                                            int T_m, int64_t N, int nJ, int skip,
+                                                            MJSet mj) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  const double NaN = qnan();
+  double f[RW];
+#pragma unroll
+  for (int k = 0; k < RW; ++k) f[k] = NaN;
+  double pff = NaN;
+  double psff[MJ_MAX];
+  int prev[MJ_MAX], lo[MJ_MAX];
+#pragma unroll
+  for (int q = 0; q < MJ_MAX; ++q) {
+    psff[q] = NaN; prev[q] = -1;
+    lo[q] = RW - mj.J[q] - skip;   // window = slots [lo, RW - skip)
+  }
+  const int hi = RW - skip;
+  for (int m0 = 0; m0 < T_m; m0 += SCAN_CHUNK) {
+    double buf[SCAN_CHUNK];
+#pragma unroll
+    for (int j = 0; j < SCAN_CHUNK; ++j)
+      buf[j] = (m0 + j < T_m) ? PM[(int64_t)(m0 + j) * N + a] : absent_val();
+#pragma unroll
+    for (int j = 0; j < SCAN_CHUNK; ++j) {
+      const int m = m0 + j;
+      if (m >= T_m) break;
+      const double x = buf[j];
+      const int64_t o = (int64_t)m * N + a;
+      if (is_absent(x)) {
+#pragma unroll
+        for (int q = 0; q < MJ_MAX; ++q)
+          if (q < nJ) { mj.M[q][o] = NaN; mj.NR[q][o] = NaN; }
+        continue;
+      }
+      const bool xv = !isnan_d(x);
+      const double pnew = xv ? x : pff;
+      const double ret = pnew / pff - 1.0;
+      pff = pnew;
+#pragma unroll
+      for (int k = 0; k + 1 < RW; ++k) f[k] = f[k + 1];
+      f[RW - 1] = 1.0 + ret;
+#pragma unroll
+      for (int q = 0; q < MJ_MAX; ++q) {
+        if (q >= nJ) break;
+        double acc = 1.0;
+#pragma unroll
+        for (int k = 0; k < RW; ++k) acc = (k >= lo[q] && k < hi) ? acc * f[k] : acc;
+        const double mom = acc - 1.0;
+        const double ps_new = xv ? x : psff[q];
+        if (prev[q] >= 0) mj.NR[q][(int64_t)prev[q] * N + a] = ps_new / psff[q] - 1.0;
+        if (!isnan_d(mom)) {
+          psff[q] = ps_new;
+          prev[q] = m;
+        } else {
+          mj.NR[q][o] = NaN;
+          prev[q] = -1;
+        }
+        mj.M[q][o] = mom;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MJ_MAX; ++q)
+    if (q < nJ && prev[q] >= 0) mj.NR[q][(int64_t)prev[q] * N + a] = NaN;
+}
+#define MJ_REG_W 16
+
 // =====================================================================================
 // Kernel AB (fused): month-end aggregation + scan in one stream over the daily panel, for
 // large N.  One wave per block, two assets per lane (16-B row loads, 1 KiB per wave-
@@ -1192,6 +1265,8 @@ static int g_tune_dec_ids = 0;
 // kernel fits two), so fewer loads are in flight per CU.  Measured C4 (461 dates): 0.57 vs
 // 0.33 ms; a 58-date shard: 0.235 vs 0.220 ms (profiles/r01/experiments/dec_reg_phases.log).
 static int g_tune_dec_reg = 0;
+// csm_momentum_multi: 1 register shift ring when max(J) + skip <= 16, 0 the LDS ring
+static int g_tune_mj_reg = 1;
 // rows with at most this many assets take the narrow-row decile kernel (deciles_narrow.hip)
 static int64_t g_tune_dec_narrow_max = 16384;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
 
@@ -1208,6 +1283,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "signal_nbuf") && (value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
   if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
   if (!strcmp(key, "dec_ids") && (value == 0 || value == 1)) { g_tune_dec_ids = value; return CSM_OK; }
+  if (!strcmp(key, "mj_reg") && (value == 0 || value == 1)) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_reg") && value >= 0 && value <= 2) { g_tune_dec_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
@@ -1342,8 +1418,14 @@ int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
     return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi: max(J) + skip = %d > 64", W);
   if (T_m == 0) return CSM_OK;
   const int tpb = SCAN_THREADS;
-  const size_t lds = (size_t)W * tpb * sizeof(double);   // <= 64 KiB
   const unsigned blocks = (unsigned)((N + tpb - 1) / tpb);
+  if (W <= MJ_REG_W && g_tune_mj_reg) {   // register shift ring
+    hipLaunchKernelGGL(k_momentum_multi_reg<MJ_REG_W>, dim3(blocks), dim3(tpb), 0, ctx->stream,
+                       PM, T_m, N, nJ, skip, mj);
+    LAUNCH_CHECK(ctx, "k_momentum_multi_reg");
+    return CSM_OK;
+  }
+  const size_t lds = (size_t)W * tpb * sizeof(double);   // <= 64 KiB
   hipLaunchKernelGGL(k_momentum_multi, dim3(blocks), dim3(tpb), lds, ctx->stream, PM, T_m, N,
                      nJ, skip, W, mj);
   LAUNCH_CHECK(ctx, "k_momentum_multi");

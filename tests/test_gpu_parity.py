@@ -401,23 +401,28 @@ def test_register_id_kernel_equals_plain_wide_kernel(engine, n, n_bins):
 
 @pytest.mark.parametrize("name", ["edge", "c1", "longwin"])
 @pytest.mark.parametrize("Js,skip", [((3, 6, 9, 12), 1), ((12,), 1), ((1, 2), 0),
-                                     ((24, 48, 12, 5, 7), 2)])
+                                     ((24, 48, 12, 5, 7), 2), ((16,), 0), ((14, 2), 2)])
 def test_momentum_multi_equals_per_J_scans(engine, name, Js, skip):
     """csm_momentum_multi (one scan, one ring of max(J) + skip factors) equals csm_momentum per
     J bit for bit -- M and the J-dependent NR -- including > 4 look-backs (two launches)."""
     z = load_golden(name)
     PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
-    outs = engine.momentum_multi(PM, Js, skip)
-    assert len(outs) == len(Js)
-    for J, (M, NR) in zip(Js, outs):
-        _, M1, NR1 = engine.momentum(PM, J, skip, chunked=False)
-        assert bits_equal(M.cpu().numpy(), M1.cpu().numpy()), J
-        assert bits_equal(NR.cpu().numpy(), NR1.cpu().numpy()), J
+    for mj_reg in (1, 0):   # register shift ring (max J + skip <= 16) and the LDS ring
+        assert engine.lib.csm_tune(b"mj_reg", mj_reg) == 0
+        try:
+            outs = engine.momentum_multi(PM, Js, skip)
+        finally:
+            engine.lib.csm_tune(b"mj_reg", 1)
+        assert len(outs) == len(Js)
+        for J, (M, NR) in zip(Js, outs):
+            _, M1, NR1 = engine.momentum(PM, J, skip, chunked=False)
+            assert bits_equal(M.cpu().numpy(), M1.cpu().numpy()), (J, mj_reg)
+            assert bits_equal(NR.cpu().numpy(), NR1.cpu().numpy()), (J, mj_reg)
 
 
 def test_sweep_batch_multi_J_scan_equals_per_J(engine):
-    """A wide sweep batch (B x N lanes fill the chip) with multi_j_scan takes the multi-J scan;
-    its summary table equals the per-J scan path bit for bit."""
+    """A wide sweep batch (B x N lanes fill the chip) takes the multi-J scan (multi_j_scan, the
+    default); its summary table equals the per-J scan path bit for bit."""
     from csmom.sweep import SweepConfig, SweepRunner
     z = load_golden("edge")
     PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
