@@ -1,0 +1,18 @@
+#!/bin/bash
+# End-of-session evidence: full GPU suite, smoke, C4 / C2 / C3 / C5 bench lines.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; tail -1 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; tail -1 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench_c4.log 2>&1 || exit $?
+grep -o '"ms_per_step": [0-9.]*\|"frac": [0-9.]*' gpurun_out/bench_c4.log | tr '\n' ' '; echo
+timeout -k 10 300 python -u bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_c2.log 2>&1 || exit $?
+grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_c2.log
+timeout -k 10 300 python -u bench.py --config c3 --steps 5 --warmup 1 > gpurun_out/bench_c3.log 2>&1 || exit $?
+grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_c3.log
+timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 > gpurun_out/bench_c5.log 2>&1 || exit $?
+grep -o '"ms_per_step": [0-9.]*\|"stage_ms": {[^}]*}' gpurun_out/bench_c5.log
+echo end done
