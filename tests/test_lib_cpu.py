@@ -39,6 +39,7 @@ def test_null_context_is_inval():
     assert lib.csm_signal(None, None, 0, 0, None, 0, 23, 12, 1, None, None, None, None, None,
                           None, None) == -1
     assert lib.csm_deciles(None, None, None, 0, 0, 10, None, None, None, None, None) == -1
+    assert lib.csm_momentum_multi(None, None, 0, 0, None, 0, 1, None, None) == -1
     assert lib.csm_sync(None) == -1
     assert lib.csm_last_error(None) == b"null context"
 
