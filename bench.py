@@ -41,6 +41,16 @@ CONFIGS = {
 }
 
 
+# The reference's pandas path (features.py:5-107, run_demo.py:41-67), timed in the survey
+# container on a 10,000 x 10,000-day proxy of C4: context for the line, not
+# measured by bench.py (the reference does not travel to the GPU box).
+REFERENCE_PANDAS = {"value": 1.41e6, "unit": "asset-days/s", "cores": 1, "kind": "reference",
+                    "value_excluding_turnover": 2.65e6,
+                    "c4_seconds_extrapolated": 720.0, "c4_seconds_excluding_turnover": 380.0,
+                    "where": "survey container, 8-core Xeon VM, pandas 2.3.3 (1 core); "
+                             "BASELINE.md, C4 proxy 1e8 asset-days, extrapolated linearly"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -58,6 +68,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-assets", type=int, default=150000)   # ~10-15 s of oracle time
     ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--no-ids", action="store_true",
+                    help="C4: decile pass streams mom_J (k_deciles) instead of the bucket ids the "
+                         "fused signal kernel writes (csm_signal_ids -> csm_deciles_ids)")
+    ap.add_argument("--match-dates", type=int, default=0,
+                    help="decile-match check on this many evenly spaced dates (0 = every date)")
     ap.add_argument("--per-j-scan", action="store_true",
                     help="C5: one scan per J instead of every J of a wide batch from one scan "
                          "(csm_momentum_multi, the default)")
@@ -167,13 +182,18 @@ def main():
     L = eng.empty((T_m, N), torch.int8)
     EW, CNT = eng.empty((T_m, nb)), eng.empty((T_m, nb), torch.int32)
     LS = eng.empty((T_m,))
+    # fused + wide rows: the signal kernel writes each mom_J's fixed-map bucket id and the
+    # decile pass histograms the 2-B ids instead of streaming mom_J three times
+    use_ids = fused and pipe is None and not args.no_ids and N % 4 == 0 and N > 16384
+    IDS = eng.empty((T_m, N), torch.int16) if use_ids else None
     chunks = 1 if fused else eng.default_chunks(T_m, N, J, skip)
     ws = None
     if chunks > 1:
         nbytes = int(eng.lib.csm_momentum_chunked_workspace(T_m, N, J, skip, chunks))
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     scan_name = f"scan(k_momentum_chunked x{chunks})" if chunks > 1 else "scan(k_momentum)"
-    stage_names = (["signal(k_signal)", "deciles(k_deciles)", "long_short"] if fused else
+    stage_names = (["signal(k_signal+ids)", "deciles(k_deciles<ids>)", "long_short"] if use_ids else
+                   ["signal(k_signal)", "deciles(k_deciles)", "long_short"] if fused else
                    ["month_end(k_month_end)", scan_name, "deciles(k_deciles)", "long_short"])
     nst = len(stage_names) + 1
     step_events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst)]
@@ -186,7 +206,10 @@ def main():
             return r.LS
         i = 0
         ev[i].record()
-        if fused:
+        if use_ids:
+            eng.signal_ids(panel.P, panel.month_start, max_days, J, skip,
+                           out=(None, None, M, NR, IDS))
+        elif fused:
             eng.signal(panel.P, panel.month_start, max_days, J, skip, out=(None, None, M, NR))
         else:
             eng.month_end(panel.P, panel.month_start, PM=PM)
@@ -198,7 +221,10 @@ def main():
                 eng.momentum(PM, J, skip, out=(None, M, NR))
         i += 1
         ev[i].record()
-        eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
+        if use_ids:
+            eng.deciles_ids(M, NR, IDS, nb, out=(L, EW, CNT, None))
+        else:
+            eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
         i += 1
         ev[i].record()
         eng.long_short(EW, CNT, LS)
@@ -231,7 +257,8 @@ def main():
     else:
         stage_ms[:] = np.nan
 
-    # decile match vs the oracle on sampled dates (metric: "decile match %")
+    # decile match vs the oracle (metric: "decile match %"): the oracle's qcut on the engine's
+    # mom_J for every date (or --match-dates evenly spaced ones), labels compared cell by cell
     match = None
     if rank == 0:
         from oracle import csmom_oracle as O
@@ -240,19 +267,25 @@ def main():
             Mh, Lh = r.M, r.L
         else:
             Mh, Lh = M, L
-        dates = sorted({T_m // 3, T_m // 2, T_m - 2})
+        if args.match_dates > 0:
+            dates = sorted({int(x) for x in np.linspace(0, T_m - 1, args.match_dates)})
+        else:
+            dates = list(range(T_m))
         tot = ok = 0
-        for t in dates:
-            row = Mh[t].cpu().numpy()
-            ref = np.full(N, -1, dtype=np.int8)
-            v = ~np.isnan(row)
-            if v.any():
-                lab = O.qcut_labels(row[v], nb)
-                ref[v] = np.where(np.isnan(lab), -1, lab).astype(np.int8)
-            got = Lh[t].cpu().numpy()
-            ok += int((got == ref).sum())
-            tot += N
-        match = dict(pct=100.0 * ok / tot, sample=f"{len(dates)} dates x {N} assets vs oracle qcut")
+        for t0 in range(0, len(dates), 64):
+            blk = dates[t0:t0 + 64]
+            mrows = Mh[blk].cpu().numpy()
+            lrows = Lh[blk].cpu().numpy()
+            for row, got in zip(mrows, lrows):
+                ref = np.full(N, -1, dtype=np.int8)
+                v = ~np.isnan(row)
+                if v.any():
+                    lab = O.qcut_labels(row[v], nb)
+                    ref[v] = np.where(np.isnan(lab), -1, lab).astype(np.int8)
+                ok += int((got == ref).sum())
+                tot += N
+        match = dict(pct=100.0 * ok / tot, sample=f"{len(dates)} of {T_m} dates x {N} assets: "
+                                                  f"oracle qcut of the engine's mom_J")
 
     ms_per_step = 1000.0 * elapsed / args.steps
     units = N * T_d * world if args.scaling == "weak" else N * total_days
@@ -301,6 +334,7 @@ def main():
                     "one global panel (prices continue across shards)",
             "engine_path": (("speculative fused k_signal + k_shard_repair" if pipe.fused else
                              "k_month_end + carried k_momentum") if pipe is not None else
+                            "fused k_signal (+ bucket ids) -> k_deciles on ids" if use_ids else
                             "fused k_signal" if fused else
                             f"k_month_end + scan ({chunks} month chunks)"),
             "config": {"workload": cfg["name"] if args.assets is None and args.days is None
@@ -318,6 +352,8 @@ def main():
             "decile_match_pct": match["pct"] if match else None,
             "decile_check": match["sample"] if match else None,
             "cpu_baseline": None,
+            # context only (not measured by this run): the reference's own pandas path
+            "reference_pandas": REFERENCE_PANDAS,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_assets, T_d, cfg["start"])

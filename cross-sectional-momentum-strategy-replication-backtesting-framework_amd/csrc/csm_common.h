@@ -75,6 +75,25 @@ struct QTab {
   double q[MAXQ];
 };
 
+// Fixed bucket map of the fused pipeline (csm_signal_ids writes one u16 id per asset-month,
+// the decile pass histograms the ids instead of re-reading mom_J): y = fl(1 + x), 2048
+// buckets per octave of y over [1/4, 4), clamped at both ends (x <= -3/4 -> 0, x >= 3 ->
+// 8191).  fl(1 + x) is monotone in x and so are the bits of a positive double, so the map is
+// monotone non-decreasing: bucket order never contradicts value order, and the decile pass
+// stays exact for ANY data -- the map only decides how many values share a bucket.  12-month
+// momentum cross-sections put ~100k / 8192 values per bucket in the bulk (log-normal-ish in
+// y); a row the map fits badly falls back to key-space refinement (slower, same labels).
+#define CSM_FB_BUCKETS 8192
+#define CSM_FB_NAN 0xFFFFu
+__device__ __forceinline__ int csm_fbucket(double x) {
+  const int64_t b = ((int64_t)__double_as_longlong(1.0 + x)) >> 41;
+  const int64_t k = b - (0x3FD0000000000000LL >> 41);   // bits(0.25) >> 41
+  return (int)(k < 0 ? 0 : (k > CSM_FB_BUCKETS - 1 ? CSM_FB_BUCKETS - 1 : k));
+}
+__device__ __forceinline__ uint32_t csm_fid(double x) {
+  return x == x ? (uint32_t)csm_fbucket(x) : CSM_FB_NAN;
+}
+
 // narrow-row decile launcher (deciles_narrow.hip), NB in {0,2,3,4,5,10,20}
 template <int NB>
 void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,

@@ -536,7 +536,7 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out, int64_t T_d) {
+    double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS) {
   static_assert(!TILED || BW == 1, "tiled panels are read one tile per wave");
   typedef typename RowT<VEC>::T VT;
   extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC * BW]
@@ -597,9 +597,16 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
         if (VEC == 2) *reinterpret_cast<double2*>(PMo + (int64_t)m * N + a0) = make_double2(pm[0], pm[VEC - 1]);
         else PMo[(int64_t)m * N + a0] = pm[0];
       }
+      double mom[VEC];
 #pragma unroll
       for (int c = 0; c < VEC; ++c)
-        scan_step<ST>(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
+        mom[c] = scan_step<ST>(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
+      if (IDS) {   // fixed-map bucket ids for the decile pass (csm_signal_ids)
+        if (VEC == 2)
+          *reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0) = csm_fid(mom[0]) | (csm_fid(mom[VEC - 1]) << 16);
+        else
+          IDS[(int64_t)m * N + a0] = (uint16_t)csm_fid(mom[0]);
+      }
     }
   };
   VT A[MAXD], B[MAXD], C[MAXD];
@@ -1436,7 +1443,7 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
                          int64_t N, const int64_t* month_start, int32_t T_m,
                          int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
                          double* M, double* NR, const double* carry, const double* next_pm,
-                         double* carry_out, bool sh = false) {
+                         double* carry_out, bool sh = false, uint16_t* ids = nullptr) {
   int r = prep(ctx);
   if (r) return r;
   if (sh && (tiled || !PM || carry || next_pm || !carry_out || T_m < 1))
@@ -1455,7 +1462,7 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   if (T_m == 0) return CSM_OK;
   const int W = J + skip;
   const bool can2 = (N % 2 == 0) && aligned16(P) && (!PM || aligned16(PM));
-  if (!tiled && can2 && g_tune_signal_mw != 0 && !sh) {
+  if (!tiled && can2 && g_tune_signal_mw != 0 && !sh && !ids) {
     const int nw = g_tune_signal_mw / 10, nb = g_tune_signal_mw % 10;
     const void* fm = nullptr;
 #define SMW(MD, NW_, NB_) (const void*)k_signal_mw<MD, NW_, NB_>
@@ -1514,7 +1521,8 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     int T_m_ = T_m, J_ = J, skip_ = skip;
     int64_t N_ = N, T_d_ = T_d;
     void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
-                    (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out, &T_d_};
+                    (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out, &T_d_,
+                    (void*)&ids};
     HIP_CHECK(ctx, hipLaunchKernel(fn, dim3(blocks), dim3(64 * bw), args, lds, ctx->stream));
   }
   LAUNCH_CHECK(ctx, who);
@@ -1527,6 +1535,16 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
                double* carry_out) {
   return signal_launch(ctx, "csm_signal", false, P, T_d, N, month_start, T_m, max_month_days, J,
                        skip, PM, R, M, NR, carry, next_pm, carry_out);
+}
+
+int csm_signal_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                   const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
+                   int32_t skip, double* PM, double* R, double* M, double* NR, uint16_t* ids) {
+  if (!ids || (N % 4) != 0 || ((uintptr_t)ids & 7u) != 0)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_ids: ids must be non-NULL and 8-B aligned, N %% 4 == 0 "
+                   "(N=%lld)", (long long)N);
+  return signal_launch(ctx, "csm_signal_ids", false, P, T_d, N, month_start, T_m, max_month_days, J,
+                       skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids);
 }
 
 int csm_signal_shard(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
@@ -1597,9 +1615,13 @@ int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double
 template <int NB>
 static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                           int32_t* CNT, int32_t* NV, uint16_t* ids, int n_cu) {
+                           int32_t* CNT, int32_t* NV, uint16_t* ids, int n_cu, bool pre = false) {
   const int ab = g_tune_dec_ablate;
   int64_t* tm = g_dec_timing;
+  if (pre) {   // ids written by csm_signal_ids (fixed map): M is read only for a few cells
+    hipLaunchKernelGGL((k_deciles<NB, true, true, 0, true>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+    return;
+  }
   if (N <= g_tune_dec_narrow_max && !ids) {   // rows of a few thousand assets (C2/C3/C5)
     launch_deciles_narrow<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
     return;
@@ -1667,6 +1689,94 @@ int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T
   if (!EW || !CNT || !LS || T_m < 0 || n_bins < 1)
     return set_err(ctx, CSM_E_INVAL, "csm_long_short: bad arguments");
   if (T_m == 0) return CSM_OK;
+  hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
+  LAUNCH_CHECK(ctx, "k_long_short");
+  return CSM_OK;
+}
+
+static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
+                            const double* M, const double* NR, int64_t N, int32_t n_bins,
+                            const QTab& q, int8_t* L, double* EW, int32_t* CNT, int32_t* NV,
+                            uint16_t* ids, bool pre) {
+  if (!NR) {
+    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, ctx->n_cu, pre);
+  } else {
+    switch (n_bins) {
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
+      default:
+        return set_err(ctx, CSM_E_INVAL, "%s: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", who, n_bins);
+    }
+  }
+  LAUNCH_CHECK(ctx, who);
+  return CSM_OK;
+}
+
+static bool ids_ok(int64_t N, const double* M, const double* NR, const int8_t* L, const uint16_t* ids) {
+  return ids && (N % 4) == 0 && ((uintptr_t)ids & 7u) == 0 && aligned16(M) && (!NR || aligned16(NR)) &&
+         (((uintptr_t)L & 3u) == 0);
+}
+
+int csm_deciles_ids(csm_ctx* ctx, const double* M, const double* NR, const uint16_t* ids,
+                    int32_t T_m, int64_t N, int32_t n_bins, const double* qtable, int8_t* L,
+                    double* EW, int32_t* CNT, int32_t* NV) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!M || !L || !qtable || N <= 0 || T_m < 0 || n_bins < 1 || n_bins > MAXQ - 1 || N > 0x7FFFFFFFLL)
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles_ids: bad arguments (N=%lld T_m=%d n_bins=%d)",
+                   (long long)N, T_m, n_bins);
+  if (NR && (!EW || !CNT))
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles_ids: EW and CNT are required when NR is given");
+  if (!ids_ok(N, M, NR, L, ids))
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles_ids: needs N %% 4 == 0, 8-B aligned ids, 16-B aligned "
+                   "M / NR, 4-B aligned L (N=%lld)", (long long)N);
+  if (T_m == 0) return CSM_OK;
+  QTab q;
+  for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
+  return deciles_dispatch(ctx, "csm_deciles_ids", true, T_m, M, NR, N, n_bins, q, L, EW, CNT, NV,
+                          const_cast<uint16_t*>(ids), true);
+}
+
+int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
+                 int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, int32_t n_bins,
+                 const double* qtable, double* PM, double* R, double* M, double* NR, int8_t* L,
+                 double* EW, int32_t* CNT, int32_t* NV, double* LS) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !qtable || !M || !NR || !L || !EW || !CNT || !LS || N <= 0 ||
+      T_m < 0 || n_bins < 1 || n_bins > MAXQ - 1 || N > 0x7FFFFFFFLL)
+    return set_err(ctx, CSM_E_INVAL, "csm_pipeline: bad arguments (N=%lld T_m=%d n_bins=%d)",
+                   (long long)N, T_m, n_bins);
+  if (T_m == 0) return CSM_OK;
+  // the id path needs 4-aligned rows and the wide decile kernel; otherwise signal + deciles
+  uint16_t* ids = nullptr;
+  const bool want_ids = (N % 4) == 0 && N > g_tune_dec_narrow_max && aligned16(P) && aligned16(M) &&
+                        aligned16(NR) && (((uintptr_t)L & 3u) == 0) && (!PM || aligned16(PM)) &&
+                        (!R || aligned16(R));
+  if (want_ids) {
+    const size_t need = (size_t)T_m * (size_t)N * sizeof(uint16_t);
+    if (ctx->scratch_bytes < need) {
+      if (ctx->scratch) HIP_CHECK(ctx, hipFree(ctx->scratch));
+      ctx->scratch = nullptr;
+      ctx->scratch_bytes = 0;
+      HIP_CHECK(ctx, hipMalloc(&ctx->scratch, need));
+      ctx->scratch_bytes = need;
+    }
+    ids = (uint16_t*)ctx->scratch;
+  }
+  r = signal_launch(ctx, "csm_pipeline", false, P, T_d, N, month_start, T_m, max_month_days, J,
+                    skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids);
+  if (r) return r;
+  QTab q;
+  for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
+  const bool v2 = (N % 2 == 0) && aligned16(M) && aligned16(NR) && (((uintptr_t)L & 1u) == 0);
+  r = deciles_dispatch(ctx, "csm_pipeline", v2, T_m, M, NR, N, n_bins, q, L, EW, CNT, NV, ids,
+                       ids != nullptr);
+  if (r) return r;
   hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
   LAUNCH_CHECK(ctx, "k_long_short");
   return CSM_OK;

@@ -29,8 +29,15 @@ _RENAME = {"Date": "date", "Ticker": "ticker", "Open": "open", "High": "high", "
            "Close": "close", "Adj Close": "adj_close", "Volume": "volume"}
 
 
-def cache_path(data_dir: str, ticker: str, freq: str = "daily") -> str:
-    return os.path.join(data_dir, f"{ticker}_{freq}.csv")
+# Module-level cache directory, as the reference's DATA_DIR (data_io.py:8); relative to the
+# working directory like the reference's.  Unlike the reference, importing this module does
+# not create it (a read-only cache is never written here: there is no network to fill it).
+DATA_DIR = "data"
+
+
+def cache_path(ticker: str, freq: str = "daily", data_dir: str | None = None) -> str:
+    """data_io.py:11-12: `<DATA_DIR>/<ticker>_<freq>.csv` (data_dir overrides DATA_DIR)."""
+    return os.path.join(DATA_DIR if data_dir is None else data_dir, f"{ticker}_{freq}.csv")
 
 
 def normalize_daily_columns(df: pd.DataFrame, ticker: str) -> pd.DataFrame:
@@ -52,14 +59,23 @@ def normalize_daily_columns(df: pd.DataFrame, ticker: str) -> pd.DataFrame:
     return df[DAILY_COLUMNS].copy()
 
 
-def fetch_daily(tickers, data_dir: str = "data", verbose: bool = True) -> pd.DataFrame:
-    """Offline `fetch_daily` (src/data_io.py:131-180): cached CSVs only."""
+def fetch_daily(tickers, start=None, end=None, interval="1d", force_refresh=False, verbose=True,
+                data_dir: str | None = None) -> pd.DataFrame:
+    """Drop-in `fetch_daily` (src/data_io.py:131-180), cached CSVs only.
+
+    Same signature and return value as the reference (data_dir is an extra keyword that
+    overrides DATA_DIR).  Like the reference, a cached read ignores start / end / interval
+    (data_io.py:149-151 reads the whole file).  A ticker without a cached file -- or every
+    ticker when force_refresh=True -- would need yfinance (data_io.py:153); offline that is
+    the reference's "yfinance returned no data" branch: a warning and the ticker is skipped.
+    """
     parts = []
     for t in tickers:
-        p = cache_path(data_dir, t, "daily")
-        if not os.path.exists(p):
+        p = cache_path(t, "daily", data_dir)
+        if force_refresh or not os.path.exists(p):
             if verbose:
-                print(f"[fetch_daily] warning: no cached data for {t} (offline)")
+                print(f"[fetch_daily] warning: yfinance returned no data for {t} "
+                      f"(offline: no download of {start}..{end} at {interval})")
             continue
         try:
             df = normalize_daily_columns(pd.read_csv(p, low_memory=False), t)
@@ -78,11 +94,11 @@ def fetch_daily(tickers, data_dir: str = "data", verbose: bool = True) -> pd.Dat
     return pd.concat(parts, ignore_index=True)
 
 
-def load_daily_panel(tickers, data_dir: str = "data", verbose: bool = False) -> DensePanel:
+def load_daily_panel(tickers, data_dir: str | None = None, verbose: bool = False) -> DensePanel:
     """Cached CSVs straight to the dense [T_d][N] panel the engine uploads (ABSENT-encoded,
     tickers in lexicographic order, union business-day axis)."""
-    return from_long(fetch_daily(tickers, data_dir, verbose))
+    return from_long(fetch_daily(tickers, verbose=verbose, data_dir=data_dir))
 
 
-__all__ = ["DAILY_COLUMNS", "cache_path", "normalize_daily_columns", "fetch_daily",
+__all__ = ["DAILY_COLUMNS", "DATA_DIR", "cache_path", "normalize_daily_columns", "fetch_daily",
            "load_daily_panel"]

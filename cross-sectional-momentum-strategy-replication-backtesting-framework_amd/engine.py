@@ -242,6 +242,71 @@ class Engine:
                    _ptr(next_pm), _ptr(carry_out))
         return PM, R, M, NR
 
+    def signal_ids(self, P, month_start, max_month_days, J=12, skip=1, with_pm=False,
+                   with_ret=False, out=None):
+        """csm_signal_ids: csm_signal (no carry) that also writes the fixed-map bucket id of
+        every mom_J (uint16 [T_m][N], read by deciles_ids).  N % 4 == 0.
+        Returns (PM, R, M, NR, IDS)."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        if out is None:
+            PM = self.empty((T_m, N)) if with_pm else None
+            R = self.empty((T_m, N)) if with_ret else None
+            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
+            IDS = self.empty((T_m, N), torch.int16)
+        else:
+            PM, R, M, NR, IDS = out
+        _need(IDS, "IDS", torch.int16, (T_m, N), self.device)
+        self._call("csm_signal_ids", _ptr(P), T_d, N, _ptr(month_start), T_m, int(max_month_days),
+                   int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR), _ptr(IDS))
+        return PM, R, M, NR, IDS
+
+    def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False):
+        """csm_deciles_ids: deciles() from the ids of signal_ids (same labels / counts)."""
+        T_m, N = M.shape
+        _need(M, "M", torch.float64, (T_m, N), self.device)
+        _need(IDS, "IDS", torch.int16, (T_m, N), self.device)
+        if NR is not None:
+            _need(NR, "NR", torch.float64, (T_m, N), self.device)
+        if out is None:
+            L = self.empty((T_m, N), torch.int8)
+            EW = self.empty((T_m, n_bins)) if NR is not None else None
+            CNT = self.empty((T_m, n_bins), torch.int32) if NR is not None else None
+            NV = self.empty((T_m,), torch.int32) if with_nv else None
+        else:
+            L, EW, CNT, NV = out
+        q = quantile_table(n_bins)
+        self._call("csm_deciles_ids", _ptr(M), _ptr(NR), _ptr(IDS), T_m, N, int(n_bins),
+                   q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV))
+        return L, EW, CNT, NV
+
+    def pipeline(self, P, month_start, J=12, skip=1, n_bins=10, max_month_days=None,
+                 with_pm=True, with_ret=False, out=None) -> PipelineOut:
+        """csm_pipeline: the whole K = 1 pass in one C call (fused signal with bucket ids,
+        labels + decile means, long-short)."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        if max_month_days is None:
+            max_month_days = int((month_start[1:] - month_start[:-1]).max().item()) if T_m else 1
+        if out is None:
+            PM = self.empty((T_m, N)) if with_pm else None
+            R = self.empty((T_m, N)) if with_ret else None
+            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
+            L = self.empty((T_m, N), torch.int8)
+            EW, CNT = self.empty((T_m, n_bins)), self.empty((T_m, n_bins), torch.int32)
+            NV, LS = self.empty((T_m,), torch.int32), self.empty((T_m,))
+        else:
+            PM, R, M, NR, L, EW, CNT, NV, LS = out
+        q = quantile_table(n_bins)
+        self._call("csm_pipeline", _ptr(P), T_d, N, _ptr(month_start), T_m, int(max_month_days),
+                   int(J), int(skip), int(n_bins), q.ctypes.data_as(ctypes.c_void_p), _ptr(PM),
+                   _ptr(R), _ptr(M), _ptr(NR), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV), _ptr(LS))
+        return PipelineOut(PM=PM, M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS, R=R, NV=NV)
+
     def tile_panel(self, P, out=None):
         """Re-block a row-major [T_d][N] panel into the asset-tiled layout
         [ceil(N/128)][T_d][128] (csm_tile_panel); returns the flat tiled tensor."""
@@ -592,10 +657,9 @@ class Engine:
             max_month_days = int((month_start[1:] - month_start[:-1]).max().item())
         if fused is None:
             fused = self.use_fused(P, V, max_month_days)
-        if fused:
-            PM, R, M, NR = self.signal(P, month_start, max_month_days, J, skip, with_pm=True,
-                                       with_ret=with_ret)
-            VOL = None
+        if fused:   # one C call: signal (+ bucket ids for wide rows) -> deciles -> long-short
+            return self.pipeline(P, month_start, J, skip, n_bins, max_month_days, with_pm=True,
+                                 with_ret=with_ret)
         else:
             PM, VOL = self.month_end(P, month_start, V)
             if self.default_chunks(T_m, N, J, skip) > 1:

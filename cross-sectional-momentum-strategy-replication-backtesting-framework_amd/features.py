@@ -2,8 +2,10 @@
 
 `compute_monthly_momentum_from_daily` keeps the reference signature and output frame
 (src/features.py:5-57) but runs month-end aggregation and the ret/mom scan on the GPU.
-`compute_monthly_turnover` (src/features.py:60-107) is host-side pandas: its result is never
-used by the momentum path, so it is kept for API completeness only.
+`compute_monthly_turnover` (src/features.py:60-107) keeps the reference frame contract and
+computes adv / turnover / the rolling mean with csm_turnover_features on the GPU (its result is
+not consumed by the decile path, SURVEY.md 8(a) a5, but monthly_replication computes it as
+run_demo.py:33 does).
 """
 from __future__ import annotations
 
@@ -63,12 +65,10 @@ def compute_monthly_momentum_from_daily(daily_df, lookback_months=12, skip_month
     return monthly_frame(panel, host["PM"], host["VOL"], host["R"], host["M"])
 
 
-def compute_monthly_turnover(monthly_df, shares_info_map=None, lookback_months=3):
-    """src/features.py:60-107 (host pandas; the momentum path never consumes it)."""
-    df = monthly_df.copy()
-    df["monthly_volume"] = pd.to_numeric(
-        df.get("monthly_volume", df.get("volume", np.nan)), errors="coerce").fillna(0)
-    df["adv_est"] = df["monthly_volume"] / 21.0
+def _shares_column(df, shares_info_map):
+    """The `shares_outstanding` column of features.py:78-97 (a per-ticker lookup, with the
+    int(market_cap / price) fallback per row), built as the reference's row-wise apply would
+    build it so the column's dtype matches (int64 when every value is an int, else float)."""
     n = len(df)
     so = np.full(n, np.nan, dtype=object)
     if isinstance(shares_info_map, dict) and n:
@@ -89,13 +89,65 @@ def compute_monthly_turnover(monthly_df, shares_info_map=None, lookback_months=3
                         so[r] = int(mcap / p)
                     except Exception:
                         so[r] = np.nan
-    df["shares_outstanding"] = pd.Series(list(so), index=df.index).infer_objects()
-    sov = pd.to_numeric(df["shares_outstanding"], errors="coerce")
-    with np.errstate(invalid="ignore", divide="ignore"):
-        df["turnover_monthly"] = np.where(sov > 0, df["adv_est"] / sov, np.nan)
-    df["turn_avg"] = (df.groupby("ticker")["turnover_monthly"]
-                      .rolling(lookback_months, min_periods=1).mean()
-                      .reset_index(level=0, drop=True))
+    return pd.Series(list(so), index=df.index).infer_objects()
+
+
+def _shares_arrays(tickers, shares_info_map):
+    """Per-asset so / mcap for csm_turnover_features (NaN = not given; the kernel applies the
+    same so-else-int(mcap / price) rule per row)."""
+    N = len(tickers)
+    so, mcap = np.full(N, np.nan), np.full(N, np.nan)
+    if isinstance(shares_info_map, dict):
+        for a, t in enumerate(tickers):
+            info = shares_info_map.get(t, {})
+            s = info.get("shares_outstanding")
+            if s is not None and not pd.isna(s):
+                so[a] = float(s)
+            m = info.get("market_cap")
+            if m is not None and m is not False:
+                try:
+                    mcap[a] = float(m)
+                except (TypeError, ValueError):
+                    mcap[a] = np.nan
+    return so, mcap
+
+
+def compute_monthly_turnover(monthly_df, shares_info_map=None, lookback_months=3, device=None):
+    """src/features.py:60-107 with the arithmetic on the GPU (csm_turnover_features, rule T1).
+
+    Same input and output frame as the reference: adv_est, shares_outstanding,
+    turnover_monthly and turn_avg columns added to a copy.  The rolling mean runs over each
+    ticker's rows in frame order (the reference's groupby-rolling), so the dense layout is
+    [row rank within ticker][ticker]; lookback_months in [1, 48].
+    """
+    df = monthly_df.copy()
+    df["monthly_volume"] = pd.to_numeric(
+        df.get("monthly_volume", df.get("volume", np.nan)), errors="coerce").fillna(0)
+    n = len(df)
+    df["adv_est"] = df["monthly_volume"] / 21.0
+    df["shares_outstanding"] = _shares_column(df, shares_info_map)
+    if n == 0:
+        df["turnover_monthly"] = np.array([], dtype=np.float64)
+        df["turn_avg"] = np.array([], dtype=np.float64)
+        return df
+    codes, tickers = pd.factorize(df["ticker"], sort=False)
+    rank = pd.Series(codes).groupby(codes).cumcount().to_numpy()
+    T, N = int(rank.max()) + 1, len(tickers)
+    eng = get_engine(device)
+    PM = np.full((T, N), np.nan)
+    PM.view(np.uint64)[...] = np.uint64(0x7FF4000000000001)    # ABSENT: ticker has no k-th row
+    price = (pd.to_numeric(df["adj_close"], errors="coerce").to_numpy(dtype=np.float64)
+             if "adj_close" in df.columns else np.full(n, np.nan))
+    PM[rank, codes] = price
+    VOL = np.zeros((T, N))
+    VOL[rank, codes] = df["monthly_volume"].to_numpy(dtype=np.float64)
+    so, mcap = _shares_arrays(list(tickers), shares_info_map)
+    up = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(eng.device)
+    ADV, SH, TURN, TAVG = eng.turnover_features(up(PM), up(VOL), up(so), up(mcap),
+                                                int(lookback_months))
+    df["adv_est"] = ADV.cpu().numpy()[rank, codes]
+    df["turnover_monthly"] = TURN.cpu().numpy()[rank, codes]
+    df["turn_avg"] = TAVG.cpu().numpy()[rank, codes]
     return df
 
 

@@ -53,10 +53,12 @@ class ReplicationResult:
 
 def monthly_replication(daily_df, shares_info=None, lookback_months=12, skip_months=1,
                         n_bins=10, plot_path=os.path.join(RESULTS, "monthly_mom_cum.png"),
-                        compute_turnover=False, keep_monthly=False, device=None,
+                        compute_turnover=True, keep_monthly=False, device=None,
                         verbose=True):
     """run_demo.py:31-79 with the GPU engine.  Returns a ReplicationResult, or None where the
-    reference prints a message and returns early."""
+    reference prints a message and returns early.  Like run_demo.py:33 it computes the share
+    turnover features (on the GPU, csm_turnover_features) even though the decile path does not
+    use them; compute_turnover=False skips them."""
     panel, host, dev = monthly_signal(daily_df, lookback_months, skip_months, device)
     monthly = None
     if host is not None and (keep_monthly or compute_turnover):
@@ -64,7 +66,7 @@ def monthly_replication(daily_df, shares_info=None, lookback_months=12, skip_mon
     turnover = None
     if compute_turnover and monthly is not None:
         turnover = compute_monthly_turnover(monthly, shares_info_map=shares_info,
-                                            lookback_months=3)
+                                            lookback_months=3, device=device)
     if host is None or np.isnan(host["M"]).all():
         if verbose:
             print("No monthly momentum data available after cleaning.")

@@ -32,6 +32,14 @@ from .distributed import all_gather_stack
 SUMMARY_FIELDS = ("months", "mean", "sharpe", "turnover", "cost", "net_mean", "net_sharpe")
 
 
+def _free_bytes(t: torch.Tensor) -> int:
+    """Free memory of t's device (host tensors: unbounded)."""
+    if t.is_cuda:
+        free, _ = torch.cuda.mem_get_info(t.device)
+        return int(free)
+    return 1 << 62
+
+
 def strategy_grid(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12)):
     return [(int(J), int(K)) for J in Js for K in Ks]
 
@@ -114,14 +122,18 @@ class SweepRunner:
                   SIG=SIG, with_costs=c.costs)
         # multi_j_scan (wide batches): every J from one scan of PMb (csm_momentum_multi, the
         # register shift ring: C5 scan stage 30.6 -> 28.9 ms/step; bit-identical per J)
+        # The multi-J scan keeps every J's M and NR live at once (2 * len(Js) [T_m][B*N] f64
+        # panels, ~10 GB at C5 with batch 100); take it only when that fits in half the free
+        # device memory, else scan per J (two panels live at a time).
         multi = None
+        need = 2 * len(c.Js) * T_m * BN * PMb.element_size()
         if (c.multi_j_scan and hasattr(st, "momentum_multi") and len(c.Js) > 1
                 and st.default_chunks(T_m, BN, max(c.Js), c.skip) == 1
-                and max(c.Js) + c.skip <= 64):
-            multi = dict(zip(c.Js, st.momentum_multi(PMb, c.Js, c.skip)))
-        for J in c.Js:   # one J's ranking / portfolio panels live at a time
+                and max(c.Js) + c.skip <= 64 and need <= _free_bytes(PMb) // 2):
+            multi = list(st.momentum_multi(PMb, c.Js, c.skip))   # by position: Js may repeat
+        for q, J in enumerate(c.Js):   # one J's ranking / portfolio panels live at a time
             if multi is not None:
-                M, NR = multi.pop(J)
+                (M, NR), multi[q] = multi[q], None
             else:
                 _, M, NR = st.momentum(PMb, J, c.skip)
             L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)

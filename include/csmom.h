@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CSM_ABI_VERSION 1
+#define CSM_ABI_VERSION 2
 #define CSM_ABSENT_BITS 0x7FF4000000000001ULL
 
 #define CSM_OK 0
@@ -42,7 +42,12 @@ int csm_abi_version(void);
  * fused kernel), "signal_nbuf" (3|4 month buffers), "dec_ablate" (profiling-only bitmask
  * that SKIPS decile passes and so produces wrong results), "dec_ids" (0|1 bucket-id scratch
  * path), "dec_reg" (0 off | 1 when T_m <= CUs | 2 always: register-resident bucket ids,
- * bit-identical), "dec_narrow_max" (widest row for the narrow-row decile kernel).  Returns
+ * bit-identical), "dec_narrow_max" (widest row for the narrow-row decile kernel),
+ * "mj_reg" (csm_momentum_multi: 1 register shift ring when max(J) + skip <= 16, the default;
+ * 0 the shared-memory ring), "month_end_rows" (0 off | max month days: one-shot month-end
+ * kernel), "signal_bw" (1|2|4 waves per fused-kernel workgroup), "signal_store" (0 plain |
+ * 1 nontemporal | 2 none: profiling ablation), "signal_mw" (0 | 21 | 22 | 41 | 42 multi-wave
+ * fused kernel), "cohort_lds" / "cohort_seg" (portfolio cohort-sum kernel choice).  Returns
  * CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
@@ -124,6 +129,15 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
                double* carry_out);
 
 /*
+ * csm_signal (no carry) that also writes ids[T_m][N] (uint16, 8-B aligned, N % 4 == 0): each
+ * mom_J's bucket under the fixed monotone map of csm_deciles_ids (0xFFFF = NaN), so the decile
+ * pass reads 2 B per cell instead of 8.
+ */
+int csm_signal_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                   const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
+                   int32_t skip, double* PM, double* R, double* M, double* NR, uint16_t* ids);
+
+/*
  * next_pm[N] for a month boundary m0: the month price of each asset's first present month
  * >= m0 (ABSENT if none).  With csm_signal's carry_out / carry this splits the fused pass into
  * month segments that chain bit for bit (so per-date ranking of early segments can overlap
@@ -175,6 +189,27 @@ int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
 int csm_deciles(csm_ctx* ctx, const double* M, const double* NR, int32_t T_m, int64_t N,
                 int32_t n_bins, const double* qtable, int8_t* L, double* EW, int32_t* CNT,
                 int32_t* NV);
+
+/*
+ * csm_deciles with the ids of csm_signal_ids: the same labels / EW / CNT / NV bit for bit;
+ * M is read only for the cells whose bucket holds an order statistic, an interior edge, or
+ * the row's min / max.  N % 4 == 0, 16-B aligned M / NR, 4-B aligned L.
+ */
+int csm_deciles_ids(csm_ctx* ctx, const double* M, const double* NR, const uint16_t* ids,
+                    int32_t T_m, int64_t N, int32_t n_bins, const double* qtable, int8_t* L,
+                    double* EW, int32_t* CNT, int32_t* NV);
+
+/*
+ * The whole K = 1 path of run_demo.py:31-67 in one call: fused month-end + scan (csm_signal,
+ * with ids when N % 4 == 0 and the row is wide), per-date labels fused with the decile means
+ * (csm_deciles / csm_deciles_ids), long-short (csm_long_short).  Arguments as in those calls;
+ * PM, R, NV nullable; qtable HOST.  The ids live in a context-owned workspace (T_m * N * 2 B,
+ * grown on first use).
+ */
+int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
+                 int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, int32_t n_bins,
+                 const double* qtable, double* PM, double* R, double* M, double* NR, int8_t* L,
+                 double* EW, int32_t* CNT, int32_t* NV, double* LS);
 
 /*
  * Long-short series.  Replaces run_demo.py:57-67: top minus bottom label mean when both

@@ -38,9 +38,26 @@ def test_normalize_quirks():
 def test_missing_file_is_skipped(tmp_path, capsys):
     import csmom.data as D
     (tmp_path / "OK_daily.csv").write_text("Date,Adj Close,Volume\n2020-01-02,5.0,7\n")
-    df = D.fetch_daily(["NOPE", "OK"], str(tmp_path))
+    df = D.fetch_daily(["NOPE", "OK"], data_dir=str(tmp_path))
     assert list(df["ticker"]) == ["OK"] and df["adj_close"].iloc[0] == 5.0
-    assert "no cached data for NOPE" in capsys.readouterr().out
+    assert "yfinance returned no data for NOPE" in capsys.readouterr().out
+
+
+def test_reference_call_signature(tmp_path, monkeypatch, capsys):
+    """run_demo.py:196 calls fetch_daily(tickers, start=..., end=..., verbose=True) with the
+    cache in DATA_DIR (data_io.py:8); cached reads ignore start / end (data_io.py:149-151)."""
+    import inspect
+    import csmom.data as D
+    params = list(inspect.signature(D.fetch_daily).parameters)
+    assert params[:6] == ["tickers", "start", "end", "interval", "force_refresh", "verbose"]
+    (tmp_path / "OK_daily.csv").write_text("Date,Adj Close,Volume\n2017-06-02,5.0,7\n"
+                                           "2020-01-02,6.0,8\n")
+    monkeypatch.setattr(D, "DATA_DIR", str(tmp_path))
+    df = D.fetch_daily(["OK"], start="2018-01-01", end="2024-12-31", verbose=True)
+    assert list(df["adj_close"]) == [5.0, 6.0]          # the 2017 row is kept, as in the reference
+    assert "loaded OK rows=2" in capsys.readouterr().out
+    assert D.fetch_daily(["OK"], force_refresh=True, verbose=False).empty   # would download
+    assert list(D.fetch_daily([], verbose=False).columns) == D.DAILY_COLUMNS
 
 
 @pytest.mark.skipif(not REF_DATA.exists(), reason="reference data/ not present")

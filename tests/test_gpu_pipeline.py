@@ -1,0 +1,190 @@
+"""GPU parity of the bucket-id pipeline (csm_signal_ids -> csm_deciles_ids, csm_pipeline).
+
+The fused signal kernel writes each mom_J's bucket under a FIXED monotone map
+(csrc/csm_common.h csm_fbucket); the decile pass histograms those 2-B ids instead of
+streaming mom_J again.  The map only decides how many values share a bucket, so labels,
+counts and ranked-row counts must equal the default decile kernel's (and the oracle's,
+run_demo.py:18-29) bit for bit on any data, decile means within 1e-10 (they are summed in a
+different fixed order).  The stress rows reach every slow path: refinement of a bucket that
+holds the whole row, extreme buckets holding huge tails, all-equal rows, +-0.0.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits_equal, load_golden, max_rel
+from oracle import csmom_oracle as O
+
+pytestmark = pytest.mark.gpu
+REL = 1e-10
+
+
+def _up(x, dev="cuda:0"):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def fixed_ids(x):
+    """NumPy restatement of csm_fid: bucket of fl(1 + x) at 2048 per octave over [1/4, 4),
+    clamped to [0, 8191]; NaN -> 0xFFFF."""
+    x = np.asarray(x, dtype=np.float64)
+    with np.errstate(invalid="ignore", over="ignore"):
+        y = 1.0 + x
+    b = y.view(np.int64) >> 41
+    k = np.clip(b - (np.float64(0.25).view(np.int64) >> 41), 0, 8191)
+    return np.where(np.isnan(x), 0xFFFF, k).astype(np.uint16)
+
+
+def _oracle_labels(row, n_bins=10):
+    ok = ~np.isnan(row)
+    out = np.full(len(row), -1, dtype=np.int8)
+    if ok.any():
+        lab = O.qcut_labels(row[ok], n_bins)
+        out[ok] = np.where(np.isnan(lab), -1, lab).astype(np.int8)
+    return out
+
+
+def _ids_dev(x):
+    return _up(fixed_ids(x).view(np.int16))
+
+
+def test_fixed_map_is_monotone():
+    """Host check of the map the kernels share: non-decreasing over a sorted sweep that
+    crosses both clamps, every octave boundary and +-0.0."""
+    xs = np.sort(np.concatenate([
+        np.linspace(-5, 10, 200_001), -np.logspace(-300, 300, 2001), np.logspace(-300, 300, 2001),
+        [-np.inf, np.inf, -0.75, -0.5, 0.0, -0.0, 1.0, 3.0, np.nextafter(-0.75, 0), np.nextafter(3.0, 4)]]))
+    ids = fixed_ids(xs).astype(np.int64)
+    assert (np.diff(ids) >= 0).all()
+    assert ids[0] == 0 and ids[-1] == 8191
+    assert fixed_ids(np.array([np.nan]))[0] == 0xFFFF
+
+
+def _panel(N=20_000, T=900, seed=11):
+    from oracle.synth_np import make_panel
+    return make_panel(N, T, seed=seed, start="2001-01-02", with_volume=False, nan_day=0.02,
+                      absent_month=0.01, nan_month=0.01, cents=True)
+
+
+def test_signal_ids_equal_fixed_map_of_mom(engine):
+    pan = _panel()
+    ms_h = pan["month_start"]
+    maxd = int(np.diff(ms_h).max())
+    P, ms = _up(pan["P"]), _up(ms_h)
+    PM, R, M, NR, IDS = engine.signal_ids(P, ms, maxd, 12, 1, with_pm=True, with_ret=True)
+    base = engine.signal(P, ms, maxd, 12, 1, with_pm=True, with_ret=True)
+    for a, b in zip((PM, R, M, NR), base):
+        assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+    m = M.cpu().numpy()
+    assert np.array_equal(IDS.cpu().numpy().view(np.uint16), fixed_ids(m))
+
+
+@pytest.mark.parametrize("J,skip", [(12, 1), (3, 0), (1, 1), (24, 2)])
+def test_pipeline_vs_oracle(engine, J, skip):
+    """csm_pipeline (one C call) on a 20,000-asset daily panel against the oracle."""
+    pan = _panel(seed=7 + J)
+    ms_h = pan["month_start"]
+    out = engine.pipeline(_up(pan["P"]), _up(ms_h), J, skip, 10, with_ret=True)
+    ref = O.pipeline(pan["P"], ms_h, J, skip, 10)
+    for k in ("PM", "R", "M", "NR"):
+        assert bits_equal(getattr(out, k).cpu().numpy(), ref[k]), k
+    assert np.array_equal(out.L.cpu().numpy(), ref["L"])
+    assert np.array_equal(out.CNT.cpu().numpy(), ref["CNT"])
+    ew, ls = out.EW.cpu().numpy(), out.LS.cpu().numpy()
+    assert np.array_equal(np.isnan(ew), np.isnan(ref["EW"])) and max_rel(ew, ref["EW"]) <= REL
+    assert np.array_equal(np.isnan(ls), np.isnan(ref["LS"])) and max_rel(ls, ref["LS"]) <= REL
+
+
+def test_pipeline_equals_stagewise_default_path(engine):
+    """The id pipeline and the default signal -> deciles -> long_short agree: labels, counts
+    and ranked rows bit for bit, means within 1e-13."""
+    pan = _panel(N=24_000, T=700, seed=3)
+    ms_h = pan["month_start"]
+    maxd = int(np.diff(ms_h).max())
+    P, ms = _up(pan["P"]), _up(ms_h)
+    out = engine.pipeline(P, ms, 12, 1, 10)
+    _, _, M, NR = engine.signal(P, ms, maxd, 12, 1)
+    L, EW, CNT, NV = engine.deciles(M, NR, 10, with_nv=True)
+    assert torch.equal(out.L, L) and torch.equal(out.CNT, CNT) and torch.equal(out.NV, NV)
+    a, b = out.EW.cpu().numpy(), EW.cpu().numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b)) and max_rel(a, b) <= 1e-13
+
+
+STRESS = ["outlier", "ties", "twoval", "dense_center", "huge_range", "neg_zero", "lognormal",
+          "pareto", "all_equal", "single", "empty", "one_bucket_tail", "clamped_low"]
+
+
+def _stress_row(case, n=200_000):
+    rng = np.random.default_rng(abs(hash(case)) % 2**32)
+    if case == "outlier":
+        x = rng.normal(0, 1e-3, n); x[7] = 1e6
+    elif case == "ties":
+        x = rng.integers(0, 5, n).astype(float)
+    elif case == "twoval":
+        x = np.where(rng.random(n) < 0.95, 0.1, 0.2)
+    elif case == "dense_center":     # every value in one fixed-map bucket: key refinement
+        x = np.concatenate([rng.normal(0, 1e-9, n - 10), rng.normal(0, 1e3, 10)])
+    elif case == "huge_range":
+        x = rng.normal(0, 1, n) * 10.0 ** rng.integers(-300, 300, n)
+    elif case == "neg_zero":
+        x = rng.choice(np.array([-0.0, 0.0, 1.0, -1.0, 2.0]), n)
+    elif case == "lognormal":
+        x = np.exp(rng.normal(0, 3, n)) - 1.0
+    elif case == "pareto":
+        x = rng.pareto(0.7, n) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    elif case == "all_equal":
+        x = np.full(n, 0.37)
+    elif case == "single":
+        x = np.full(n, np.nan); x[12345] = 0.5
+        return x
+    elif case == "empty":
+        return np.full(n, np.nan)
+    elif case == "one_bucket_tail":  # most of the row above the top clamp (x >= 3)
+        x = 3.0 + rng.exponential(1.0, n); x[:1000] = rng.normal(0, 0.1, 1000)
+    else:                            # clamped_low: most of the row below -3/4
+        x = -0.75 - rng.random(n) * 0.25; x[:500] = rng.normal(0.1, 0.2, 500)
+    x[rng.random(n) < 0.05] = np.nan
+    return x
+
+
+@pytest.mark.parametrize("case", STRESS)
+def test_deciles_ids_stress(engine, case):
+    x = _stress_row(case)
+    M = _up(x[None, :])
+    L, _, _, NV = engine.deciles_ids(M, None, _ids_dev(x[None, :]), 10, with_nv=True)
+    assert np.array_equal(L.cpu().numpy()[0], _oracle_labels(x)), case
+    assert int(NV.cpu()[0]) == int((~np.isnan(x)).sum())
+
+
+@pytest.mark.parametrize("n_bins", [2, 3, 4, 5, 10, 20])
+def test_deciles_ids_nbins_with_means(engine, n_bins):
+    pan = _panel(N=20_000, T=520, seed=n_bins)
+    ms_h = pan["month_start"]
+    P, ms = _up(pan["P"]), _up(ms_h)
+    _, _, M, NR, IDS = engine.signal_ids(P, ms, int(np.diff(ms_h).max()), 6, 1)
+    L, EW, CNT, NV = engine.deciles_ids(M, NR, IDS, n_bins, with_nv=True)
+    m, nr = M.cpu().numpy(), NR.cpu().numpy()
+    refL = O.assign_deciles(m, n_bins)
+    assert np.array_equal(L.cpu().numpy(), refL)
+    rEW, rCNT, _ = O.portfolio_ew(refL, nr, n_bins)
+    assert np.array_equal(CNT.cpu().numpy(), rCNT)
+    assert max_rel(EW.cpu().numpy(), rEW) <= REL
+
+
+def test_deciles_ids_rejects_bad_layout(engine):
+    import csmom
+    M = torch.zeros((2, 18), dtype=torch.float64, device="cuda:0")   # N % 4 != 0
+    ids = torch.zeros((2, 18), dtype=torch.int16, device="cuda:0")
+    with pytest.raises(csmom.CsmError):
+        engine.deciles_ids(M, None, ids, 10)
+
+
+def test_pipeline_narrow_rows_fall_back(engine):
+    """Rows at or below the narrow-row width (and N % 4 != 0) take signal + deciles without ids:
+    same results as the stage-wise calls."""
+    z = load_golden("edge")
+    for P_h in (z["P"], z["P"][:, :-2]):
+        ms_h = z["month_start"].astype(np.int64)
+        out = engine.pipeline(_up(P_h), _up(ms_h), 12, 1, 10)
+        ref = O.pipeline(P_h, ms_h, 12, 1, 10)
+        assert np.array_equal(out.L.cpu().numpy(), ref["L"])
+        assert max_rel(out.LS.cpu().numpy(), ref["LS"]) <= REL

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     raw = ctypes.CDLL(str(csmom.lib_path()))
     for s in header_symbols():
         assert hasattr(raw, s), s
-    assert lib.csm_abi_version() == 1
+    assert lib.csm_abi_version() == 2
 
 
 def test_null_context_is_inval():
