@@ -239,6 +239,71 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
   return mom;
 }
 
+// scan_step for two adjacent assets a0, a0 + 1 (a0 even) with their stores paired: mom_J
+// (and ret_1m) as one 16-B store per row, next_ret as one 16-B store when both assets write
+// the same row (the steady state), so a wave issues half the store instructions.  Same
+// arithmetic in the same order as two scan_step calls: bit-identical outputs.
+__device__ __forceinline__ void scan_step_pair(ScanLane (&s)[2], const double (&x)[2], int m,
+                                               double* ring0, int RS, int W, int J, int64_t N,
+                                               int64_t a0, double* __restrict__ R,
+                                               double* __restrict__ M, double* __restrict__ NR,
+                                               double (&mom)[2]) {
+  const double NaN = qnan();
+  double ret[2];
+  int wp[2];          // next_ret row of the pending ranked row (-1: none)
+  double vp[2];
+  bool wc[2];         // NaN next_ret at row m
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    double* ring = ring0 + c;
+    wp[c] = -1;
+    vp[c] = NaN;
+    if (is_absent(x[c])) {
+      ret[c] = NaN; mom[c] = NaN; wc[c] = true;
+      continue;
+    }
+    const bool xv = !isnan_d(x[c]);
+    const double pnew = xv ? x[c] : s[c].pff;
+    ret[c] = pnew / s[c].pff - 1.0;
+    s[c].pff = pnew;
+    ring[s[c].head * RS] = 1.0 + ret[c];
+    s[c].head = (s[c].head + 1 == W) ? 0 : s[c].head + 1;
+    double acc = ring[s[c].head * RS];
+    int idx = s[c].head;
+    for (int k = 1; k < J; ++k) {
+      idx = (idx + 1 == W) ? 0 : idx + 1;
+      acc = acc * ring[idx * RS];
+    }
+    mom[c] = acc - 1.0;
+    const bool ranked = !isnan_d(mom[c]);
+    const double ps_new = xv ? x[c] : s[c].psff;
+    if (s[c].prev >= 0) { wp[c] = s[c].prev; vp[c] = ps_new / s[c].psff - 1.0; }
+    if (ranked) {
+      s[c].psff = ps_new;
+      s[c].prev = m;
+      wc[c] = false;
+    } else {
+      s[c].prev = -1;
+      wc[c] = true;
+    }
+  }
+  const int64_t o = (int64_t)m * N + a0;
+  if (R) *reinterpret_cast<double2*>(R + o) = make_double2(ret[0], ret[1]);
+  *reinterpret_cast<double2*>(M + o) = make_double2(mom[0], mom[1]);
+  if (wp[0] >= 0 && wp[0] == wp[1]) {
+    *reinterpret_cast<double2*>(NR + (int64_t)wp[0] * N + a0) = make_double2(vp[0], vp[1]);
+  } else {
+    if (wp[0] >= 0) NR[(int64_t)wp[0] * N + a0] = vp[0];
+    if (wp[1] >= 0) NR[(int64_t)wp[1] * N + a0 + 1] = vp[1];
+  }
+  if (wc[0] && wc[1]) {
+    *reinterpret_cast<double2*>(NR + o) = make_double2(NaN, NaN);
+  } else {
+    if (wc[0]) NR[o] = NaN;
+    if (wc[1]) NR[o + 1] = NaN;
+  }
+}
+
 __device__ __forceinline__ void scan_finish(ScanLane& s, double* ring, int RS, int W, int64_t N,
                                             int64_t a, double* __restrict__ NR,
                                             const double* __restrict__ next_pm,
@@ -531,12 +596,13 @@ __device__ __forceinline__ bool shard_pm_kept(int m, int T_m, int W) {
 // price, and the first / last present month (-1 none) -- for k_shard_summary_state and
 // k_shard_repair.
 template <int MAXD, int VEC, int NBUF, bool TILED = false, int ST = 0, int BW = 1,
-          bool SH = false>
+          bool SH = false, bool PS = true>
 __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS) {
+    double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS, int* __restrict__ tick,
+    int lag) {
   static_assert(!TILED || BW == 1, "tiled panels are read one tile per wave");
   typedef typename RowT<VEC>::T VT;
   extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC * BW]
@@ -598,9 +664,15 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
         else PMo[(int64_t)m * N + a0] = pm[0];
       }
       double mom[VEC];
+      if constexpr (VEC == 2 && ST == 0 && PS) {   // paired 16-B stores (R / M / NR are 16-B aligned)
+        scan_step_pair(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
+                       m, ring_lds + VEC * tid, RS, W, J, N, a0, R, M, NR,
+                       reinterpret_cast<double (&)[2]>(mom));
+      } else {
 #pragma unroll
-      for (int c = 0; c < VEC; ++c)
-        mom[c] = scan_step<ST>(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
+        for (int c = 0; c < VEC; ++c)
+          mom[c] = scan_step<ST>(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
+      }
       if (IDS) {   // fixed-map bucket ids for the decile pass (csm_signal_ids)
         if (VEC == 2)
           *reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0) = csm_fid(mom[0]) | (csm_fid(mom[VEC - 1]) << 16);
@@ -630,6 +702,15 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
     load_month(B, 1);
     load_month(C, 2);
     for (int m = 0; m < T_m; m += 4) {
+      // experiment (csm_tune "signal_sync" = lag): pace the waves so none runs more than lag
+      // 4-month steps ahead of the slowest (a bounded wait: the pacing only shapes the access
+      // stream, never the results)
+      if (tick && lag > 0 && (m >> 2) >= lag && threadIdx.x == 0) {
+        int guard = 0;
+        while (__hip_atomic_load(tick + (m >> 2) - lag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                   (int)gridDim.x && ++guard < 4000)
+          __builtin_amdgcn_s_sleep(2);
+      }
       load_month(D, m + 3);
       if (BW > 1) __syncthreads();
       process(A, m);
@@ -639,6 +720,7 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
       if (m + 2 < T_m) process(C, m + 2);
       load_month(C, m + 6);
       if (m + 3 < T_m) process(D, m + 3);
+      if (tick && lag > 0 && threadIdx.x == 0) atomicAdd(tick + (m >> 2), 1);
     }
   }
   if (live) {
@@ -1262,6 +1344,8 @@ static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<..,
 static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
 static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
 static int g_tune_month_end_rows = 0;
+static int g_tune_signal_pair = 1;
+static int g_tune_signal_sync = 0;     // experiment: >0 paces k_signal's waves to this many 4-month steps     // k_signal paired 16-B output stores (VEC 2): 1 on, 0 off
 static int64_t* g_dec_timing = nullptr;
 // k_deciles bucket-id scratch path (N % 4 == 0): 1 on, 0 off.  Off by default: it moves
 // fewer bytes but measured slower at C4 (0.44 vs 0.40 ms, profiles/r01/experiments).
@@ -1296,6 +1380,8 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
   if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
+  if (!strcmp(key, "signal_pair") && (value == 0 || value == 1)) { g_tune_signal_pair = value; return CSM_OK; }
+  if (!strcmp(key, "signal_sync") && value >= 0 && value <= 64) { g_tune_signal_sync = value; return CSM_OK; }
   if (!strcmp(key, "signal_mw") && (value == 0 || value == 21 || value == 22 || value == 41 ||
                                     value == 42)) { g_tune_signal_mw = value; return CSM_OK; }
   return CSM_E_INVAL;
@@ -1324,9 +1410,10 @@ int csm_create(int device, csm_ctx** out) {
 }
 
 int csm_destroy(csm_ctx* ctx) {
-  if (ctx && ctx->scratch) {
+  if (ctx && (ctx->scratch || ctx->aux)) {
     (void)hipSetDevice(ctx->device);
-    (void)hipFree(ctx->scratch);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->aux) (void)hipFree(ctx->aux);
   }
   free(ctx);
   return CSM_OK;
@@ -1461,7 +1548,8 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     return set_err(ctx, CSM_E_INVAL, "%s: the tiled panel needs even N and 16-B aligned buffers", who);
   if (T_m == 0) return CSM_OK;
   const int W = J + skip;
-  const bool can2 = (N % 2 == 0) && aligned16(P) && (!PM || aligned16(PM));
+  const bool can2 = (N % 2 == 0) && aligned16(P) && (!PM || aligned16(PM)) && aligned16(M) &&
+                    aligned16(NR) && (!R || aligned16(R));
   if (!tiled && can2 && g_tune_signal_mw != 0 && !sh && !ids) {
     const int nw = g_tune_signal_mw / 10, nb = g_tune_signal_mw % 10;
     const void* fm = nullptr;
@@ -1509,6 +1597,8 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     fn = (const void*)k_signal<24, 2, 4, false, 1>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 2)
     fn = (const void*)k_signal<24, 2, 4, false, 2>;
+  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_pair == 0)
+    fn = (const void*)k_signal<24, 2, 4, false, 0, 1, false, false>;
   else if (max_month_days <= 24)
     fn = vec == 2 ? (nbuf == 3 ? SIG(24, 2, 3) : SIG(24, 2, 4)) : (nbuf == 3 ? SIG(24, 1, 3) : SIG(24, 1, 4));
   else
@@ -1520,9 +1610,23 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   {
     int T_m_ = T_m, J_ = J, skip_ = skip;
     int64_t N_ = N, T_d_ = T_d;
+    int* tick = nullptr;
+    int lag = g_tune_signal_sync;
+    if (lag > 0 && !sh && nbuf == 4) {   // pacing experiment: one arrival counter per 4 months
+      const size_t need = (size_t)(T_m / 4 + 2) * sizeof(int);
+      if (ctx->aux_bytes < need) {
+        if (ctx->aux) HIP_CHECK(ctx, hipFree(ctx->aux));
+        ctx->aux = nullptr;
+        ctx->aux_bytes = 0;
+        HIP_CHECK(ctx, hipMalloc(&ctx->aux, need));
+        ctx->aux_bytes = need;
+      }
+      tick = (int*)ctx->aux;
+      HIP_CHECK(ctx, hipMemsetAsync(tick, 0, need, ctx->stream));
+    }
     void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
                     (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out, &T_d_,
-                    (void*)&ids};
+                    (void*)&ids, (void*)&tick, &lag};
     HIP_CHECK(ctx, hipLaunchKernel(fn, dim3(blocks), dim3(64 * bw), args, lds, ctx->stream));
   }
   LAUNCH_CHECK(ctx, who);

@@ -33,16 +33,19 @@ def month_partition(T_m: int, G: int):
 
 
 def all_gather_stack(x: torch.Tensor, group=None) -> torch.Tensor:
-    """[G, *x.shape] all-gather; RCCL gets the single-buffer form, gloo the list form."""
+    """[G, *x.shape] all-gather; RCCL gets the single-buffer form, gloo the list form (device
+    tensors staged through host memory: gloo's all-gather is host-only)."""
     G = dist.get_world_size(group)
     if G == 1:
         return x.unsqueeze(0)
-    out = torch.empty((G,) + tuple(x.shape), dtype=x.dtype, device=x.device)
     if dist.get_backend(group) == "nccl":
+        out = torch.empty((G,) + tuple(x.shape), dtype=x.dtype, device=x.device)
         dist.all_gather_into_tensor(out.view(-1), x.contiguous().view(-1), group=group)
-    else:
-        dist.all_gather(list(out.unbind(0)), x.contiguous(), group=group)
-    return out
+        return out
+    xs = x.detach().contiguous().cpu()
+    out = torch.empty((G,) + tuple(x.shape), dtype=x.dtype)
+    dist.all_gather(list(out.unbind(0)), xs, group=group)
+    return out.to(x.device)
 
 
 @dataclass

@@ -13,7 +13,7 @@ import csmom  # noqa: E402
 from csmom.synth import bday_calendar, make_device_panel  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
-IDS = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+IDS = int(sys.argv[2]) if len(sys.argv) > 2 else 0   # 2: fixed-map ids from csm_signal_ids
 REG = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 ABL = int(sys.argv[4]) if len(sys.argv) > 4 else 0   # dec_ablate bitmask (1: no decile sums)
 ROWS = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # >0: time only the first ROWS dates
@@ -26,20 +26,28 @@ maxd = int(np.diff(ms).max())
 M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
 L = eng.empty((T_m, N), torch.int8)
 EW, CNT = eng.empty((T_m, 10)), eng.empty((T_m, 10), torch.int32)
-eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
-eng.lib.csm_tune(b"dec_ids", IDS)
+IDB = eng.empty((T_m, N), torch.int16)
+eng.signal_ids(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR, IDB))
+eng.lib.csm_tune(b"dec_ids", 1 if IDS == 1 else 0)
 eng.lib.csm_tune(b"dec_reg", REG)
 eng.lib.csm_tune(b"dec_ablate", ABL)
 if ROWS:
-    M, NR, L, EW, CNT = M[:ROWS], NR[:ROWS], L[:ROWS], EW[:ROWS], CNT[:ROWS]
+    M, NR, L, EW, CNT, IDB = M[:ROWS], NR[:ROWS], L[:ROWS], EW[:ROWS], CNT[:ROWS], IDB[:ROWS]
     T_m = ROWS
+def dec():
+    if IDS == 2:
+        eng.deciles_ids(M, NR, IDB, 10, out=(L, EW, CNT, None))
+    else:
+        eng.deciles(M, NR, 10, out=(L, EW, CNT, None))
+
+
 for _ in range(3):
-    eng.deciles(M, NR, 10, out=(L, EW, CNT, None))
+    dec()
 tim = torch.full((T_m, 9), -1, dtype=torch.int64, device="cuda:0")
 eng.lib.csm_tune_ptr(b"dec_timing", ctypes.c_void_p(tim.data_ptr()))
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
-eng.deciles(M, NR, 10, out=(L, EW, CNT, None))
+dec()
 e1.record()
 torch.cuda.synchronize()
 eng.lib.csm_tune_ptr(b"dec_timing", None)

@@ -1,0 +1,67 @@
+"""Round-2 A/B of the fused signal kernel on C4, interleaved in one process (median of 5
+rounds): paired 16-B output stores vs per-asset 8-B stores, with / without the bucket-id
+output, store ablation (reads only), 3 vs 4 month buffers; checks the variants' outputs are
+bit-identical.  Dev tool: prints one JSON line."""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import csmom  # noqa: E402
+from csmom.synth import bday_calendar, make_device_panel  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+TD = 10_000
+days, ms, _ = bday_calendar("1985-01-01", TD)
+pan = make_device_panel(N, days, ms, seed=4000, device="cuda:0", shard=(0, 1, 4, float(TD)))
+eng = csmom.Engine(0)
+T_m = len(ms) - 1
+maxd = int(np.diff(ms).max())
+tune = lambda k, v: eng.lib.csm_tune(k.encode(), v)
+outs = {}
+
+
+def timed(fn):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(); fn(); b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b)
+
+
+def run(name):
+    M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
+    IDS = eng.empty((T_m, N), torch.int16)
+    pair = 0 if name.startswith("nopair") else 1
+    tune("signal_pair", pair)
+    tune("signal_store", 2 if name == "nostore" else 0)
+    tune("signal_nbuf", 3 if name.endswith("nbuf3") else 4)
+    tune("signal_sync", int(name.split("sync")[1]) if "sync" in name else 0)
+    if "ids" in name:
+        f = lambda: eng.signal_ids(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR, IDS))
+    else:
+        f = lambda: eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
+    t = timed(f)
+    outs[name] = (M, NR)
+    return t
+
+
+names = (sys.argv[2].split(",") if len(sys.argv) > 2 else
+         ["pair_ids", "pair", "nopair_ids", "nopair", "nostore", "pair_ids_nbuf3"])
+times = {n: [] for n in names}
+for rnd in range(6):
+    for n in names:
+        t = run(n)
+        if rnd:
+            times[n].append(t)
+for k, v in (("signal_pair", 1), ("signal_store", 0), ("signal_nbuf", 4), ("signal_sync", 0)):
+    tune(k, v)
+eq = lambda a, b: bool(torch.equal(a.view(torch.int64), b.view(torch.int64)))
+base = outs["nopair" if "nopair" in outs else names[0]]
+same = {n: eq(outs[n][0], base[0]) and eq(outs[n][1], base[1]) for n in names if n != "nostore"}
+alg = 8.0 * N * TD + 16.0 * N * T_m
+res = {n: round(float(np.median(t)), 4) for n, t in times.items()}
+print(json.dumps({"N": N, "T_d": TD, "k_signal_ms": res,
+                  "GBps": {n: round(alg / (v * 1e-3) / 1e9, 1) for n, v in res.items()},
+                  "bits_equal_to_nopair": same}), flush=True)

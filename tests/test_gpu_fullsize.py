@@ -1,0 +1,196 @@
+"""GPU parity at the BASELINE configs' workload sizes (C3, C4, C5), the bench's own layouts.
+
+C4: the 100,000-asset x 10,000-day panel is generated in HBM exactly as bench.py does and run
+through the benchmarked path (csm_pipeline: fused signal with bucket ids -> labels + decile
+means -> long-short).  The scan is per asset, so a column subset checked against the oracle
+is exact for those columns: month prices, mom_J and next_ret bit for bit on 2,048 columns;
+labels on EVERY date (all 461) are the oracle's qcut of the engine's mom_J; counts exact and
+decile means / long-short within 1e-10 of the oracle's portfolio on the engine's next_ret.
+C3: the 5,000 x 6,522-day value-weighted 16-strategy grid with square-root-impact costs, every
+(J, K), against the portfolio oracle (rules E1-E5).  C5: SweepRunner.run_bootstrap at the
+bench's layout (5,000 assets, 300 months, one batch of 100 panels, 16 strategies, turnover +
+spread costs); sampled panels' summary rows against the oracle stages.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits_equal, max_rel
+from oracle import csmom_oracle as O
+from oracle import portfolio_oracle as PO
+
+pytestmark = pytest.mark.gpu
+REL = 1e-10
+
+
+def _labels_ref(rows, n_bins=10):
+    out = np.full(rows.shape, -1, dtype=np.int8)
+    for t, row in enumerate(rows):
+        v = ~np.isnan(row)
+        if v.any():
+            lab = O.qcut_labels(row[v], n_bins)
+            out[t, v] = np.where(np.isnan(lab), -1, lab).astype(np.int8)
+    return out
+
+
+@pytest.fixture(scope="module")
+def c4(engine):
+    import csmom  # noqa: F401
+    from csmom.synth import bday_calendar, make_device_panel
+    N, T_d = 100_000, 10_000
+    days, ms_h, _ = bday_calendar("1985-01-01", T_d)
+    pan = make_device_panel(N, days, ms_h, seed=4 * 1000, device="cuda:0",
+                            shard=(0, 1, 4, float(T_d)))          # bench.py's N = 1 panel
+    out = engine.pipeline(pan.P, pan.month_start, 12, 1, 10, with_pm=True)
+    torch.cuda.synchronize()
+    return N, T_d, ms_h, pan, out
+
+
+def test_c4_columns_bit_exact(c4):
+    N, T_d, ms_h, pan, out = c4
+    cols = np.unique(np.concatenate([np.arange(0, 64), np.arange(N - 64, N),
+                                     np.random.default_rng(44).choice(N, 1920, replace=False)]))
+    assert len(cols) >= 2000
+    ci = torch.from_numpy(cols).to(pan.P.device)
+    P_h = pan.P.index_select(1, ci).cpu().numpy()
+    PM_r, _ = O.month_end(P_h, ms_h)
+    _, M_r, NR_r, _ = O.momentum_scan(PM_r, 12, 1)
+    assert bits_equal(out.PM.index_select(1, ci).cpu().numpy(), PM_r)
+    assert bits_equal(out.M.index_select(1, ci).cpu().numpy(), M_r)
+    assert bits_equal(out.NR.index_select(1, ci).cpu().numpy(), NR_r)
+
+
+def test_c4_labels_every_date_and_means(c4):
+    N, T_d, ms_h, pan, out = c4
+    M_h, NR_h = out.M.cpu().numpy(), out.NR.cpu().numpy()
+    T_m = M_h.shape[0]
+    assert T_m == 461
+    L_ref = _labels_ref(M_h)
+    L_h = out.L.cpu().numpy()
+    bad = np.nonzero((L_h != L_ref).any(axis=1))[0]
+    assert len(bad) == 0, f"label mismatch on dates {bad[:10]}"
+    assert np.array_equal(out.NV.cpu().numpy(), (~np.isnan(M_h)).sum(axis=1))
+    EW_r, CNT_r, LS_r = O.portfolio_ew(L_ref, NR_h, 10)
+    assert np.array_equal(out.CNT.cpu().numpy(), CNT_r)
+    ew, ls = out.EW.cpu().numpy(), out.LS.cpu().numpy()
+    assert np.array_equal(np.isnan(ew), np.isnan(EW_r)) and max_rel(ew, EW_r) <= REL
+    assert np.array_equal(np.isnan(ls), np.isnan(LS_r)) and max_rel(ls, LS_r) <= REL
+
+
+def test_c4_default_decile_kernel_agrees(engine, c4):
+    """The streaming decile kernel (no ids) on the same mom_J: identical labels and counts."""
+    N, T_d, ms_h, pan, out = c4
+    L, EW, CNT, NV = engine.deciles(out.M, out.NR, 10, with_nv=True)
+    assert torch.equal(L, out.L) and torch.equal(CNT, out.CNT) and torch.equal(NV, out.NV)
+    a, b = EW.cpu().numpy(), out.EW.cpu().numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b)) and max_rel(a, b) <= 1e-13
+
+
+# ------------------------------------------------------------------------------------ C3
+@pytest.fixture(scope="module")
+def c3(engine):
+    from csmom.synth import bday_calendar, make_device_panel
+    N, T_d = 5_000, 6_522
+    days, ms_h, _ = bday_calendar("2000-01-03", T_d)
+    seed = 4 * 1000 + 3
+    pan = make_device_panel(N, days, ms_h, seed=seed, device="cuda:0")
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(seed)
+    shares = torch.exp(torch.randn(N, generator=g, device="cuda:0", dtype=torch.float64) + 16.0)
+    turn = torch.rand(N, generator=g, device="cuda:0", dtype=torch.float64) * 0.018 + 0.002
+    PM, _ = engine.month_end(pan.P, pan.month_start)
+    W = PM.abs() * shares
+    ADV = W * turn
+    return PM, W, ADV
+
+
+@pytest.mark.parametrize("J", [3, 6, 9, 12])
+def test_c3_value_weighted_grid_with_impact_costs(engine, c3, J):
+    import csmom
+    PM, W, ADV = c3
+    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    _, M, NR = engine.momentum(PM, J, 1)
+    L, _, _, _ = engine.deciles(M, None, 10)
+    PM_h, W_h, ADV_h = PM.cpu().numpy(), W.cpu().numpy(), ADV.cpu().numpy()
+    _, M_r, NR_r, _ = O.momentum_scan(PM_h, J, 1)
+    assert bits_equal(M.cpu().numpy(), M_r) and bits_equal(NR.cpu().numpy(), NR_r)
+    L_r = O.assign_deciles(M_r, 10)
+    assert np.array_equal(L.cpu().numpy(), L_r)
+    outs = engine.portfolio_multi(L, NR, 10, Ks=cfg.Ks, W=W, half_spread=cfg.half_spread,
+                                  k_impact=cfg.k_impact, aum=cfg.aum, ADV=ADV)
+    for K in cfg.Ks:
+        ref = PO.portfolio(L_r, NR_r, 10, K=K, W=W_h, half_spread=cfg.half_spread,
+                           k_impact=cfg.k_impact, aum=cfg.aum, ADV=ADV_h)
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            g = getattr(outs[K], f).cpu().numpy().reshape(ref[f].shape)
+            assert np.array_equal(np.isnan(g), np.isnan(ref[f])), (J, K, f)
+            assert max_rel(g, ref[f]) <= REL, (J, K, f, max_rel(g, ref[f]))
+
+
+def test_c3_sweep_runner_summary(engine, c3):
+    """The bench's C3 step (SweepRunner.run_batch with value weights and ADV) gives the summary
+    rows of the per-(J, K) device portfolios."""
+    import csmom
+    PM, W, ADV = c3
+    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    summ, series = csmom.SweepRunner(engine, cfg).run_batch(PM, 1, W=W, ADV=ADV)
+    assert tuple(summ.shape) == (1, 16, 7)
+    for s, (J, K) in enumerate(cfg.strategies):
+        o = series[(J, K)]
+        one = engine.summary(o.LS, o.TURN, o.COST, o.NET)[0, 0]
+        assert bits_equal(summ[0, s].cpu().numpy(), one.cpu().numpy()), (J, K)
+
+
+# ------------------------------------------------------------------------------------ C5
+@pytest.fixture(scope="module")
+def c5(engine):
+    import csmom
+    from csmom.synth import bday_calendar, make_device_panel
+    N, T_d = 5_000, 6_522
+    days, ms_h, _ = bday_calendar("2000-01-03", T_d)
+    pan = make_device_panel(N, days, ms_h, seed=4 * 1000 + 5, device="cuda:0")
+    PM0, _ = engine.month_end(pan.P, pan.month_start)
+    R0, _, _ = engine.momentum(PM0, 12, 1, with_ret=True)
+    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    summ = csmom.SweepRunner(engine, cfg).run_bootstrap(R0, 100, seed=5000, mean_block=6.0,
+                                                         batch=100)
+    torch.cuda.synchronize()
+    return cfg, R0.cpu().numpy(), summ.cpu().numpy()
+
+
+def _oracle_panel_summary(cfg, R_h, b):
+    T_m, N = R_h.shape
+    src = PO.bootstrap_indices(T_m, 1, 5000, 6.0, b0=b)
+    pm = PO.bootstrap_panel(R_h, src).reshape(T_m, N)
+    rows = []
+    for J in cfg.Js:
+        _, M, NR, _ = O.momentum_scan(pm, J, cfg.skip)
+        L = O.assign_deciles(M, cfg.n_bins)
+        for K in cfg.Ks:
+            r = PO.portfolio(L, NR, cfg.n_bins, K=K, half_spread=cfg.half_spread,
+                             k_impact=cfg.k_impact, aum=cfg.aum)
+            x = lambda f: r[f].reshape(1, T_m, 1)
+            rows.append(_summary_rows(x("LS"), x("TURN"), x("COST"), x("NET"))[0, 0])
+    return np.stack(rows)
+
+
+def _summary_rows(LS, TURN, COST, NET, freq=12.0):
+    from test_gpu_portfolio import _summary_ref
+    return _summary_ref(LS, TURN, COST, NET, freq)
+
+
+def test_c5_shape_and_finite(c5):
+    cfg, R_h, summ = c5
+    assert summ.shape == (100, 16, 7)
+    assert np.isfinite(summ[..., :3]).all()
+
+
+@pytest.mark.parametrize("b", [0, 57, 99])
+def test_c5_sampled_panels_vs_oracle(c5, b):
+    cfg, R_h, summ = c5
+    ref = _oracle_panel_summary(cfg, R_h, b)
+    got = summ[b]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(got[:, 0], ref[:, 0])                 # months per strategy
+    m = ~np.isnan(ref)
+    assert np.allclose(got[m], ref[m], rtol=1e-9, atol=1e-13), b
