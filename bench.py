@@ -173,6 +173,7 @@ def main():
     J, skip, nb = 12, 1, 10
     # preallocated outputs: the timed loop performs no allocation
     max_days = int(np.diff(ms_host).max())
+    min_days = int(np.diff(ms_host)[1:-1].min()) if len(ms_host) > 3 else 1 << 30   # interior months
     fused = eng.use_fused(panel.P, None, max_days)
     pipe = (DateShardPipeline(eng, months, J, skip, nb,
                               fused=fused and args.shard_mode == "fused")
@@ -208,7 +209,7 @@ def main():
         ev[i].record()
         if use_ids:
             eng.signal_ids(panel.P, panel.month_start, max_days, J, skip,
-                           out=(None, None, M, NR, IDS))
+                           out=(None, None, M, NR, IDS), min_month_days=min_days)
         elif fused:
             eng.signal(panel.P, panel.month_start, max_days, J, skip, out=(None, None, M, NR))
         else:

@@ -103,11 +103,11 @@ def _declare(lib):
                                             _p, _p, _p, _p]),
         "csm_shard_summary_state": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p,
                                                    _p]),
-        "csm_signal_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p,
-                                          _p, _p, _p]),
+        "csm_signal_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _p,
+                                          _p, _p, _p, _p]),
         "csm_deciles_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
-        "csm_pipeline": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _p,
-                                        _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+        "csm_pipeline": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _i32,
+                                        _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -28,8 +28,6 @@ struct csm_ctx {
   void* scratch;          // context-owned device workspace (k_deciles bucket ids), grown lazily
   size_t scratch_bytes;
   int n_cu;               // compute units of the device (decile kernel choice)
-  void* aux;              // small context-owned device buffer (pacing counters), grown lazily
-  size_t aux_bytes;
 };
 
 static inline int set_err(csm_ctx* c, int code, const char* fmt, ...) {

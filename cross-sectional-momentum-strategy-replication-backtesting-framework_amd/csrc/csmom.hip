@@ -601,8 +601,7 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS, int* __restrict__ tick,
-    int lag) {
+    double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS) {
   static_assert(!TILED || BW == 1, "tiled panels are read one tile per wave");
   typedef typename RowT<VEC>::T VT;
   extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC * BW]
@@ -702,15 +701,6 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
     load_month(B, 1);
     load_month(C, 2);
     for (int m = 0; m < T_m; m += 4) {
-      // experiment (csm_tune "signal_sync" = lag): pace the waves so none runs more than lag
-      // 4-month steps ahead of the slowest (a bounded wait: the pacing only shapes the access
-      // stream, never the results)
-      if (tick && lag > 0 && (m >> 2) >= lag && threadIdx.x == 0) {
-        int guard = 0;
-        while (__hip_atomic_load(tick + (m >> 2) - lag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                   (int)gridDim.x && ++guard < 4000)
-          __builtin_amdgcn_s_sleep(2);
-      }
       load_month(D, m + 3);
       if (BW > 1) __syncthreads();
       process(A, m);
@@ -720,7 +710,6 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
       if (m + 2 < T_m) process(C, m + 2);
       load_month(C, m + 6);
       if (m + 3 < T_m) process(D, m + 3);
-      if (tick && lag > 0 && threadIdx.x == 0) atomicAdd(tick + (m >> 2), 1);
     }
   }
   if (live) {
@@ -737,6 +726,116 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
         carry_out[4 * N + a0 + k] = (double)q[2 * RS];
       }
     }
+  }
+}
+
+// =====================================================================================
+// Kernel AB'' (fused, day batches): k_signal for the common case -- 16-B row loads (even N),
+// no carry, every month but the first and the last at least D days long (host-checked; the
+// end of the data closes a short last month) -- streaming the day rows in
+// fixed batches of D instead of one register buffer per month.  k_signal pads every month to
+// MAXD loads (re-loads of the last day: cache hits, but they take issue slots and a share of
+// the 63 loads a wave can have outstanding); here every load is a new day row, NB - 1
+// batches in flight.  A batch holds at most one month end (months are >= D days): the rows
+// before it finish the current month, the rows after it start the next one, both reduced
+// branch-free with per-row uniform selects.  Same per-month arithmetic and stores as
+// k_signal (scan_step_pair): bit-identical outputs.
+// =====================================================================================
+template <int D, int NB>
+__global__ __launch_bounds__(64) void k_signal_db(
+    const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
+    int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
+    double* __restrict__ NR, int64_t T_d, uint16_t* __restrict__ IDS) {
+  static_assert(NB == 4, "four batch buffers (three in flight)");
+  extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][128]
+  const int W = J + skip;
+  const int tid = threadIdx.x;
+  const int64_t a0 = ((int64_t)blockIdx.x * 64 + tid) * 2;
+  const bool live = a0 < N;
+  constexpr int RS = 128;
+  ScanLane sl[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) scan_init(sl[c], ring_lds + 2 * tid + c, RS, W, nullptr, N, a0 + c, live);
+  const double* base = P + (live ? a0 : 0);
+  // the month being reduced: last valid price, any row present, any valid price
+  double last[2] = {0.0, 0.0};
+  bool pp[2] = {false, false}, vv[2] = {false, false};
+  int m = 0;
+  int64_t mend = T_m > 0 ? month_start[1] : 0;   // first day after month m
+  auto load_batch = [&](double2 (&buf)[D], int64_t d0) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int64_t d = d0 + k < T_d ? d0 + k : T_d - 1;
+      buf[k] = *reinterpret_cast<const double2*>(base + d * N);
+    }
+  };
+  auto finish = [&]() {   // month m is complete: month price, scan, stores
+    double pm[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) pm[c] = pp[c] ? (vv[c] ? last[c] : qnan()) : absent_val();
+    if (live) {
+      const int64_t o = (int64_t)m * N + a0;
+      if (PMo) *reinterpret_cast<double2*>(PMo + o) = make_double2(pm[0], pm[1]);
+      double mom[2];
+      scan_step_pair(sl, pm, m, ring_lds + 2 * tid, RS, W, J, N, a0, R, M, NR, mom);
+      if (IDS) *reinterpret_cast<uint32_t*>(IDS + o) = csm_fid(mom[0]) | (csm_fid(mom[1]) << 16);
+    }
+    ++m;
+    mend = m < T_m ? month_start[m + 1] : INT64_MAX;
+  };
+  auto consume = [&](const double2 (&X)[D], int64_t d0) {
+    // rows [0, kb) belong to month m, rows [kb, D) to month m + 1 (kb == D: no month end here)
+    const int kb = (int)(mend - d0 < D ? mend - d0 : D);
+    double lB[2] = {0.0, 0.0};
+    bool pB[2] = {false, false}, vB[2] = {false, false};
+    // kb is wave-uniform: a scalar branch per row picks the accumulator (no per-row lane masks)
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      if (k < kb) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const double x = c == 0 ? X[k].x : X[k].y;
+          const bool ok = x == x;
+          pp[c] |= !is_absent(x);
+          vv[c] |= ok;
+          last[c] = ok ? x : last[c];
+        }
+      } else if (d0 + k < T_d) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const double x = c == 0 ? X[k].x : X[k].y;
+          const bool ok = x == x;
+          pB[c] |= !is_absent(x);
+          vB[c] |= ok;
+          lB[c] = ok ? x : lB[c];
+        }
+      }
+    }
+    if (kb < D || d0 + D == mend) {   // month m ends in this batch (wave-uniform)
+      finish();
+#pragma unroll
+      for (int c = 0; c < 2; ++c) { last[c] = lB[c]; pp[c] = pB[c]; vv[c] = vB[c]; }
+    }
+  };
+  double2 A[D], B[D], C[D], E[D];
+  load_batch(A, 0);
+  load_batch(B, D);
+  load_batch(C, 2 * D);
+  for (int64_t d0 = 0; d0 < T_d; d0 += 4 * D) {
+    load_batch(E, d0 + 3 * D);
+    consume(A, d0);
+    load_batch(A, d0 + 4 * D);
+    if (d0 + D < T_d) consume(B, d0 + D);
+    load_batch(B, d0 + 5 * D);
+    if (d0 + 2 * D < T_d) consume(C, d0 + 2 * D);
+    load_batch(C, d0 + 6 * D);
+    if (d0 + 3 * D < T_d) consume(E, d0 + 3 * D);
+  }
+  if (m < T_m) finish();   // a short last month that began in the batch where its predecessor ended
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      scan_finish(sl[c], ring_lds + 2 * tid + c, RS, W, N, a0 + c, NR, nullptr, nullptr);
   }
 }
 
@@ -1344,8 +1443,9 @@ static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<..,
 static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
 static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
 static int g_tune_month_end_rows = 0;
-static int g_tune_signal_pair = 1;
-static int g_tune_signal_sync = 0;     // experiment: >0 paces k_signal's waves to this many 4-month steps     // k_signal paired 16-B output stores (VEC 2): 1 on, 0 off
+static int g_tune_signal_pair = 1;     // k_signal paired 16-B output stores (VEC 2): 1 on, 0 off
+static int g_tune_signal_db = 0;       // k_signal_db day-batch rows (16 | 20 | 21), 0 off
+static int g_tune_signal_maxd23 = 1;   // k_signal month buffers of 23 day rows when months fit: 1.789 -> 1.744 ms at C4 (profiles/r02)
 static int64_t* g_dec_timing = nullptr;
 // k_deciles bucket-id scratch path (N % 4 == 0): 1 on, 0 off.  Off by default: it moves
 // fewer bytes but measured slower at C4 (0.44 vs 0.40 ms, profiles/r01/experiments).
@@ -1381,7 +1481,8 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
   if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
   if (!strcmp(key, "signal_pair") && (value == 0 || value == 1)) { g_tune_signal_pair = value; return CSM_OK; }
-  if (!strcmp(key, "signal_sync") && value >= 0 && value <= 64) { g_tune_signal_sync = value; return CSM_OK; }
+  if (!strcmp(key, "signal_maxd23") && (value == 0 || value == 1)) { g_tune_signal_maxd23 = value; return CSM_OK; }
+  if (!strcmp(key, "signal_db") && (value == 0 || value == 16 || value == 20 || value == 21)) { g_tune_signal_db = value; return CSM_OK; }
   if (!strcmp(key, "signal_mw") && (value == 0 || value == 21 || value == 22 || value == 41 ||
                                     value == 42)) { g_tune_signal_mw = value; return CSM_OK; }
   return CSM_E_INVAL;
@@ -1410,10 +1511,9 @@ int csm_create(int device, csm_ctx** out) {
 }
 
 int csm_destroy(csm_ctx* ctx) {
-  if (ctx && (ctx->scratch || ctx->aux)) {
+  if (ctx && ctx->scratch) {
     (void)hipSetDevice(ctx->device);
-    if (ctx->scratch) (void)hipFree(ctx->scratch);
-    if (ctx->aux) (void)hipFree(ctx->aux);
+    (void)hipFree(ctx->scratch);
   }
   free(ctx);
   return CSM_OK;
@@ -1530,7 +1630,8 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
                          int64_t N, const int64_t* month_start, int32_t T_m,
                          int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
                          double* M, double* NR, const double* carry, const double* next_pm,
-                         double* carry_out, bool sh = false, uint16_t* ids = nullptr) {
+                         double* carry_out, bool sh = false, uint16_t* ids = nullptr,
+                         int32_t min_month_days = 0) {
   int r = prep(ctx);
   if (r) return r;
   if (sh && (tiled || !PM || carry || next_pm || !carry_out || T_m < 1))
@@ -1573,6 +1674,24 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   }
   const int vec = tiled ? 2 : ((g_tune_signal_vec == 1 || !can2) ? 1 : 2);
   const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : 4;
+  const int db = g_tune_signal_db;
+  if (db > 0 && !tiled && !sh && vec == 2 && nbuf == 4 && !carry && !next_pm && !carry_out &&
+      g_tune_signal_bw == 1 && g_tune_signal_store == 0 && g_tune_signal_pair &&
+      min_month_days >= db) {   // day batches (every month >= db days)
+    const void* fd = db >= 21 ? (const void*)k_signal_db<21, 4>
+                   : db >= 20 ? (const void*)k_signal_db<20, 4> : (const void*)k_signal_db<16, 4>;
+    const size_t ldsd = (size_t)W * 128 * sizeof(double);
+    if (ldsd > 65536)
+      HIP_CHECK(ctx, hipFuncSetAttribute(fd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd));
+    int T_m_ = T_m, J_ = J, skip_ = skip;
+    int64_t N_ = N, T_d_ = T_d;
+    void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
+                    (void*)&M, (void*)&NR, &T_d_, (void*)&ids};
+    HIP_CHECK(ctx, hipLaunchKernel(fd, dim3((unsigned)((N / 2 + 63) / 64)), dim3(64), args, ldsd,
+                                   ctx->stream));
+    LAUNCH_CHECK(ctx, who);
+    return CSM_OK;
+  }
   const int bw = (!sh && !tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
   const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double) +
                      (sh ? (size_t)3 * 64 * vec * sizeof(int) : 0);
@@ -1597,6 +1716,8 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     fn = (const void*)k_signal<24, 2, 4, false, 1>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 2)
     fn = (const void*)k_signal<24, 2, 4, false, 2>;
+  else if (vec == 2 && nbuf == 4 && max_month_days <= 23 && g_tune_signal_maxd23 && g_tune_signal_pair)
+    fn = (const void*)k_signal<23, 2, 4, false, 0, 1, false, true>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_pair == 0)
     fn = (const void*)k_signal<24, 2, 4, false, 0, 1, false, false>;
   else if (max_month_days <= 24)
@@ -1610,23 +1731,9 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   {
     int T_m_ = T_m, J_ = J, skip_ = skip;
     int64_t N_ = N, T_d_ = T_d;
-    int* tick = nullptr;
-    int lag = g_tune_signal_sync;
-    if (lag > 0 && !sh && nbuf == 4) {   // pacing experiment: one arrival counter per 4 months
-      const size_t need = (size_t)(T_m / 4 + 2) * sizeof(int);
-      if (ctx->aux_bytes < need) {
-        if (ctx->aux) HIP_CHECK(ctx, hipFree(ctx->aux));
-        ctx->aux = nullptr;
-        ctx->aux_bytes = 0;
-        HIP_CHECK(ctx, hipMalloc(&ctx->aux, need));
-        ctx->aux_bytes = need;
-      }
-      tick = (int*)ctx->aux;
-      HIP_CHECK(ctx, hipMemsetAsync(tick, 0, need, ctx->stream));
-    }
     void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
                     (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out, &T_d_,
-                    (void*)&ids, (void*)&tick, &lag};
+                    (void*)&ids};
     HIP_CHECK(ctx, hipLaunchKernel(fn, dim3(blocks), dim3(64 * bw), args, lds, ctx->stream));
   }
   LAUNCH_CHECK(ctx, who);
@@ -1642,13 +1749,14 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
 }
 
 int csm_signal_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
-                   const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
-                   int32_t skip, double* PM, double* R, double* M, double* NR, uint16_t* ids) {
+                   const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                   int32_t min_month_days, int32_t J, int32_t skip, double* PM, double* R,
+                   double* M, double* NR, uint16_t* ids) {
   if (!ids || (N % 4) != 0 || ((uintptr_t)ids & 7u) != 0)
     return set_err(ctx, CSM_E_INVAL, "csm_signal_ids: ids must be non-NULL and 8-B aligned, N %% 4 == 0 "
                    "(N=%lld)", (long long)N);
   return signal_launch(ctx, "csm_signal_ids", false, P, T_d, N, month_start, T_m, max_month_days, J,
-                       skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids);
+                       skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids, min_month_days);
 }
 
 int csm_signal_shard(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
@@ -1846,7 +1954,8 @@ int csm_deciles_ids(csm_ctx* ctx, const double* M, const double* NR, const uint1
 }
 
 int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
-                 int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, int32_t n_bins,
+                 int32_t T_m, int32_t max_month_days, int32_t min_month_days, int32_t J,
+                 int32_t skip, int32_t n_bins,
                  const double* qtable, double* PM, double* R, double* M, double* NR, int8_t* L,
                  double* EW, int32_t* CNT, int32_t* NV, double* LS) {
   int r = prep(ctx);
@@ -1873,7 +1982,7 @@ int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const in
     ids = (uint16_t*)ctx->scratch;
   }
   r = signal_launch(ctx, "csm_pipeline", false, P, T_d, N, month_start, T_m, max_month_days, J,
-                    skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids);
+                    skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids, min_month_days);
   if (r) return r;
   QTab q;
   for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;

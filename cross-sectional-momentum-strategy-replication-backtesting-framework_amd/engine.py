@@ -243,7 +243,7 @@ class Engine:
         return PM, R, M, NR
 
     def signal_ids(self, P, month_start, max_month_days, J=12, skip=1, with_pm=False,
-                   with_ret=False, out=None):
+                   with_ret=False, out=None, min_month_days=0):
         """csm_signal_ids: csm_signal (no carry) that also writes the fixed-map bucket id of
         every mom_J (uint16 [T_m][N], read by deciles_ids).  N % 4 == 0.
         Returns (PM, R, M, NR, IDS)."""
@@ -260,7 +260,8 @@ class Engine:
             PM, R, M, NR, IDS = out
         _need(IDS, "IDS", torch.int16, (T_m, N), self.device)
         self._call("csm_signal_ids", _ptr(P), T_d, N, _ptr(month_start), T_m, int(max_month_days),
-                   int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR), _ptr(IDS))
+                   int(min_month_days), int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR),
+                   _ptr(IDS))
         return PM, R, M, NR, IDS
 
     def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False):
@@ -282,16 +283,30 @@ class Engine:
                    q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV))
         return L, EW, CNT, NV
 
+    @staticmethod
+    def month_days(month_start):
+        """(longest month, shortest interior month) in days, one device sync; the first and
+        the last month may be partial (csm_signal_ids' min_month_days excepts them)."""
+        if month_start.numel() < 2:
+            return 1, 0
+        d = month_start[1:] - month_start[:-1]
+        inner = d[1:-1] if d.numel() > 2 else d[:0]
+        mn = inner.min() if inner.numel() else torch.full_like(d[0], 1 << 30)
+        mx, mn = torch.stack([d.max(), mn]).tolist()
+        return int(mx), int(mn)
+
     def pipeline(self, P, month_start, J=12, skip=1, n_bins=10, max_month_days=None,
-                 with_pm=True, with_ret=False, out=None) -> PipelineOut:
+                 with_pm=True, with_ret=False, out=None, min_month_days=None) -> PipelineOut:
         """csm_pipeline: the whole K = 1 pass in one C call (fused signal with bucket ids,
         labels + decile means, long-short)."""
         T_d, N = P.shape
         T_m = month_start.numel() - 1
         _need(P, "P", torch.float64, (T_d, N), self.device)
         _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
-        if max_month_days is None:
-            max_month_days = int((month_start[1:] - month_start[:-1]).max().item()) if T_m else 1
+        if max_month_days is None or min_month_days is None:
+            mx, mn = self.month_days(month_start)
+            max_month_days = mx if max_month_days is None else max_month_days
+            min_month_days = mn if min_month_days is None else min_month_days
         if out is None:
             PM = self.empty((T_m, N)) if with_pm else None
             R = self.empty((T_m, N)) if with_ret else None
@@ -303,7 +318,8 @@ class Engine:
             PM, R, M, NR, L, EW, CNT, NV, LS = out
         q = quantile_table(n_bins)
         self._call("csm_pipeline", _ptr(P), T_d, N, _ptr(month_start), T_m, int(max_month_days),
-                   int(J), int(skip), int(n_bins), q.ctypes.data_as(ctypes.c_void_p), _ptr(PM),
+                   int(min_month_days), int(J), int(skip), int(n_bins),
+                   q.ctypes.data_as(ctypes.c_void_p), _ptr(PM),
                    _ptr(R), _ptr(M), _ptr(NR), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV), _ptr(LS))
         return PipelineOut(PM=PM, M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS, R=R, NV=NV)
 
@@ -653,13 +669,14 @@ class Engine:
         """One full pass: month-end -> signal -> labels + EW decile means -> long-short.
         Large panels take the fused month-end + scan kernel (no PM round trip)."""
         T_m, N = month_start.numel() - 1, P.shape[1]
+        min_month_days = None
         if max_month_days is None and T_m > 0:
-            max_month_days = int((month_start[1:] - month_start[:-1]).max().item())
+            max_month_days, min_month_days = self.month_days(month_start)
         if fused is None:
             fused = self.use_fused(P, V, max_month_days)
         if fused:   # one C call: signal (+ bucket ids for wide rows) -> deciles -> long-short
             return self.pipeline(P, month_start, J, skip, n_bins, max_month_days, with_pm=True,
-                                 with_ret=with_ret)
+                                 with_ret=with_ret, min_month_days=min_month_days)
         else:
             PM, VOL = self.month_end(P, month_start, V)
             if self.default_chunks(T_m, N, J, skip) > 1:

@@ -131,11 +131,14 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
 /*
  * csm_signal (no carry) that also writes ids[T_m][N] (uint16, 8-B aligned, N % 4 == 0): each
  * mom_J's bucket under the fixed monotone map of csm_deciles_ids (0xFFFF = NaN), so the decile
- * pass reads 2 B per cell instead of 8.
+ * pass reads 2 B per cell instead of 8.  min_month_days (HOST value: the shortest month in
+ * days, the first and the last month excepted; 0 = unknown) lets the kernel stream fixed day
+ * batches when every interior month is long enough.
  */
 int csm_signal_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
-                   const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
-                   int32_t skip, double* PM, double* R, double* M, double* NR, uint16_t* ids);
+                   const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                   int32_t min_month_days, int32_t J, int32_t skip, double* PM, double* R,
+                   double* M, double* NR, uint16_t* ids);
 
 /*
  * next_pm[N] for a month boundary m0: the month price of each asset's first present month
@@ -202,12 +205,14 @@ int csm_deciles_ids(csm_ctx* ctx, const double* M, const double* NR, const uint1
 /*
  * The whole K = 1 path of run_demo.py:31-67 in one call: fused month-end + scan (csm_signal,
  * with ids when N % 4 == 0 and the row is wide), per-date labels fused with the decile means
- * (csm_deciles / csm_deciles_ids), long-short (csm_long_short).  Arguments as in those calls;
+ * (csm_deciles / csm_deciles_ids), long-short (csm_long_short).  Arguments as in those calls
+ * (min_month_days as in csm_signal_ids);
  * PM, R, NV nullable; qtable HOST.  The ids live in a context-owned workspace (T_m * N * 2 B,
  * grown on first use).
  */
 int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
-                 int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, int32_t n_bins,
+                 int32_t T_m, int32_t max_month_days, int32_t min_month_days, int32_t J,
+                 int32_t skip, int32_t n_bins,
                  const double* qtable, double* PM, double* R, double* M, double* NR, int8_t* L,
                  double* EW, int32_t* CNT, int32_t* NV, double* LS);
 

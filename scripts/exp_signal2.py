@@ -20,6 +20,7 @@ pan = make_device_panel(N, days, ms, seed=4000, device="cuda:0", shard=(0, 1, 4,
 eng = csmom.Engine(0)
 T_m = len(ms) - 1
 maxd = int(np.diff(ms).max())
+mind = int(np.diff(ms)[1:-1].min())   # interior months
 tune = lambda k, v: eng.lib.csm_tune(k.encode(), v)
 outs = {}
 
@@ -37,9 +38,11 @@ def run(name):
     tune("signal_pair", pair)
     tune("signal_store", 2 if name == "nostore" else 0)
     tune("signal_nbuf", 3 if name.endswith("nbuf3") else 4)
-    tune("signal_sync", int(name.split("sync")[1]) if "sync" in name else 0)
+    tune("signal_maxd23", 0 if "d24" in name else 1)
+    tune("signal_db", int(name.split("db")[1]) if "db" in name else 0)
     if "ids" in name:
-        f = lambda: eng.signal_ids(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR, IDS))
+        f = lambda: eng.signal_ids(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR, IDS),
+                                   min_month_days=mind)
     else:
         f = lambda: eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
     t = timed(f)
@@ -55,7 +58,7 @@ for rnd in range(6):
         t = run(n)
         if rnd:
             times[n].append(t)
-for k, v in (("signal_pair", 1), ("signal_store", 0), ("signal_nbuf", 4), ("signal_sync", 0)):
+for k, v in (("signal_pair", 1), ("signal_store", 0), ("signal_nbuf", 4), ("signal_maxd23", 1), ("signal_db", 0)):
     tune(k, v)
 eq = lambda a, b: bool(torch.equal(a.view(torch.int64), b.view(torch.int64)))
 base = outs["nopair" if "nopair" in outs else names[0]]

@@ -64,3 +64,50 @@ def test_double_sort_vs_oracle(engine, case, K):
     ls = res.LS.cpu().numpy()
     rls = rp.reshape(-1, 10, 3)[:, 9, :] - rp.reshape(-1, 10, 3)[:, 0, :]
     assert np.array_equal(np.isnan(ls), np.isnan(rls))
+
+
+def _fixture_shares_map(z):
+    """The shares map tests/golden/make_golden.py:264-277 built (every branch of the
+    reference's _get_shares), recovered from the fixture's so / mcap arrays."""
+    shares = {}
+    for i, t in enumerate(z["tickers"]):
+        kind = i % 6
+        if kind in (0, 1):
+            shares[str(t)] = {"shares_outstanding": int(z["so"][i]), "market_cap": None}
+        elif kind == 2:
+            shares[str(t)] = {"shares_outstanding": None, "market_cap": float(z["mcap"][i])}
+        elif kind == 3:
+            shares[str(t)] = {"shares_outstanding": np.nan, "market_cap": float(z["mcap"][i])}
+        elif kind == 4:
+            shares[str(t)] = {}
+    return shares
+
+
+@pytest.mark.parametrize("lb", [3, 2, 5])
+def test_drop_in_compute_monthly_turnover_bit_exact(engine, lb):
+    """csmom.compute_monthly_turnover (the drop-in of src/features.py:60-107, GPU arithmetic)
+    on the frame csmom.compute_monthly_momentum_from_daily returns, against the reference's
+    own outputs (turnover.npz)."""
+    import pandas as pd
+
+    import csmom
+    from oracle.synth_np import to_long
+    z = load_golden("turnover")
+    days = pd.DatetimeIndex(z["day_ns"])
+    daily = to_long(dict(P=z["P"], V=z["V"], days=days, tickers=z["tickers"].astype(object)))
+    monthly = csmom.compute_monthly_momentum_from_daily(daily, lookback_months=12, skip_months=1)
+    out = csmom.compute_monthly_turnover(monthly, shares_info_map=_fixture_shares_map(z),
+                                         lookback_months=lb)
+    tix = {str(t): i for i, t in enumerate(z["tickers"])}
+    mix = {d: i for i, d in enumerate(pd.DatetimeIndex(z["month_end_ns"]))}
+    T_m, N = z[f"lb{lb}_turn_avg"].shape
+
+    def dense(col):
+        a = np.full((T_m, N), np.nan)
+        a[out["date"].map(mix).to_numpy(), out["ticker"].map(tix).to_numpy()] = \
+            pd.to_numeric(out[col], errors="coerce").to_numpy(dtype=np.float64)
+        return a
+    assert bits_equal(dense("turn_avg"), z[f"lb{lb}_turn_avg"])
+    if lb == 3:
+        for col in ("adv_est", "shares_outstanding", "turnover_monthly"):
+            assert bits_equal(dense(col), z[f"lb3_{col}"]), col

@@ -188,3 +188,32 @@ def test_pipeline_narrow_rows_fall_back(engine):
         ref = O.pipeline(P_h, ms_h, 12, 1, 10)
         assert np.array_equal(out.L.cpu().numpy(), ref["L"])
         assert max_rel(out.LS.cpu().numpy(), ref["LS"]) <= REL
+
+
+@pytest.mark.parametrize("db", [16, 20, 21])
+def test_day_batch_signal_kernel_bit_identical(engine, db):
+    """k_signal_db (fixed day batches; interior months >= db days, the first and last month
+    partial: 7, 15 and 1 days here) equals k_signal bit for bit -- month prices, ret_1m, mom_J,
+    next_ret, ids."""
+    lib = engine.lib
+    for T in (1_333, 1_341, 1_347):
+        pan = _panel(N=8_000, T=T, seed=db)
+        ms_h = pan["month_start"]
+        d = np.diff(ms_h)
+        maxd, mind = int(d.max()), int(d[1:-1].min())
+        assert mind >= 20 and (d[0] < 20 or d[-1] < 20)
+        P, ms = _up(pan["P"]), _up(ms_h)
+        ref = engine.signal_ids(P, ms, maxd, 12, 1, with_pm=True, with_ret=True)
+        try:
+            assert lib.csm_tune(b"signal_db", db) == 0
+            got = engine.signal_ids(P, ms, maxd, 12, 1, with_pm=True, with_ret=True,
+                                    min_month_days=mind)
+        finally:
+            lib.csm_tune(b"signal_db", 0)
+        for a, b in zip(got, ref):
+            if a.dtype == torch.float64:
+                assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (T, db)
+            else:
+                assert torch.equal(a, b), (T, db)
+        r = O.pipeline(pan["P"], ms_h, 12, 1, 10)
+        assert bits_equal(got[2].cpu().numpy(), r["M"]) and bits_equal(got[3].cpu().numpy(), r["NR"])

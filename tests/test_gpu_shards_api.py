@@ -210,8 +210,32 @@ def test_monthly_replication_prints_reference_numbers(engine, tmp_path):
     assert abs(res.sharpe - float(z["J12s1_sharpe"])) <= 1e-10 * abs(float(z["J12s1_sharpe"]))
     assert max_rel(res.cum.to_numpy(), z["J12s1_cum"]) <= 1e-10
     assert (tmp_path / "cum.png").exists()
-    printed = str(z["printed"])
-    assert buf.getvalue().splitlines()[0].split(":")[0] == printed.splitlines()[0].split(":")[0]
+    # the two printed lines, number formatting included (run_demo.py:72-73)
+    printed = str(z["printed"]).splitlines()
+    got = [ln for ln in buf.getvalue().splitlines() if ln.startswith(("Monthly", "Sharpe"))]
+    assert got == [ln for ln in printed if ln.startswith(("Monthly", "Sharpe"))]
+
+
+def test_ingestion_csv_to_engine(engine, tmp_path):
+    """Cached CSVs -> csmom.fetch_daily (the reference's call, run_demo.py:196) ->
+    monthly_replication on the GPU: the real-data numbers.  The CSVs are written here from the
+    real-data fixture's present rows in the cache's column layout (data_io.py:23-73)."""
+    import csmom
+    df, z = _real_long()
+    for t, g in df.groupby("ticker", sort=False):
+        out = pd.DataFrame({"Date": g["date"].dt.strftime("%Y-%m-%d"), "Adj Close": g["adj_close"],
+                            "Close": g["adj_close"], "Volume": g["volume"]})
+        out.to_csv(tmp_path / f"{t}_daily.csv", index=False)
+    daily = csmom.fetch_daily(list(z["tickers"]), start="2018-01-01", end="2024-12-31",
+                              verbose=False, data_dir=str(tmp_path))
+    assert len(daily) == len(df)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        res = csmom.monthly_replication(daily, {}, plot_path=None)
+    assert len(res.mom_ret) == 70
+    assert abs(res.mean - float(z["J12s1_mean"])) <= 1e-10 * abs(float(z["J12s1_mean"]))
+    assert abs(res.sharpe - float(z["J12s1_sharpe"])) <= 1e-10 * abs(float(z["J12s1_sharpe"]))
+    assert res.turnover is not None and "turn_avg" in res.turnover.columns
 
 
 def test_assign_deciles_per_date_api(engine):

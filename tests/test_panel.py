@@ -67,14 +67,33 @@ def test_monthly_frame_layout():
     assert (out.groupby("ticker")["date"].apply(lambda s: s.is_monotonic_increasing)).all()
 
 
-def test_turnover_host_matches_reference_rules():
-    import csmom
+def _turnover_case():
     m = pd.DataFrame({"ticker": ["A"] * 4 + ["B"] * 2,
                       "date": pd.to_datetime(["2020-01-31", "2020-02-29", "2020-03-31",
                                               "2020-04-30", "2020-01-31", "2020-02-29"]),
                       "adj_close": [10.0, np.nan, 20.0, 0.0, 5.0, 5.0],
                       "monthly_volume": [2100.0, 4200.0, 0.0, 21.0, 2100.0, np.nan]})
     info = {"A": {"market_cap": 1000}, "B": {"shares_outstanding": 50}}
+    return m, info
+
+
+def test_turnover_shares_column_host_rules():
+    """The shares_outstanding lookup of features.py:78-97 (host: a per-ticker dict lookup with
+    the int(market_cap / price) fallback); the arithmetic columns are the GPU kernel's."""
+    from csmom.features import _shares_arrays, _shares_column
+    m, info = _turnover_case()
+    so = _shares_column(m, info).to_numpy(dtype=float)
+    assert so[0] == 100 and np.isnan(so[1]) and so[2] == 50 and np.isnan(so[3])
+    assert so[4] == 50 and so[5] == 50
+    a, b = _shares_arrays(["A", "B", "C"], info)
+    assert np.isnan(a[0]) and a[1] == 50 and np.isnan(a[2])
+    assert b[0] == 1000 and np.isnan(b[1]) and np.isnan(b[2])
+
+
+@pytest.mark.gpu
+def test_turnover_matches_reference_rules_gpu():
+    import csmom
+    m, info = _turnover_case()
     out = csmom.compute_monthly_turnover(m, info, 3)
     assert list(out["adv_est"]) == [100.0, 200.0, 0.0, 1.0, 100.0, 0.0]
     so = out["shares_outstanding"].to_numpy(dtype=float)
