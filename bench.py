@@ -73,10 +73,19 @@ def parse():
                          "fused signal kernel writes (csm_signal_ids -> csm_deciles_ids)")
     ap.add_argument("--match-dates", type=int, default=0,
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
+    ap.add_argument("--tune", action="append", default=[],
+                    help="csm_tune key=value applied before the run (kernel A/B), repeatable")
     ap.add_argument("--per-j-scan", action="store_true",
                     help="C5: one scan per J instead of every J of a wide batch from one scan "
                          "(csm_momentum_multi, the default)")
     return ap.parse_args()
+
+
+def apply_tunes(eng, tunes):
+    for kv in tunes:
+        k, v = kv.split("=")
+        if eng.lib.csm_tune(k.encode(), int(v)) != 0:
+            raise SystemExit(f"csm_tune({k}, {v}) rejected")
 
 
 def cpu_baseline(n_assets: int, days: int, start: str):
@@ -170,6 +179,7 @@ def main():
     T_d, T_m = len(days), len(ms_host) - 1
 
     eng = csmom.Engine(local)
+    apply_tunes(eng, args.tune)
     J, skip, nb = 12, 1, 10
     # preallocated outputs: the timed loop performs no allocation
     max_days = int(np.diff(ms_host).max())
@@ -461,6 +471,7 @@ def sweep_main(args):
     days, ms_host, _ = bday_calendar(cfg["start"], T_d)
     T_m = len(ms_host) - 1
     eng = csmom.Engine(local)
+    apply_tunes(eng, args.tune)
     ts = TimedStages(eng)
     scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
                              multi_j_scan=not args.per_j_scan)

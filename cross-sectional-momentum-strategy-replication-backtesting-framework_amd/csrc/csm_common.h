@@ -76,18 +76,20 @@ struct QTab {
 };
 
 // Fixed bucket map of the fused pipeline (csm_signal_ids writes one u16 id per asset-month,
-// the decile pass histograms the ids instead of re-reading mom_J): y = fl(1 + x), 2048
-// buckets per octave of y over [1/4, 4), clamped at both ends (x <= -3/4 -> 0, x >= 3 ->
-// 8191).  fl(1 + x) is monotone in x and so are the bits of a positive double, so the map is
+// the decile pass histograms the ids instead of re-reading mom_J): y = fl(1 + x), 1024
+// buckets per octave of y over [1/16, 16), clamped at both ends (x <= -15/16 -> 0, x >= 15
+// -> 8191).  fl(1 + x) is monotone in x and so are the bits of a positive double, so the map is
 // monotone non-decreasing: bucket order never contradicts value order, and the decile pass
 // stays exact for ANY data -- the map only decides how many values share a bucket.  12-month
-// momentum cross-sections put ~100k / 8192 values per bucket in the bulk (log-normal-ish in
-// y); a row the map fits badly falls back to key-space refinement (slower, same labels).
+// momentum cross-sections (log-normal-ish in y) put ~5-10 of 100k values in a bulk bucket and
+// almost none in the clamped end buckets (2048 per octave over [1/4, 4) halved the target
+// buckets but left ~600-3000 values in the end buckets, whose exact min / max the pass needs);
+// a row the map fits badly falls back to key-space refinement (slower, same labels).
 #define CSM_FB_BUCKETS 8192
 #define CSM_FB_NAN 0xFFFFu
 __device__ __forceinline__ int csm_fbucket(double x) {
-  const int64_t b = ((int64_t)__double_as_longlong(1.0 + x)) >> 41;
-  const int64_t k = b - (0x3FD0000000000000LL >> 41);   // bits(0.25) >> 41
+  const int64_t b = ((int64_t)__double_as_longlong(1.0 + x)) >> 42;
+  const int64_t k = b - (0x3FB0000000000000LL >> 42);   // bits(1/16) >> 42
   return (int)(k < 0 ? 0 : (k > CSM_FB_BUCKETS - 1 ? CSM_FB_BUCKETS - 1 : k));
 }
 __device__ __forceinline__ uint32_t csm_fid(double x) {
@@ -99,6 +101,12 @@ template <int NB>
 void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                            int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
+
+// one-wave-per-row decile launcher (deciles_wave.hip), NB in {0,2,3,4,5,10,20}
+template <int NB>
+void launch_deciles_wave(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
+                         int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
+                         int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
 
 // wide-row decile launcher with register-resident bucket ids (deciles_reg.hip): rows with
 // N even and N <= deciles_reg_max_n(), 16-B aligned M / NR, 2-B aligned L.  The first

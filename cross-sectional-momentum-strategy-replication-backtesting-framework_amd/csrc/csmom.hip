@@ -1459,6 +1459,7 @@ static int g_tune_dec_reg = 0;
 // csm_momentum_multi: 1 register shift ring when max(J) + skip <= 16, 0 the LDS ring
 static int g_tune_mj_reg = 1;
 // rows with at most this many assets take the narrow-row decile kernel (deciles_narrow.hip)
+static int64_t g_tune_dec_wave_max = 0;       // rows with at most this many assets: deciles_wave.hip
 static int64_t g_tune_dec_narrow_max = 16384;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
 
 extern "C" {
@@ -1477,6 +1478,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "mj_reg") && (value == 0 || value == 1)) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_reg") && value >= 0 && value <= 2) { g_tune_dec_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
+  if (!strcmp(key, "dec_wave_max") && value >= 0) { g_tune_dec_wave_max = value; return CSM_OK; }
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
   if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
@@ -1832,6 +1834,10 @@ static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, co
   int64_t* tm = g_dec_timing;
   if (pre) {   // ids written by csm_signal_ids (fixed map): M is read only for a few cells
     hipLaunchKernelGGL((k_deciles<NB, true, true, 0, true>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+    return;
+  }
+  if (N <= g_tune_dec_wave_max && !ids) {     // the narrowest rows: one wave per row
+    launch_deciles_wave<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
     return;
   }
   if (N <= g_tune_dec_narrow_max && !ids) {   // rows of a few thousand assets (C2/C3/C5)

@@ -56,6 +56,9 @@ ok = (tim.cpu().numpy() >= 0).all(axis=1)
 t = t[ok]
 names = ["sample", "histogram", "targets", "refine", "gather", "select", "edges+table",
          "labels+sums", ]
+if ABL & 16:   # fine marks (csrc/deciles.inc): hist, targets+refine, gather prologue, sweep, ...
+    names = ["histogram", "targets+refine", "gather_prologue", "gather_sweep", "gather_flush+minmax",
+             "select", "edges", "table"]
 d = np.diff(t, axis=1)
 out = {"N": N, "ids": IDS, "reg": REG, "ablate": ABL, "rows": T_m, "rows_timed": int(ok.sum()), "kernel_ms": round(e0.elapsed_time(e1), 4),
        "phase_us_mean": {n: round(float(d[:, i].mean()), 2) for i, n in enumerate(names)},

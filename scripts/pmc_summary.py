@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--workload", default="")
     ap.add_argument("--emit", nargs="*", default=[])
     ap.add_argument("--emit-dir", default=None)
+    ap.add_argument("--source", default="", help="where the committed summary will live")
     a = ap.parse_args()
     stats = read_stats(os.path.join(a.prof_dir, "trace"))
     fetch = read_counters(os.path.join(a.prof_dir, "pmc_fetch"))
@@ -86,7 +87,7 @@ def main():
             out = {"N": a.N, "T_d": a.T_d, "kernel": k,
                    "hbm_bytes_per_launch": kern[k]["hbm_bytes_corrected"],
                    "avg_ns": stats.get(k, {}).get("avg_ns"),
-                   "source": "profiles/r01/c4_pmc_summary.json"}
+                   "source": a.source}
             with open(os.path.join(a.emit_dir or a.prof_dir, f"pmc_{k}.json"), "w") as fh:
                 json.dump(out, fh, indent=1)
     print(json.dumps({k: (v["hbm_bytes_corrected"], stats.get(k, {}).get("avg_ns"))

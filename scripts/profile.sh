@@ -18,5 +18,5 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
 rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/pmc_fetch.log"; echo "FATAL fetch rc=$rc"; exit $rc; }
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/pmc_write.log"; echo "FATAL write rc=$rc"; exit $rc; }
-python3 scripts/pmc_summary.py "$OUT" --N "$NN" --T_d "$TD" --workload "bench.py --config $CFG" --emit k_signal k_deciles k_month_end k_cohort
+python3 scripts/pmc_summary.py "$OUT" --N "$NN" --T_d "$TD" --workload "bench.py --config $CFG" --source "profiles/$TAG/${CFG}_pmc_summary.json" --emit k_signal k_deciles k_month_end k_cohort_seg k_turnover k_label_sort
 echo "profile done"

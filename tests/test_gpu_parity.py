@@ -444,3 +444,30 @@ def test_sweep_batch_multi_J_scan_equals_per_J(engine):
 
     b, _ = SweepRunner(PerJ(engine), cfg).run_batch(PMb, B)
     assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+@pytest.mark.parametrize("name", ["edge", "c1", "small", "real_data"])
+def test_wave_decile_kernel_equals_narrow(engine, name):
+    """One wave per row (deciles_wave.hip): labels, counts and ranked rows equal the narrow-row
+    kernel's bit for bit (the range sample differs; the order statistics are exact either
+    way), decile means to rounding; and the stress rows at narrow width against the oracle."""
+    z = load_golden(name)
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    _, M, NR = engine.momentum(PM, 12, 1)
+    lib = engine.lib
+    a = engine.deciles(M, NR, 10, with_nv=True)
+    try:
+        assert lib.csm_tune(b"dec_wave_max", 16384) == 0
+        b = engine.deciles(M, NR, 10, with_nv=True)
+        for case in [c for c in STRESS if c != "odd_n"][: (3 if name != "edge" else len(STRESS))]:
+            xs = _stress_row(case)[:12_000]
+            Ls, _, _, _ = engine.deciles(_up(xs[None, :]), None, 10)
+            assert np.array_equal(Ls.cpu().numpy()[0], _oracle_labels(xs)), case
+        xo = _stress_row("odd_n")[:9_999]
+        Lo, _, _, _ = engine.deciles(_up(xo[None, :]), None, 10)
+        assert np.array_equal(Lo.cpu().numpy()[0], _oracle_labels(xo))
+    finally:
+        lib.csm_tune(b"dec_wave_max", 0)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+    ea, eb = a[1].cpu().numpy(), b[1].cpu().numpy()
+    assert np.array_equal(np.isnan(ea), np.isnan(eb)) and max_rel(ea, eb) <= 1e-12

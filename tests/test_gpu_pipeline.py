@@ -24,13 +24,13 @@ def _up(x, dev="cuda:0"):
 
 
 def fixed_ids(x):
-    """NumPy restatement of csm_fid: bucket of fl(1 + x) at 2048 per octave over [1/4, 4),
+    """NumPy restatement of csm_fid: bucket of fl(1 + x) at 1024 per octave over [1/16, 16),
     clamped to [0, 8191]; NaN -> 0xFFFF."""
     x = np.asarray(x, dtype=np.float64)
     with np.errstate(invalid="ignore", over="ignore"):
         y = 1.0 + x
-    b = y.view(np.int64) >> 41
-    k = np.clip(b - (np.float64(0.25).view(np.int64) >> 41), 0, 8191)
+    b = y.view(np.int64) >> 42
+    k = np.clip(b - (np.float64(1.0 / 16).view(np.int64) >> 42), 0, 8191)
     return np.where(np.isnan(x), 0xFFFF, k).astype(np.uint16)
 
 
@@ -52,7 +52,8 @@ def test_fixed_map_is_monotone():
     crosses both clamps, every octave boundary and +-0.0."""
     xs = np.sort(np.concatenate([
         np.linspace(-5, 10, 200_001), -np.logspace(-300, 300, 2001), np.logspace(-300, 300, 2001),
-        [-np.inf, np.inf, -0.75, -0.5, 0.0, -0.0, 1.0, 3.0, np.nextafter(-0.75, 0), np.nextafter(3.0, 4)]]))
+        [-np.inf, np.inf, -0.9375, -0.5, 0.0, -0.0, 1.0, 15.0, np.nextafter(-0.9375, 0),
+         np.nextafter(15.0, 16)]]))
     ids = fixed_ids(xs).astype(np.int64)
     assert (np.diff(ids) >= 0).all()
     assert ids[0] == 0 and ids[-1] == 8191
@@ -138,10 +139,10 @@ def _stress_row(case, n=200_000):
         return x
     elif case == "empty":
         return np.full(n, np.nan)
-    elif case == "one_bucket_tail":  # most of the row above the top clamp (x >= 3)
-        x = 3.0 + rng.exponential(1.0, n); x[:1000] = rng.normal(0, 0.1, 1000)
-    else:                            # clamped_low: most of the row below -3/4
-        x = -0.75 - rng.random(n) * 0.25; x[:500] = rng.normal(0.1, 0.2, 500)
+    elif case == "one_bucket_tail":  # most of the row above the top clamp (x >= 15)
+        x = 15.0 + rng.exponential(1.0, n); x[:1000] = rng.normal(0, 0.1, 1000)
+    else:                            # clamped_low: most of the row below -15/16
+        x = -0.9375 - rng.random(n) * 0.0625; x[:500] = rng.normal(0.1, 0.2, 500)
     x[rng.random(n) < 0.05] = np.nan
     return x
 
