@@ -73,6 +73,9 @@ def parse():
                          "fused signal kernel writes (csm_signal_ids -> csm_deciles_ids)")
     ap.add_argument("--match-dates", type=int, default=0,
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the step as one captured hipGraph (auto: the unfused narrow "
+                         "panels, C2, where launch gaps are a large share of the step)")
     ap.add_argument("--tune", action="append", default=[],
                     help="csm_tune key=value applied before the run (kernel A/B), repeatable")
     ap.add_argument("--per-j-scan", action="store_true",
@@ -215,8 +218,10 @@ def main():
         if pipe is not None:
             r = pipe.run(panel.P, panel.month_start, max_days)
             return r.LS
+        rec = (lambda e: e.record()) if ev is not None else (lambda e: None)
+        ev = ev if ev is not None else [None] * nst
         i = 0
-        ev[i].record()
+        rec(ev[i])
         if use_ids:
             eng.signal_ids(panel.P, panel.month_start, max_days, J, skip,
                            out=(None, None, M, NR, IDS), min_month_days=min_days)
@@ -225,26 +230,35 @@ def main():
         else:
             eng.month_end(panel.P, panel.month_start, PM=PM)
             i += 1
-            ev[i].record()
+            rec(ev[i])
             if chunks > 1:
                 eng.momentum_chunked(PM, J, skip, chunks=chunks, out=(None, M, NR), workspace=ws)
             else:
                 eng.momentum(PM, J, skip, out=(None, M, NR))
         i += 1
-        ev[i].record()
+        rec(ev[i])
         if use_ids:
             eng.deciles_ids(M, NR, IDS, nb, out=(L, EW, CNT, None))
         else:
             eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
         i += 1
-        ev[i].record()
+        rec(ev[i])
         eng.long_short(EW, CNT, LS)
-        ev[i + 1].record()
+        rec(ev[i + 1])
         return LS
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    use_graph = (world == 1 and pipe is None and
+                 (args.graph == "on" or (args.graph == "auto" and not fused)))
+    graph = None
+    if use_graph:   # the whole pass as one hipGraph (no host launches inside the timed loop)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step(None)
+        graph.replay()
+        torch.cuda.synchronize()
 
     stage_ms = np.zeros(len(stage_names))
     if world > 1:
@@ -252,11 +266,18 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(step_events[k])   # HIP events on the launch stream; read after the loop
+        if graph is not None:
+            graph.replay()
+        else:
+            step(step_events[k])   # HIP events on the launch stream; read after the loop
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if graph is not None:   # per-stage device times from an untimed eager pass
+        for k in range(args.steps):
+            step(step_events[k])
+        torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -343,6 +364,7 @@ def main():
             "data": "synthetic seeded GBM panel generated in HBM (late listings, delistings, "
                     "NaN days, absent and all-NaN months); N>1: rank r holds date shard r of "
                     "one global panel (prices continue across shards)",
+            "hipgraph": graph is not None,
             "engine_path": (("speculative fused k_signal + k_shard_repair" if pipe.fused else
                              "k_month_end + carried k_momentum") if pipe is not None else
                             "fused k_signal (+ bucket ids) -> k_deciles on ids" if use_ids else

@@ -28,6 +28,8 @@ struct csm_ctx {
   void* scratch;          // context-owned device workspace (k_deciles bucket ids), grown lazily
   size_t scratch_bytes;
   int n_cu;               // compute units of the device (decile kernel choice)
+  int32_t* dec_flg;       // [dec_flg_n] rows the merged decile pass left to the general kernel
+  int32_t dec_flg_n;      // (allocated at create, so a captured pipeline never allocates)
 };
 
 static inline int set_err(csm_ctx* c, int code, const char* fmt, ...) {
@@ -101,6 +103,15 @@ template <int NB>
 void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                            int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
+
+// fused-pipeline decile launcher on the bucket ids of csm_signal_ids (deciles_pre.hip),
+// NB in {0,2,3,4,5,10,20}.  flg (T_m ints) non-NULL: the merged kernel first, then the general
+// kernel for the rows it left (flg[t] = 1); NULL: the general kernel only
+template <int NB>
+void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
+                        int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
+                        int32_t* NV, int ablate, int64_t* tim, uint16_t* ids, int32_t* flg,
+                        bool merged_only);
 
 // one-wave-per-row decile launcher (deciles_wave.hip), NB in {0,2,3,4,5,10,20}
 template <int NB>

@@ -596,7 +596,7 @@ __device__ __forceinline__ bool shard_pm_kept(int m, int T_m, int W) {
 // price, and the first / last present month (-1 none) -- for k_shard_summary_state and
 // k_shard_repair.
 template <int MAXD, int VEC, int NBUF, bool TILED = false, int ST = 0, int BW = 1,
-          bool SH = false, bool PS = true>
+          bool SH = false, bool PS = true, bool BSYNC = true>
 __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
@@ -681,7 +681,16 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
     }
   };
   VT A[MAXD], B[MAXD], C[MAXD];
-  if (NBUF == 3) {
+  if (NBUF == 2) {
+    // month m+1 in flight while month m is reduced (half the registers: two waves per SIMD)
+    load_month(A, 0);
+    for (int m = 0; m < T_m; m += 2) {
+      load_month(B, m + 1);
+      process(A, m);
+      load_month(A, m + 2);
+      if (m + 1 < T_m) process(B, m + 1);
+    }
+  } else if (NBUF == 3) {
     // months m+1, m+2 in flight while month m is reduced
     load_month(A, 0);
     load_month(B, 1);
@@ -702,7 +711,7 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
     load_month(C, 2);
     for (int m = 0; m < T_m; m += 4) {
       load_month(D, m + 3);
-      if (BW > 1) __syncthreads();
+      if (BW > 1 && BSYNC) __syncthreads();
       process(A, m);
       load_month(A, m + 4);
       if (m + 1 < T_m) process(B, m + 1);
@@ -1439,9 +1448,12 @@ __global__ __launch_bounds__(256) void k_tile_panel(const double* __restrict__ P
 static int g_tune_signal_vec = 2;      // k_signal assets per lane: 1 or 2
 static int g_tune_signal_nbuf = 4;     // k_signal month buffers: 3 or 4
 static int g_tune_dec_ablate = 0;      // k_deciles pass ablation bitmask (profiling only: wrong results)
+static int g_tune_dec_merge = 1;       // PRE decile pass: merged sweep + general kernel for the rest (1), general only (0), merged only (2: test hook, rows it leaves are not written)
 static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<.., NW, NB>
 static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
 static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
+static int g_tune_signal_bwf = 0;      // k_signal waves per workgroup with NO barrier (adjacent columns, independent walks); 0 auto
+#define SIGNAL_BWF_MIN_N (180 * 512)
 static int g_tune_month_end_rows = 0;
 static int g_tune_signal_pair = 1;     // k_signal paired 16-B output stores (VEC 2): 1 on, 0 off
 static int g_tune_signal_db = 0;       // k_signal_db day-batch rows (16 | 20 | 21), 0 off
@@ -1472,8 +1484,9 @@ int csm_tune(const char* key, int value) {
   if (!key) return CSM_E_INVAL;
   if (!strcmp(key, "cohort_lds") || !strcmp(key, "cohort_seg")) return csm_tune_portfolio(key, value);
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
-  if (!strcmp(key, "signal_nbuf") && (value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
+  if (!strcmp(key, "signal_nbuf") && (value == 2 || value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
   if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
+  if (!strcmp(key, "dec_merge") && value >= 0 && value <= 2) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "dec_ids") && (value == 0 || value == 1)) { g_tune_dec_ids = value; return CSM_OK; }
   if (!strcmp(key, "mj_reg") && (value == 0 || value == 1)) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_reg") && value >= 0 && value <= 2) { g_tune_dec_reg = value; return CSM_OK; }
@@ -1481,6 +1494,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "dec_wave_max") && value >= 0) { g_tune_dec_wave_max = value; return CSM_OK; }
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
+  if (!strcmp(key, "signal_bwf") && value >= 0 && value <= 4) { g_tune_signal_bwf = value; return CSM_OK; }
   if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
   if (!strcmp(key, "signal_pair") && (value == 0 || value == 1)) { g_tune_signal_pair = value; return CSM_OK; }
   if (!strcmp(key, "signal_maxd23") && (value == 0 || value == 1)) { g_tune_signal_maxd23 = value; return CSM_OK; }
@@ -1508,14 +1522,20 @@ int csm_create(int device, csm_ctx** out) {
   c->stream = nullptr;
   if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->n_cu = 256;
+  c->dec_flg_n = 1 << 16;
+  if (hipMalloc(&c->dec_flg, (size_t)c->dec_flg_n * sizeof(int32_t)) != hipSuccess) {
+    free(c);
+    return CSM_E_HIP;
+  }
   *out = c;
   return CSM_OK;
 }
 
 int csm_destroy(csm_ctx* ctx) {
-  if (ctx && ctx->scratch) {
+  if (ctx && (ctx->scratch || ctx->dec_flg)) {
     (void)hipSetDevice(ctx->device);
-    (void)hipFree(ctx->scratch);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->dec_flg) (void)hipFree(ctx->dec_flg);
   }
   free(ctx);
   return CSM_OK;
@@ -1675,7 +1695,7 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     return CSM_OK;
   }
   const int vec = tiled ? 2 : ((g_tune_signal_vec == 1 || !can2) ? 1 : 2);
-  const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : 4;
+  const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : (g_tune_signal_nbuf == 2) ? 2 : 4;
   const int db = g_tune_signal_db;
   if (db > 0 && !tiled && !sh && vec == 2 && nbuf == 4 && !carry && !next_pm && !carry_out &&
       g_tune_signal_bw == 1 && g_tune_signal_store == 0 && g_tune_signal_pair &&
@@ -1694,7 +1714,24 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     LAUNCH_CHECK(ctx, who);
     return CSM_OK;
   }
-  const int bw = (!sh && !tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
+  // Barrier-free multi-wave workgroups: the BWF waves of a block walk adjacent 1-KiB column
+  // slices of the same day rows independently, so a CU's loads of a day row are one 4-KiB span.
+  // Auto (signal_bwf 0): 4 waves x 2 month buffers once the grid still covers >= 180 CUs
+  // (C4 1.75-1.85 -> 1.63-1.78 ms interleaved on three boxes, profiles/r02/experiments).
+  int bwf = g_tune_signal_bwf;
+  int nbf = nbuf;
+  if (bwf == 0) {
+    const bool big = N >= (int64_t)SIGNAL_BWF_MIN_N && g_tune_signal_nbuf == 4;
+    bwf = big ? 4 : 1;
+    nbf = big ? 2 : nbuf;
+  }
+  const bool bwf_ok = !sh && !tiled && vec == 2 && max_month_days <= 23 && g_tune_signal_maxd23 &&
+                      g_tune_signal_pair && g_tune_signal_bw == 1 && g_tune_signal_store == 0 &&
+                      ((nbf == 4 && (bwf == 2 || bwf == 4)) ||
+                       (nbf == 3 && bwf >= 2 && bwf <= 4) ||
+                       (nbf == 2 && bwf >= 1 && bwf <= 4));
+  const int bw = bwf_ok ? bwf
+                     : (!sh && !tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
   const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double) +
                      (sh ? (size_t)3 * 64 * vec * sizeof(int) : 0);
   const unsigned blocks = (unsigned)((N / vec + 64 * bw - 1) / (64 * bw));
@@ -1718,6 +1755,24 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     fn = (const void*)k_signal<24, 2, 4, false, 1>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 2)
     fn = (const void*)k_signal<24, 2, 4, false, 2>;
+  else if (bwf_ok && nbf == 4 && bwf == 2)
+    fn = (const void*)k_signal<23, 2, 4, false, 0, 2, false, true, false>;
+  else if (bwf_ok && nbf == 4 && bwf == 4)
+    fn = (const void*)k_signal<23, 2, 4, false, 0, 4, false, true, false>;
+  else if (bwf_ok && nbf == 3 && bwf == 2)
+    fn = (const void*)k_signal<23, 2, 3, false, 0, 2, false, true, false>;
+  else if (bwf_ok && nbf == 2 && bwf == 1)
+    fn = (const void*)k_signal<23, 2, 2, false, 0, 1, false, true, false>;
+  else if (bwf_ok && nbf == 2 && bwf == 4)
+    fn = (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false>;
+  else if (bwf_ok && nbf == 2 && bwf == 2)
+    fn = (const void*)k_signal<23, 2, 2, false, 0, 2, false, true, false>;
+  else if (bwf_ok && nbf == 2 && bwf == 3)
+    fn = (const void*)k_signal<23, 2, 2, false, 0, 3, false, true, false>;
+  else if (bwf_ok && nbf == 3 && bwf == 3)
+    fn = (const void*)k_signal<23, 2, 3, false, 0, 3, false, true, false>;
+  else if (bwf_ok && nbf == 3 && bwf == 4)
+    fn = (const void*)k_signal<23, 2, 3, false, 0, 4, false, true, false>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 23 && g_tune_signal_maxd23 && g_tune_signal_pair)
     fn = (const void*)k_signal<23, 2, 4, false, 0, 1, false, true>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_pair == 0)
@@ -1829,11 +1884,13 @@ int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double
 template <int NB>
 static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                           int32_t* CNT, int32_t* NV, uint16_t* ids, int n_cu, bool pre = false) {
+                           int32_t* CNT, int32_t* NV, uint16_t* ids, int n_cu, bool pre = false,
+                           int32_t* flg = nullptr) {
   const int ab = g_tune_dec_ablate;
   int64_t* tm = g_dec_timing;
   if (pre) {   // ids written by csm_signal_ids (fixed map): M is read only for a few cells
-    hipLaunchKernelGGL((k_deciles<NB, true, true, 0, true>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+    launch_deciles_pre<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids,
+                           g_tune_dec_merge ? flg : nullptr, g_tune_dec_merge == 2);
     return;
   }
   if (N <= g_tune_dec_wave_max && !ids) {     // the narrowest rows: one wave per row
@@ -1916,16 +1973,27 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
                             const double* M, const double* NR, int64_t N, int32_t n_bins,
                             const QTab& q, int8_t* L, double* EW, int32_t* CNT, int32_t* NV,
                             uint16_t* ids, bool pre) {
+  int32_t* flg = nullptr;
+  if (pre) {
+    if (ctx->dec_flg_n < T_m) {   // beyond the create-time capacity (not capture-safe)
+      if (ctx->dec_flg) HIP_CHECK(ctx, hipFree(ctx->dec_flg));
+      ctx->dec_flg = nullptr;
+      ctx->dec_flg_n = 0;
+      HIP_CHECK(ctx, hipMalloc(&ctx->dec_flg, (size_t)T_m * sizeof(int32_t)));
+      ctx->dec_flg_n = T_m;
+    }
+    flg = ctx->dec_flg;
+  }
   if (!NR) {
-    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, ctx->n_cu, pre);
+    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, ctx->n_cu, pre, flg);
   } else {
     switch (n_bins) {
-      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
-      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
-      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
-      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
-      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
-      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre); break;
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
       default:
         return set_err(ctx, CSM_E_INVAL, "%s: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", who, n_bins);
     }

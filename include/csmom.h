@@ -39,13 +39,17 @@ typedef struct csm_ctx csm_ctx;
 int csm_abi_version(void);
 
 /* Process-wide tuning knobs for A/B measurement: "signal_vec" (1|2 assets per lane in the
- * fused kernel), "signal_nbuf" (3|4 month buffers), "dec_ablate" (profiling-only bitmask
+ * fused kernel), "signal_nbuf" (2|3|4 month buffers; 2 only with "signal_bwf"), "dec_ablate" (profiling-only bitmask
  * that SKIPS decile passes and so produces wrong results), "dec_ids" (0|1 bucket-id scratch
- * path), "dec_reg" (0 off | 1 when T_m <= CUs | 2 always: register-resident bucket ids,
+ * path), "dec_merge" (1: csm_deciles_ids' merged label sweep, the
+ * general kernel for the rows it leaves | 0: the general kernel only | 2: test hook, the merged
+ * kernel only -- rows it leaves are not written), "dec_reg" (0 off | 1 when T_m <= CUs | 2 always: register-resident bucket ids,
  * bit-identical), "dec_narrow_max" (widest row for the narrow-row decile kernel),
  * "mj_reg" (csm_momentum_multi: 1 register shift ring when max(J) + skip <= 16, the default;
  * 0 the shared-memory ring), "month_end_rows" (0 off | max month days: one-shot month-end
- * kernel), "signal_bw" (1|2|4 waves per fused-kernel workgroup), "signal_store" (0 plain |
+ * kernel), "signal_bw" (1|2|4 waves per fused-kernel workgroup), "signal_bwf" (0 auto:
+ * 4 waves x 2 month buffers when N >= 92160, else 1 | 1..4 waves per fused-kernel workgroup with
+ * no barrier, walking adjacent 1-KiB column slices independently; with signal_nbuf 2 | 3 | 4), "signal_store" (0 plain |
  * 1 nontemporal | 2 none: profiling ablation), "signal_mw" (0 | 21 | 22 | 41 | 42 multi-wave
  * fused kernel), "cohort_lds" / "cohort_seg" (portfolio cohort-sum kernel choice).  Returns
  * CSM_E_INVAL for an unknown key or value. */

@@ -37,16 +37,17 @@ def run(name):
     pair = 0 if name.startswith("nopair") else 1
     tune("signal_pair", pair)
     tune("signal_store", 2 if name == "nostore" else 0)
-    tune("signal_nbuf", 3 if name.endswith("nbuf3") else 4)
+    tune("signal_nbuf", int(name.split("nbuf")[1][0]) if "nbuf" in name else 4)
     tune("signal_maxd23", 0 if "d24" in name else 1)
     tune("signal_db", int(name.split("db")[1]) if "db" in name else 0)
+    tune("signal_bwf", int(name.split("bwf")[1].split("_")[0]) if "bwf" in name else 1)
     if "ids" in name:
         f = lambda: eng.signal_ids(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR, IDS),
                                    min_month_days=mind)
     else:
         f = lambda: eng.signal(pan.P, pan.month_start, maxd, 12, 1, out=(None, None, M, NR))
     t = timed(f)
-    outs[name] = (M, NR)
+    outs[name] = (M, NR, IDS if "ids" in name else None)
     return t
 
 
@@ -58,11 +59,14 @@ for rnd in range(6):
         t = run(n)
         if rnd:
             times[n].append(t)
-for k, v in (("signal_pair", 1), ("signal_store", 0), ("signal_nbuf", 4), ("signal_maxd23", 1), ("signal_db", 0)):
+for k, v in (("signal_pair", 1), ("signal_store", 0), ("signal_nbuf", 4), ("signal_maxd23", 1), ("signal_db", 0),
+             ("signal_bwf", 1)):
     tune(k, v)
 eq = lambda a, b: bool(torch.equal(a.view(torch.int64), b.view(torch.int64)))
 base = outs["nopair" if "nopair" in outs else names[0]]
-same = {n: eq(outs[n][0], base[0]) and eq(outs[n][1], base[1]) for n in names if n != "nostore"}
+same = {n: eq(outs[n][0], base[0]) and eq(outs[n][1], base[1]) and
+        (outs[n][2] is None or base[2] is None or bool(torch.equal(outs[n][2], base[2])))
+        for n in names if n != "nostore"}
 alg = 8.0 * N * TD + 16.0 * N * T_m
 res = {n: round(float(np.median(t)), 4) for n, t in times.items()}
 print(json.dumps({"N": N, "T_d": TD, "k_signal_ms": res,

@@ -1,0 +1,140 @@
+// Read-pattern microbenchmarks, round 2 (dev tool, not part of the engine): which day-row
+// access order can a fused month-end + scan kernel use on the [T_d][N] f64 panel?
+// Every kernel reads the whole panel once (16-B loads, two assets per lane) and writes
+// nothing but a guard value.  "Months" are fixed 21-day blocks here.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MD 21
+
+__device__ __forceinline__ void guard(double acc, double* out) {
+  if (acc == 12345.678) out[0] = acc;
+}
+
+// (a) one-shot row sweep: one thread per (2 assets, month); all MD rows in flight
+__global__ __launch_bounds__(256) void mb_rows(const double* __restrict__ P, int64_t T_d, int64_t N, double* out) {
+  const int64_t a = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  const int64_t d0 = (int64_t)blockIdx.y * MD;
+  if (a >= N) return;
+  double2 v[MD];
+#pragma unroll
+  for (int k = 0; k < MD; ++k) {
+    const int64_t d = d0 + k < T_d ? d0 + k : T_d - 1;
+    v[k] = *reinterpret_cast<const double2*>(P + d * N + a);
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < MD; ++k) acc += v[k].x + v[k].y;
+  guard(acc, out);
+}
+
+// (b) long walk, 3 month buffers (2 months in flight while one is consumed); one wave per
+// 128 assets over a day range [d_begin, d_end) of T_d / G days (G = gridDim.y segments)
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void mb_long(const double* __restrict__ P, int64_t T_d, int64_t N, double* out) {
+  const int64_t a0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (a0 >= N) return;
+  const int64_t seg = (T_d + gridDim.y - 1) / gridDim.y;
+  const int64_t db = (int64_t)blockIdx.y * seg;
+  const int64_t de = db + seg < T_d ? db + seg : T_d;
+  const double* base = P + a0;
+  double acc = 0.0;
+  double2 A[MD], B[MD], C[MD];
+  auto ld = [&](double2 (&b)[MD], int64_t d0) {
+#pragma unroll
+    for (int k = 0; k < MD; ++k) { int64_t d = d0 + k < de ? d0 + k : de - 1; b[k] = *reinterpret_cast<const double2*>(base + d * N); }
+  };
+  auto use = [&](const double2 (&b)[MD]) {
+#pragma unroll
+    for (int k = 0; k < MD; ++k) acc += b[k].x * b[k].y;
+  };
+  ld(A, db); ld(B, db + MD);
+  for (int64_t d = db; d < de; d += 3 * MD) {
+    ld(C, d + 2 * MD); use(A);
+    ld(A, d + 3 * MD); use(B);
+    ld(B, d + 4 * MD); use(C);
+  }
+  guard(acc, out);
+}
+
+// (c) month-block chain pattern: wave (chunk x, block y) reads BM consecutive months of its
+// 128 assets with one month in flight while the previous one is consumed (2 buffers); the
+// grid is block-major (x = chunk fastest), so resident waves cover a band of months.
+template <int BM>
+__global__ __launch_bounds__(64) void mb_chain(const double* __restrict__ P, int64_t T_d, int64_t N, double* out) {
+  const int64_t a0 = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 2;
+  if (a0 >= N) return;
+  const int64_t db = (int64_t)blockIdx.y * BM * MD;
+  if (db >= T_d) return;
+  const int64_t de = db + BM * MD < T_d ? db + BM * MD : T_d;
+  const double* base = P + a0;
+  double acc = 0.0;
+  double2 A[MD], B[MD];
+  auto ld = [&](double2 (&b)[MD], int64_t d0) {
+#pragma unroll
+    for (int k = 0; k < MD; ++k) { int64_t d = d0 + k < de ? d0 + k : de - 1; b[k] = *reinterpret_cast<const double2*>(base + d * N); }
+  };
+  auto use = [&](const double2 (&b)[MD]) {
+#pragma unroll
+    for (int k = 0; k < MD; ++k) acc += b[k].x * b[k].y;
+  };
+  ld(A, db);
+  for (int m = 0; m < BM; m += 2) {
+    ld(B, db + (m + 1) * MD); use(A);
+    ld(A, db + (m + 2) * MD); use(B);
+  }
+  guard(acc, out);
+}
+
+// (d) chain pattern, 3 buffers (two months in flight)
+template <int BM>
+__global__ __launch_bounds__(64) void mb_chain3(const double* __restrict__ P, int64_t T_d, int64_t N, double* out) {
+  const int64_t a0 = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 2;
+  if (a0 >= N) return;
+  const int64_t db = (int64_t)blockIdx.y * BM * MD;
+  if (db >= T_d) return;
+  const int64_t de = db + BM * MD < T_d ? db + BM * MD : T_d;
+  const double* base = P + a0;
+  double acc = 0.0;
+  double2 A[MD], B[MD], C[MD];
+  auto ld = [&](double2 (&b)[MD], int64_t d0) {
+#pragma unroll
+    for (int k = 0; k < MD; ++k) { int64_t d = d0 + k < de ? d0 + k : de - 1; b[k] = *reinterpret_cast<const double2*>(base + d * N); }
+  };
+  auto use = [&](const double2 (&b)[MD]) {
+#pragma unroll
+    for (int k = 0; k < MD; ++k) acc += b[k].x * b[k].y;
+  };
+  ld(A, db); ld(B, db + MD);
+  for (int m = 0; m < BM; m += 3) {
+    ld(C, db + (m + 2) * MD); use(A);
+    ld(A, db + (m + 3) * MD); use(B);
+    ld(B, db + (m + 4) * MD); use(C);
+  }
+  guard(acc, out);
+}
+
+extern "C" {
+// kind: 0 rows | 1..4 long G=1,2,4,8 | 5 long WPB=4 | 6..9 chain BM=2,4,8,16 | 10..12 chain3 BM=3,6,12
+int mb2_launch(int kind, const double* P, int64_t T_d, int64_t N, double* out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if ((N % 2) != 0) return -3;
+  const unsigned ch = (unsigned)((N / 2 + 63) / 64);
+  const unsigned mon = (unsigned)((T_d + MD - 1) / MD);
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(mb_rows, dim3((N / 2 + 255) / 256, mon), dim3(256), 0, st, P, T_d, N, out); break;
+    case 1: case 2: case 3: case 4:
+      hipLaunchKernelGGL(mb_long<1>, dim3(ch, 1u << (kind - 1)), dim3(64), 0, st, P, T_d, N, out); break;
+    case 5: hipLaunchKernelGGL(mb_long<4>, dim3((ch + 3) / 4, 1), dim3(256), 0, st, P, T_d, N, out); break;
+    case 6: hipLaunchKernelGGL(mb_chain<2>, dim3(ch, (mon + 1) / 2), dim3(64), 0, st, P, T_d, N, out); break;
+    case 7: hipLaunchKernelGGL(mb_chain<4>, dim3(ch, (mon + 3) / 4), dim3(64), 0, st, P, T_d, N, out); break;
+    case 8: hipLaunchKernelGGL(mb_chain<8>, dim3(ch, (mon + 7) / 8), dim3(64), 0, st, P, T_d, N, out); break;
+    case 9: hipLaunchKernelGGL(mb_chain<16>, dim3(ch, (mon + 15) / 16), dim3(64), 0, st, P, T_d, N, out); break;
+    case 10: hipLaunchKernelGGL(mb_chain3<3>, dim3(ch, (mon + 2) / 3), dim3(64), 0, st, P, T_d, N, out); break;
+    case 11: hipLaunchKernelGGL(mb_chain3<6>, dim3(ch, (mon + 5) / 6), dim3(64), 0, st, P, T_d, N, out); break;
+    case 12: hipLaunchKernelGGL(mb_chain3<12>, dim3(ch, (mon + 11) / 12), dim3(64), 0, st, P, T_d, N, out); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+}

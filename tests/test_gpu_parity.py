@@ -283,12 +283,20 @@ def test_signal_kernel_variants_bit_identical(engine, name):
                 check(engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True),
                       f"{knob}={v}")
                 lib.csm_tune(knob, 0 if knob != b"signal_bw" else 1)
+        # barrier-free multi-wave blocks (adjacent column slices, partial last block)
+        for bwf, nbuf in ((4, 2), (3, 2), (2, 2), (1, 2), (4, 3), (2, 3), (4, 4), (2, 4)):
+            assert lib.csm_tune(b"signal_nbuf", nbuf) == 0
+            assert lib.csm_tune(b"signal_bwf", bwf) == 0
+            check(engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True),
+                  f"signal_bwf={bwf} nbuf={nbuf}")
+        lib.csm_tune(b"signal_bwf", 0)
+        lib.csm_tune(b"signal_nbuf", 4)
         assert lib.csm_tune(b"month_end_rows", maxd) == 0
         PM, _ = engine.month_end(Pd, ms)
         assert bits_equal(PM.cpu().numpy(), base[0].cpu().numpy())
     finally:
         for knob, v in ((b"signal_mw", 0), (b"signal_bw", 1), (b"signal_store", 0),
-                        (b"month_end_rows", 0)):
+                        (b"month_end_rows", 0), (b"signal_bwf", 0), (b"signal_nbuf", 4)):
             lib.csm_tune(knob, v)
 
 

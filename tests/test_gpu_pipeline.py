@@ -139,6 +139,12 @@ def _stress_row(case, n=200_000):
         return x
     elif case == "empty":
         return np.full(n, np.nan)
+    elif case == "lognormal_mild":   # momentum-like: the merged pass takes it
+        x = np.exp(rng.normal(0, 0.8, n)) - 1.0
+    elif case == "wave_cluster":     # 1500 ties at the median inside wave 0's cells: its list
+        x = np.exp(rng.normal(0, 0.8, n)) - 1.0   # of uncertain cells overflows
+        idx = np.arange(n)
+        x[idx[(idx % 2048) < 256][:1500]] = np.median(x)
     elif case == "one_bucket_tail":  # most of the row above the top clamp (x >= 15)
         x = 15.0 + rng.exponential(1.0, n); x[:1000] = rng.normal(0, 0.1, 1000)
     else:                            # clamped_low: most of the row below -15/16
@@ -218,3 +224,58 @@ def test_day_batch_signal_kernel_bit_identical(engine, db):
                 assert torch.equal(a, b), (T, db)
         r = O.pipeline(pan["P"], ms_h, 12, 1, 10)
         assert bits_equal(got[2].cpu().numpy(), r["M"]) and bits_equal(got[3].cpu().numpy(), r["NR"])
+
+
+MERGE_CASES = STRESS + ["lognormal_mild", "wave_cluster"]
+
+
+@pytest.fixture
+def tune_merge(engine):
+    lib = engine.lib
+    yield lambda v: lib.csm_tune(b"dec_merge", v)
+    lib.csm_tune(b"dec_merge", 1)
+
+
+@pytest.mark.parametrize("case", MERGE_CASES)
+def test_deciles_ids_merged_equals_general(engine, tune_merge, case):
+    """The merged decile pass (one sweep of ids + next_ret; the general kernel for the rows it
+    leaves) equals the general kernel alone: labels, counts, ranked rows bit for bit, means
+    within 1e-13; labels equal the oracle's qcut.  Three rows per case: the case, a mild
+    momentum-like row, and the case again with other next_ret."""
+    rng = np.random.default_rng(7)
+    x = np.stack([_stress_row(case), _stress_row("lognormal_mild"), _stress_row(case)])
+    nr = rng.normal(0.01, 0.1, x.shape)
+    nr[rng.random(x.shape) < 0.03] = np.nan
+    M, NR, IDS = _up(x), _up(nr), _ids_dev(x)
+    got = {}
+    for v in (1, 0):
+        assert tune_merge(v) == 0
+        got[v] = engine.deciles_ids(M, NR, IDS, 10, with_nv=True)
+    (L1, EW1, C1, N1), (L0, EW0, C0, N0) = got[1], got[0]
+    assert torch.equal(L1, L0) and torch.equal(C1, C0) and torch.equal(N1, N0), case
+    a, b = EW1.cpu().numpy(), EW0.cpu().numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b)) and max_rel(a, b) <= 1e-13, case
+    for r in range(x.shape[0]):
+        assert np.array_equal(L1.cpu().numpy()[r], _oracle_labels(x[r])), (case, r)
+    rEW, rCNT, _ = O.portfolio_ew(np.stack([_oracle_labels(x[r]) for r in range(3)]), nr, 10)
+    assert np.array_equal(C1.cpu().numpy(), rCNT)
+    assert max_rel(a, rEW) <= REL
+
+
+def test_deciles_ids_merged_pass_takes_and_leaves_rows(engine, tune_merge):
+    """Test hook dec_merge = 2 (merged kernel only): it labels a momentum-like row itself and
+    leaves a row whose uncertain cells overflow one wave's list (its uncertain cells keep the
+    sentinel), a row of ties across edges and an empty row (untouched)."""
+    x = np.stack([_stress_row("lognormal_mild"), _stress_row("wave_cluster"),
+                  _stress_row("ties"), _stress_row("empty")])
+    M, IDS = _up(x), _ids_dev(x)
+    L = torch.full(x.shape, 100, dtype=torch.int8, device="cuda:0")
+    assert tune_merge(2) == 0
+    engine.deciles_ids(M, None, IDS, 10, out=(L, None, None, None))
+    torch.cuda.synchronize()
+    Lh = L.cpu().numpy()
+    assert np.array_equal(Lh[0], _oracle_labels(x[0]))
+    assert (Lh[1] == 100).any()   # certain cells were written before the overflow showed
+    for r in (2, 3):
+        assert (Lh[r] == 100).all(), r
+
