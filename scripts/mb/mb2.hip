@@ -116,6 +116,7 @@ __global__ __launch_bounds__(64) void mb_chain3(const double* __restrict__ P, in
 
 extern "C" {
 // kind: 0 rows | 1..4 long G=1,2,4,8 | 5 long WPB=4 | 6..9 chain BM=2,4,8,16 | 10..12 chain3 BM=3,6,12
+// | 13,14 long WPB=4 G=2,4 | 15,16 long WPB=2 G=1,2 | 17 long WPB=4 G=3
 int mb2_launch(int kind, const double* P, int64_t T_d, int64_t N, double* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((N % 2) != 0) return -3;
@@ -133,6 +134,11 @@ int mb2_launch(int kind, const double* P, int64_t T_d, int64_t N, double* out, v
     case 10: hipLaunchKernelGGL(mb_chain3<3>, dim3(ch, (mon + 2) / 3), dim3(64), 0, st, P, T_d, N, out); break;
     case 11: hipLaunchKernelGGL(mb_chain3<6>, dim3(ch, (mon + 5) / 6), dim3(64), 0, st, P, T_d, N, out); break;
     case 12: hipLaunchKernelGGL(mb_chain3<12>, dim3(ch, (mon + 11) / 12), dim3(64), 0, st, P, T_d, N, out); break;
+    case 13: hipLaunchKernelGGL(mb_long<4>, dim3((ch + 3) / 4, 2), dim3(256), 0, st, P, T_d, N, out); break;
+    case 14: hipLaunchKernelGGL(mb_long<4>, dim3((ch + 3) / 4, 4), dim3(256), 0, st, P, T_d, N, out); break;
+    case 15: hipLaunchKernelGGL(mb_long<2>, dim3((ch + 1) / 2, 1), dim3(128), 0, st, P, T_d, N, out); break;
+    case 16: hipLaunchKernelGGL(mb_long<2>, dim3((ch + 1) / 2, 2), dim3(128), 0, st, P, T_d, N, out); break;
+    case 17: hipLaunchKernelGGL(mb_long<4>, dim3((ch + 3) / 4, 3), dim3(256), 0, st, P, T_d, N, out); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

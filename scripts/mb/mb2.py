@@ -13,7 +13,8 @@ N, T_d = 100_000, 10_000
 P = torch.rand(T_d, N, dtype=torch.float64, device="cuda")
 out = torch.zeros(4, dtype=torch.float64, device="cuda")
 names = ["rows", "long_G1", "long_G2", "long_G4", "long_G8", "long_wpb4",
-         "chain2_B2", "chain2_B4", "chain2_B8", "chain2_B16", "chain3_B3", "chain3_B6", "chain3_B12"]
+         "chain2_B2", "chain2_B4", "chain2_B8", "chain2_B16", "chain3_B3", "chain3_B6", "chain3_B12",
+         "long_wpb4_G2", "long_wpb4_G4", "long_wpb2", "long_wpb2_G2", "long_wpb4_G3"]
 res = {n: [] for n in names}
 st = torch.cuda.current_stream()
 for rnd in range(8):
