@@ -78,6 +78,9 @@ def parse():
                          "panels, C2, where launch gaps are a large share of the step)")
     ap.add_argument("--tune", action="append", default=[],
                     help="csm_tune key=value applied before the run (kernel A/B), repeatable")
+    ap.add_argument("--no-decile-ids", action="store_true",
+                    help="sweeps: rank from mom_J (streaming decile kernel) instead of the bucket "
+                         "ids the multi-J scan writes (csm_momentum_multi_ids -> csm_deciles_ids)")
     ap.add_argument("--per-j-scan", action="store_true",
                     help="C5: one scan per J instead of every J of a wide batch from one scan "
                          "(csm_momentum_multi, the default)")
@@ -426,10 +429,10 @@ class TimedStages:
         T_m, N = PM.shape
         return self._wrap("scan(k_momentum*)", 24.0 * N * T_m, self.eng.momentum, PM, J, skip, **k)
 
-    def momentum_multi(self, PM, Js, skip=1):
+    def momentum_multi(self, PM, Js, skip=1, with_ids=False):
         T_m, N = PM.shape
         return self._wrap("scan(k_momentum*)", (8.0 + 16.0 * len(Js)) * N * T_m,
-                          self.eng.momentum_multi, PM, Js, skip)
+                          self.eng.momentum_multi, PM, Js, skip, with_ids=with_ids)
 
     def default_chunks(self, *a, **k):
         return self.eng.default_chunks(*a, **k)
@@ -437,6 +440,11 @@ class TimedStages:
     def deciles(self, M, NR=None, n_bins=10, **k):
         R_, N = M.shape
         return self._wrap("deciles(k_deciles)", 9.0 * N * R_, self.eng.deciles, M, NR, n_bins, **k)
+
+    def deciles_ids(self, M, NR, IDS, n_bins=10, **k):
+        R_, N = M.shape   # algorithmic: the labels of every cell (mom_J read, label written)
+        return self._wrap("deciles(k_deciles)", 9.0 * N * R_, self.eng.deciles_ids, M, NR, IDS,
+                          n_bins, **k)
 
     def portfolio(self, L, NR, n_bins=10, **k):
         T_m, BN = L.shape
@@ -496,7 +504,7 @@ def sweep_main(args):
     apply_tunes(eng, args.tune)
     ts = TimedStages(eng)
     scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
-                             multi_j_scan=not args.per_j_scan)
+                             multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":

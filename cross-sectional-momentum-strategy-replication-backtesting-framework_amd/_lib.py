@@ -27,7 +27,7 @@ EXPORTS = (
     "csm_double_sort_labels", "csm_tune_ptr", "csm_next_present",
     "csm_last_present_month", "csm_portfolio_from_cohorts_multi", "csm_summary",
     "csm_shard_repair", "csm_signal_shard", "csm_shard_summary_state", "csm_momentum_multi",
-    "csm_signal_ids", "csm_deciles_ids", "csm_pipeline",
+    "csm_signal_ids", "csm_deciles_ids", "csm_pipeline", "csm_momentum_multi_ids",
 )
 
 
@@ -68,6 +68,7 @@ def _declare(lib):
         "csm_month_end": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i32, _p, _p]),
         "csm_momentum": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p]),
         "csm_momentum_multi": (ctypes.c_int, [_p, _p, _i32, _i64, _p, _i32, _i32, _p, _p]),
+        "csm_momentum_multi_ids": (ctypes.c_int, [_p, _p, _i32, _i64, _p, _i32, _i32, _p, _p, _p]),
         "csm_signal": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
                                       _p, _p, _p]),
         "csm_signal_tiled": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p,

@@ -113,6 +113,13 @@ void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* 
                         int32_t* NV, int ablate, int64_t* tim, uint16_t* ids, int32_t* flg,
                         bool merged_only);
 
+// the same on narrow rows (deciles_narrow.hip: 1024 buckets = the fixed map's ids >> 3)
+template <int NB>
+void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
+                               int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
+                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim,
+                               uint16_t* ids, int32_t* flg, bool merged_only);
+
 // one-wave-per-row decile launcher (deciles_wave.hip), NB in {0,2,3,4,5,10,20}
 template <int NB>
 void launch_deciles_wave(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,

@@ -243,6 +243,23 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
 // (and ret_1m) as one 16-B store per row, next_ret as one 16-B store when both assets write
 // the same row (the steady state), so a wave issues half the store instructions.  Same
 // arithmetic in the same order as two scan_step calls: bit-identical outputs.
+// Output stores of the paired scan: plain, or nontemporal (NT) -- the monthly panels are
+// streamed past the caches to the next kernel.
+template <bool NT>
+__device__ __forceinline__ void st_d2(double* p, double a, double b) {
+  if (NT) {
+    __builtin_nontemporal_store(a, p);
+    __builtin_nontemporal_store(b, p + 1);
+  } else {
+    *reinterpret_cast<double2*>(p) = make_double2(a, b);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st_d1(double* p, double a) {
+  if (NT) __builtin_nontemporal_store(a, p);
+  else *p = a;
+}
+template <bool NT = false>
 __device__ __forceinline__ void scan_step_pair(ScanLane (&s)[2], const double (&x)[2], int m,
                                                double* ring0, int RS, int W, int J, int64_t N,
                                                int64_t a0, double* __restrict__ R,
@@ -301,6 +318,63 @@ __device__ __forceinline__ void scan_step_pair(ScanLane (&s)[2], const double (&
   } else {
     if (wc[0]) NR[o] = NaN;
     if (wc[1]) NR[o + 1] = NaN;
+  }
+}
+
+// scan_step_pair with the J+skip ring in REGISTERS (a shift register of RW >= J + skip factors
+// per asset, rg[c][0] the newest): no LDS round trips on the product chain, and no branches --
+// an absent month selects the old state back.  The product runs over the same factors in the
+// same order (oldest first) as the LDS ring; it starts from 1.0 and multiplies by 1.0 outside
+// the window (both exact), so the outputs are bit-identical to scan_step_pair's.
+template <int RW, bool NT = false>
+__device__ __forceinline__ void scan_step_pair_rr(ScanLane (&s)[2], const double (&x)[2], int m,
+                                                  double (&rg)[2][RW], int W, int J, int64_t N,
+                                                  int64_t a0, double* __restrict__ R,
+                                                  double* __restrict__ M, double* __restrict__ NR,
+                                                  double (&mom)[2]) {
+  const double NaN = qnan();
+  double ret[2], vp[2];
+  int wp[2];
+  bool wc[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const bool ab = is_absent(x[c]);
+    const bool xv = x[c] == x[c];
+    const double pnew = xv ? x[c] : s[c].pff;
+    const double r = pnew / s[c].pff - 1.0;
+    const double f = 1.0 + r;
+#pragma unroll
+    for (int k = RW - 1; k > 0; --k) rg[c][k] = ab ? rg[c][k] : rg[c][k - 1];
+    rg[c][0] = ab ? rg[c][0] : f;
+    s[c].pff = ab ? s[c].pff : pnew;
+    double acc = 1.0;
+#pragma unroll
+    for (int k = RW - 1; k >= 0; --k)   // wave-uniform window test
+      acc = (k < W && k >= W - J) ? acc * rg[c][k] : acc;
+    mom[c] = ab ? NaN : acc - 1.0;
+    ret[c] = ab ? NaN : r;
+    const bool ranked = mom[c] == mom[c];
+    const double ps_new = xv ? x[c] : s[c].psff;
+    wp[c] = (!ab && s[c].prev >= 0) ? s[c].prev : -1;
+    vp[c] = ps_new / s[c].psff - 1.0;
+    wc[c] = !ranked;
+    s[c].psff = ranked ? ps_new : s[c].psff;
+    s[c].prev = ranked ? m : (ab ? s[c].prev : -1);
+  }
+  const int64_t o = (int64_t)m * N + a0;
+  if (R) st_d2<NT>(R + o, ret[0], ret[1]);
+  st_d2<NT>(M + o, mom[0], mom[1]);
+  if (wp[0] >= 0 && wp[0] == wp[1]) {
+    st_d2<NT>(NR + (int64_t)wp[0] * N + a0, vp[0], vp[1]);
+  } else {
+    if (wp[0] >= 0) st_d1<NT>(NR + (int64_t)wp[0] * N + a0, vp[0]);
+    if (wp[1] >= 0) st_d1<NT>(NR + (int64_t)wp[1] * N + a0 + 1, vp[1]);
+  }
+  if (wc[0] && wc[1]) {
+    st_d2<NT>(NR + o, NaN, NaN);
+  } else {
+    if (wc[0]) st_d1<NT>(NR + o, NaN);
+    if (wc[1]) st_d1<NT>(NR + o + 1, NaN);
   }
 }
 
@@ -416,6 +490,7 @@ struct MJSet {
   int J[MJ_MAX];
   double* M[MJ_MAX];
   double* NR[MJ_MAX];
+  uint16_t* IDS[MJ_MAX];   // nullable: fixed-map bucket ids of M (csm_momentum_multi_ids)
 };
 
 __global__ __launch_bounds__(256) void k_momentum_multi(const double* __restrict__ PM, int T_m,
@@ -449,7 +524,10 @@ __global__ __launch_bounds__(256) void k_momentum_multi(const double* __restrict
       if (is_absent(x)) {
 #pragma unroll
         for (int q = 0; q < MJ_MAX; ++q)
-          if (q < nJ) { mj.M[q][o] = NaN; mj.NR[q][o] = NaN; }
+          if (q < nJ) {
+            mj.M[q][o] = NaN; mj.NR[q][o] = NaN;
+            if (mj.IDS[q]) mj.IDS[q][o] = (uint16_t)CSM_FB_NAN;
+          }
         continue;
       }
       const bool xv = !isnan_d(x);
@@ -480,6 +558,7 @@ __global__ __launch_bounds__(256) void k_momentum_multi(const double* __restrict
           prev[q] = -1;
         }
         mj.M[q][o] = mom;
+        if (mj.IDS[q]) mj.IDS[q][o] = (uint16_t)csm_fid(mom);
       }
     }
   }
@@ -525,7 +604,10 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg(const double* __rest
       if (is_absent(x)) {
 #pragma unroll
         for (int q = 0; q < MJ_MAX; ++q)
-          if (q < nJ) { mj.M[q][o] = NaN; mj.NR[q][o] = NaN; }
+          if (q < nJ) {
+            mj.M[q][o] = NaN; mj.NR[q][o] = NaN;
+            if (mj.IDS[q]) mj.IDS[q][o] = (uint16_t)CSM_FB_NAN;
+          }
         continue;
       }
       const bool xv = !isnan_d(x);
@@ -552,6 +634,7 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg(const double* __rest
           prev[q] = -1;
         }
         mj.M[q][o] = mom;
+        if (mj.IDS[q]) mj.IDS[q][o] = (uint16_t)csm_fid(mom);
       }
     }
   }
@@ -595,8 +678,11 @@ __device__ __forceinline__ bool shard_pm_kept(int m, int T_m, int W) {
 // months of the shard, the pending ranked row (month index, -1 none), its subset-ffilled
 // price, and the first / last present month (-1 none) -- for k_shard_summary_state and
 // k_shard_repair.
+// RR > 0 (VEC 2, paired stores, no carry in / out): the scan ring lives in registers
+// (scan_step_pair_rr, J + skip <= RR), no LDS.  ST 3 is a profiling ablation: no scan, M = the
+// month price (wrong results).
 template <int MAXD, int VEC, int NBUF, bool TILED = false, int ST = 0, int BW = 1,
-          bool SH = false, bool PS = true, bool BSYNC = true>
+          bool SH = false, bool PS = true, bool BSYNC = true, int RR = 0, bool BL = false>
 __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
@@ -610,12 +696,23 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   const int64_t a0 = ((int64_t)blockIdx.x * 64 * BW + tid) * VEC;
   const bool live = a0 < N;
   const int RS = 64 * VEC * BW;
+  static_assert(RR == 0 || (VEC == 2 && !SH && !TILED), "register rings: paired lanes only");
   ScanLane sl[VEC];
+  double rg[2][RR > 0 ? RR : 1];
   // SH counters live in LDS after the ring ([3][RS] ints: present months, first, last present
   // month): the kernel already holds ~500 registers, and these are touched once per month
   int* shc = reinterpret_cast<int*>(ring_lds + W * RS);
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
+    if constexpr (RR > 0) {
+#pragma unroll
+      for (int q = 0; q < RR; ++q) rg[k][q] = qnan();
+      sl[k].pff = qnan();
+      sl[k].psff = qnan();
+      sl[k].head = 0;
+      sl[k].prev = -1;
+      continue;
+    }
     scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, carry, N, a0 + k, live);
     if (SH) {
       shc[VEC * tid + k] = 0;
@@ -628,15 +725,32 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   const int64_t rstride = TILED ? 64 * VEC : N;
   // Loads are issued unconditionally (months past the end re-load the last month: cache
   // hits) so every wait is a counted vmcnt; only the processing is guarded.
+  // BL: raw buffer loads over a per-month resource that ends at the month's last day row, so
+  // the padding loads past it are out of range: counted by vmcnt like any load, but they return
+  // 0 without a memory request (process masks them by the wave-uniform row count).
+  static_assert(!BL || (VEC == 2 && !TILED), "buffer loads: row-major paired lanes");
+  const int voff = (int)((live ? a0 : 0) * 8);
   auto load_month = [&](VT (&buf)[MAXD], int mm) {
     mm = mm < T_m ? mm : T_m - 1;
     const int64_t f0 = month_start[mm], nn = month_start[mm + 1] - f0;
+    if constexpr (BL) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(P + f0 * N), (short)0, (int)(nn * N * 8), 0x00020000);
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-      buf[k] = *reinterpret_cast<const VT*>(base + (f0 + (k < nn ? k : nn - 1)) * rstride);
+      for (int k = 0; k < MAXD; ++k) {
+        const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + k * (int)(N * 8), 0, 0);
+        buf[k] = *reinterpret_cast<const VT*>(&w);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k)
+        buf[k] = *reinterpret_cast<const VT*>(base + (f0 + (k < nn ? k : nn - 1)) * rstride);
+    }
   };
   auto process = [&](const VT (&X)[MAXD], int m) {
     double pm[VEC];
+    const int nnm = BL ? (int)(month_start[m + 1] - month_start[m]) : MAXD;
 #pragma unroll
     for (int c = 0; c < VEC; ++c) {
       double last = 0.0;
@@ -644,8 +758,9 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
 #pragma unroll
       for (int k = 0; k < MAXD; ++k) {
         const double x = comp(X[k], c);
-        const bool ok = x == x;  // a valid price (ABSENT and missing are NaN)
-        p |= !is_absent(x);
+        const bool in = !BL || k < nnm;   // wave-uniform
+        const bool ok = in && x == x;  // a valid price (ABSENT and missing are NaN)
+        p |= in && !is_absent(x);
         v |= ok;
         last = ok ? x : last;
       }
@@ -663,8 +778,18 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
         else PMo[(int64_t)m * N + a0] = pm[0];
       }
       double mom[VEC];
-      if constexpr (VEC == 2 && ST == 0 && PS) {   // paired 16-B stores (R / M / NR are 16-B aligned)
-        scan_step_pair(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
+      if constexpr (ST == 3 || ST == 4) {   // ablations: no scan (3), no scan and no stores (4)
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) mom[c] = pm[c];
+        if (ST == 3 || pm[0] == 1234.5678) {
+          if (VEC == 2) *reinterpret_cast<double2*>(M + (int64_t)m * N + a0) = make_double2(pm[0], pm[VEC - 1]);
+          else M[(int64_t)m * N + a0] = pm[0];
+        }
+      } else if constexpr (RR > 0) {
+        scan_step_pair_rr<RR>(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
+                              m, rg, W, J, N, a0, R, M, NR, reinterpret_cast<double (&)[2]>(mom));
+      } else if constexpr (VEC == 2 && (ST == 0 || ST == 1) && PS) {   // paired 16-B stores (R / M / NR are 16-B aligned)
+        scan_step_pair<ST == 1>(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
                        m, ring_lds + VEC * tid, RS, W, J, N, a0, R, M, NR,
                        reinterpret_cast<double (&)[2]>(mom));
       } else {
@@ -672,9 +797,13 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
         for (int c = 0; c < VEC; ++c)
           mom[c] = scan_step<ST>(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
       }
-      if (IDS) {   // fixed-map bucket ids for the decile pass (csm_signal_ids)
+      if (IDS && ST != 4) {   // fixed-map bucket ids for the decile pass (csm_signal_ids)
         if (VEC == 2)
-          *reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0) = csm_fid(mom[0]) | (csm_fid(mom[VEC - 1]) << 16);
+        {
+          const uint32_t w = csm_fid(mom[0]) | (csm_fid(mom[VEC - 1]) << 16);
+          if (ST == 1) __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0));
+          else *reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0) = w;
+        }
         else
           IDS[(int64_t)m * N + a0] = (uint16_t)csm_fid(mom[0]);
       }
@@ -725,7 +854,7 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm,
-                  SH ? nullptr : carry_out);
+                  (SH || RR > 0) ? nullptr : carry_out);
       if (SH) {
         const int* q = shc + VEC * tid + k;
         carry_out[a0 + k] = (double)q[0];
@@ -1452,6 +1581,8 @@ static int g_tune_dec_merge = 1;       // PRE decile pass: merged sweep + genera
 static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<.., NW, NB>
 static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
 static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
+static int g_tune_signal_bl = 1;       // k_signal month rows by raw buffer loads (padding out of range): C4 1.695 -> 1.674 ms (profiles/r02/experiments/exp_signal_bl.log)
+static int g_tune_signal_rr = 0;       // k_signal scan ring in registers (J + skip <= 16): 1 on
 static int g_tune_signal_bwf = 0;      // k_signal waves per workgroup with NO barrier (adjacent columns, independent walks); 0 auto
 #define SIGNAL_BWF_MIN_N (180 * 512)
 static int g_tune_month_end_rows = 0;
@@ -1495,7 +1626,9 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
   if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
   if (!strcmp(key, "signal_bwf") && value >= 0 && value <= 4) { g_tune_signal_bwf = value; return CSM_OK; }
-  if (!strcmp(key, "signal_store") && value >= 0 && value <= 2) { g_tune_signal_store = value; return CSM_OK; }
+  if (!strcmp(key, "signal_rr") && (value == 0 || value == 1)) { g_tune_signal_rr = value; return CSM_OK; }
+  if (!strcmp(key, "signal_bl") && (value == 0 || value == 1)) { g_tune_signal_bl = value; return CSM_OK; }
+  if (!strcmp(key, "signal_store") && value >= 0 && value <= 4) { g_tune_signal_store = value; return CSM_OK; }
   if (!strcmp(key, "signal_pair") && (value == 0 || value == 1)) { g_tune_signal_pair = value; return CSM_OK; }
   if (!strcmp(key, "signal_maxd23") && (value == 0 || value == 1)) { g_tune_signal_maxd23 = value; return CSM_OK; }
   if (!strcmp(key, "signal_db") && (value == 0 || value == 16 || value == 20 || value == 21)) { g_tune_signal_db = value; return CSM_OK; }
@@ -1610,9 +1743,9 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
   return CSM_OK;
 }
 
-int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
-                       const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
-                       double* const* NR) {
+static int momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                          const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
+                          double* const* NR, uint16_t* const* IDS) {
   int r = prep(ctx);
   if (r) return r;
   if (!PM || !Js || !M || !NR || N <= 0 || T_m < 0 || nJ < 1 || nJ > MJ_MAX || skip < 0)
@@ -1624,6 +1757,9 @@ int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
     mj.J[q] = q < nJ ? Js[q] : 1;
     mj.M[q] = q < nJ ? M[q] : nullptr;
     mj.NR[q] = q < nJ ? NR[q] : nullptr;
+    mj.IDS[q] = (q < nJ && IDS) ? IDS[q] : nullptr;
+    if (q < nJ && IDS && !IDS[q])
+      return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi_ids: ids[%d] is NULL", q);
     if (q < nJ && (Js[q] < 1 || !M[q] || !NR[q]))
       return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi: J[%d]=%d or its outputs invalid", q,
                      q < nJ ? Js[q] : 0);
@@ -1646,6 +1782,19 @@ int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
                      nJ, skip, W, mj);
   LAUNCH_CHECK(ctx, "k_momentum_multi");
   return CSM_OK;
+}
+
+int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                       const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
+                       double* const* NR) {
+  return momentum_multi(ctx, PM, T_m, N, Js, nJ, skip, M, NR, nullptr);
+}
+
+int csm_momentum_multi_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                           const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
+                           double* const* NR, uint16_t* const* IDS) {
+  if (!IDS) return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi_ids: ids is NULL");
+  return momentum_multi(ctx, PM, T_m, N, Js, nJ, skip, M, NR, IDS);
 }
 
 static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double* P, int64_t T_d,
@@ -1725,14 +1874,23 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     bwf = big ? 4 : 1;
     nbf = big ? 2 : nbuf;
   }
+  // profiling ablation (signal_store 3, 4-wave blocks x 2 buffers): no scan, wrong results
+  const bool noscan = g_tune_signal_store >= 3 && !sh && !tiled && vec == 2 && max_month_days <= 23 &&
+                      g_tune_signal_pair && g_tune_signal_bw == 1;
   const bool bwf_ok = !sh && !tiled && vec == 2 && max_month_days <= 23 && g_tune_signal_maxd23 &&
-                      g_tune_signal_pair && g_tune_signal_bw == 1 && g_tune_signal_store == 0 &&
+                      g_tune_signal_pair && g_tune_signal_bw == 1 &&
+                      (g_tune_signal_store == 0 || (g_tune_signal_store == 1 && bwf == 4 && nbf == 2)) &&
                       ((nbf == 4 && (bwf == 2 || bwf == 4)) ||
                        (nbf == 3 && bwf >= 2 && bwf <= 4) ||
                        (nbf == 2 && bwf >= 1 && bwf <= 4));
-  const int bw = bwf_ok ? bwf
+  const bool rr = bwf_ok && g_tune_signal_rr && W <= 16 && !carry && !carry_out &&
+                  ((bwf == 4 && nbf >= 2) || (bwf == 1 && nbf == 2));
+  // raw buffer loads (padding rows out of range): rows of at most 2 GiB / 32
+  const bool bl = bwf_ok && g_tune_signal_bl && N * 8 * 32 < ((int64_t)1 << 31) &&
+                  bwf == 4 && (nbf == 2 || nbf == 3);
+  const int bw = noscan ? 4 : bwf_ok ? bwf
                      : (!sh && !tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
-  const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double) +
+  const size_t lds = rr ? 0 : (size_t)W * 64 * vec * bw * sizeof(double) +
                      (sh ? (size_t)3 * 64 * vec * sizeof(int) : 0);
   const unsigned blocks = (unsigned)((N / vec + 64 * bw - 1) / (64 * bw));
   const void* fn = nullptr;
@@ -1751,10 +1909,29 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
     fn = (const void*)k_signal<24, 2, 4, false, 0, 2>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_bw == 4)
     fn = (const void*)k_signal<24, 2, 4, false, 0, 4>;
+  else if (bwf_ok && g_tune_signal_store == 1)   // 4 waves x 2 buffers, nontemporal stores
+    fn = bl ? (const void*)k_signal<23, 2, 2, false, 1, 4, false, true, false, 0, true>
+            : (const void*)k_signal<23, 2, 2, false, 1, 4, false, true, false>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 1)
     fn = (const void*)k_signal<24, 2, 4, false, 1>;
   else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 2)
     fn = (const void*)k_signal<24, 2, 4, false, 2>;
+  else if (bl && nbf == 2 && bwf == 4)
+    fn = rr ? (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false, 16, true>
+            : (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false, 0, true>;
+  else if (bl && nbf == 3 && bwf == 4)
+    fn = (const void*)k_signal<23, 2, 3, false, 0, 4, false, true, false, 0, true>;
+  else if (rr && nbf == 2 && bwf == 4)
+    fn = (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false, 16>;
+  else if (rr && nbf == 3 && bwf == 4)
+    fn = (const void*)k_signal<23, 2, 3, false, 0, 4, false, true, false, 16>;
+  else if (rr && nbf == 4 && bwf == 4)
+    fn = (const void*)k_signal<23, 2, 4, false, 0, 4, false, true, false, 16>;
+  else if (rr && nbf == 2 && bwf == 1)
+    fn = (const void*)k_signal<23, 2, 2, false, 0, 1, false, true, false, 16>;
+  else if (noscan)
+    fn = g_tune_signal_store == 4 ? (const void*)k_signal<23, 2, 2, false, 4, 4, false, true, false>
+                                  : (const void*)k_signal<23, 2, 2, false, 3, 4, false, true, false>;
   else if (bwf_ok && nbf == 4 && bwf == 2)
     fn = (const void*)k_signal<23, 2, 4, false, 0, 2, false, true, false>;
   else if (bwf_ok && nbf == 4 && bwf == 4)
@@ -1888,9 +2065,13 @@ static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, co
                            int32_t* flg = nullptr) {
   const int ab = g_tune_dec_ablate;
   int64_t* tm = g_dec_timing;
-  if (pre) {   // ids written by csm_signal_ids (fixed map): M is read only for a few cells
-    launch_deciles_pre<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids,
-                           g_tune_dec_merge ? flg : nullptr, g_tune_dec_merge == 2);
+  if (pre) {   // ids written by csm_signal_ids / csm_momentum_multi_ids (fixed map): M is read only for a few cells
+    if (N <= g_tune_dec_narrow_max)   // sweep rows: 1024 buckets (the fixed map's ids >> 3)
+      launch_deciles_pre_narrow<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids,
+                                    g_tune_dec_merge ? flg : nullptr, g_tune_dec_merge == 2);
+    else
+      launch_deciles_pre<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids,
+                             g_tune_dec_merge ? flg : nullptr, g_tune_dec_merge == 2);
     return;
   }
   if (N <= g_tune_dec_wave_max && !ids) {     // the narrowest rows: one wave per row

@@ -170,9 +170,11 @@ class Engine:
                    _ptr(NR), _ptr(carry), _ptr(next_pm), _ptr(carry_out))
         return R, M, NR
 
-    def momentum_multi(self, PM, Js, skip=1):
+    def momentum_multi(self, PM, Js, skip=1, with_ids=False):
         """csm_momentum_multi: one scan for several look-backs (up to 4 per launch).  Returns
-        [(M, NR)] in the order of Js, each equal bit for bit to momentum(PM, J, skip)."""
+        [(M, NR)] in the order of Js, each equal bit for bit to momentum(PM, J, skip).
+        with_ids (csm_momentum_multi_ids): [(M, NR, IDS)], IDS the fixed-map bucket id of
+        every mom_J (uint16 [T_m][N], read by deciles_ids on rows of any width)."""
         T_m, N = PM.shape
         _need(PM, "PM", torch.float64, (T_m, N), self.device)
         Js = [int(J) for J in Js]
@@ -184,9 +186,16 @@ class Engine:
             jarr = (ctypes.c_int32 * len(grp))(*grp)
             marr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in Ms])
             narr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in NRs])
-            self._call("csm_momentum_multi", _ptr(PM), T_m, N, jarr, len(grp), int(skip), marr,
-                       narr)
-            outs.extend(zip(Ms, NRs))
+            if with_ids:
+                IDs = [self.empty((T_m, N), torch.int16) for _ in grp]
+                iarr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in IDs])
+                self._call("csm_momentum_multi_ids", _ptr(PM), T_m, N, jarr, len(grp), int(skip),
+                           marr, narr, iarr)
+                outs.extend(zip(Ms, NRs, IDs))
+            else:
+                self._call("csm_momentum_multi", _ptr(PM), T_m, N, jarr, len(grp), int(skip),
+                           marr, narr)
+                outs.extend(zip(Ms, NRs))
         return outs
 
     @staticmethod
@@ -265,7 +274,9 @@ class Engine:
         return PM, R, M, NR, IDS
 
     def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False):
-        """csm_deciles_ids: deciles() from the ids of signal_ids (same labels / counts)."""
+        """csm_deciles_ids: deciles() from the ids of signal_ids / momentum_multi(with_ids=True)
+        (same labels / counts).  Rows of <= 16384 assets take the narrow kernel (1024 buckets);
+        needs N % 4 == 0."""
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)
         _need(IDS, "IDS", torch.int16, (T_m, N), self.device)

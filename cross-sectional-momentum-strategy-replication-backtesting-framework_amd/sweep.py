@@ -91,6 +91,10 @@ class SweepConfig:
     aum: float = 0.0
     costs: bool = True
     multi_j_scan: bool = True
+    # with the multi-J scan, also write each mom_J's fixed-map bucket ids and rank the batch's
+    # rows from them (csm_momentum_multi_ids -> csm_deciles_ids): 2-B ids per cell instead of
+    # up to three passes over mom_J; same labels
+    decile_ids: bool = True
     extra: dict = field(default_factory=dict)
 
     @property
@@ -126,18 +130,28 @@ class SweepRunner:
         # panels, ~10 GB at C5 with batch 100); take it only when that fits in half the free
         # device memory, else scan per J (two panels live at a time).
         multi = None
-        need = 2 * len(c.Js) * T_m * BN * PMb.element_size()
+        ids = (c.decile_ids and hasattr(st, "deciles_ids") and N % 4 == 0)
+        need = (2 * PMb.element_size() + (2 if ids else 0)) * len(c.Js) * T_m * BN
         if (c.multi_j_scan and hasattr(st, "momentum_multi") and len(c.Js) > 1
                 and st.default_chunks(T_m, BN, max(c.Js), c.skip) == 1
                 and max(c.Js) + c.skip <= 64 and need <= _free_bytes(PMb) // 2):
-            multi = list(st.momentum_multi(PMb, c.Js, c.skip))   # by position: Js may repeat
+            # by position: Js may repeat
+            multi = list(st.momentum_multi(PMb, c.Js, c.skip, with_ids=True) if ids
+                         else st.momentum_multi(PMb, c.Js, c.skip))
         for q, J in enumerate(c.Js):   # one J's ranking / portfolio panels live at a time
+            IDS = None
             if multi is not None:
-                (M, NR), multi[q] = multi[q], None
+                mo, multi[q] = multi[q], None
+                M, NR = mo[0], mo[1]
+                IDS = mo[2] if ids else None
             else:
                 _, M, NR = st.momentum(PMb, J, c.skip)
-            L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
-            del M
+            if IDS is not None:
+                L, _, _, _ = st.deciles_ids(M.reshape(T_m * B, N), None,
+                                            IDS.reshape(T_m * B, N), c.n_bins)
+            else:
+                L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
+            del M, IDS
             L = L.reshape(T_m, BN)
             if hasattr(st, "summary"):   # device path: one cohort pass for every K of this J,
                 outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)

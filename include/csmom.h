@@ -50,7 +50,9 @@ int csm_abi_version(void);
  * kernel), "signal_bw" (1|2|4 waves per fused-kernel workgroup), "signal_bwf" (0 auto:
  * 4 waves x 2 month buffers when N >= 92160, else 1 | 1..4 waves per fused-kernel workgroup with
  * no barrier, walking adjacent 1-KiB column slices independently; with signal_nbuf 2 | 3 | 4), "signal_store" (0 plain |
- * 1 nontemporal | 2 none: profiling ablation), "signal_mw" (0 | 21 | 22 | 41 | 42 multi-wave
+ * 1 nontemporal | 2 none | 3 no scan | 4 no scan, no stores: profiling ablations, wrong results), "signal_rr" (0 | 1:
+ * fused-kernel scan ring in registers when J + skip <= 16, no carry; bit-identical), "signal_bl" (0 | 1, the default: fused-kernel day
+ * rows by raw buffer loads, padding rows out of range; bit-identical), "signal_mw" (0 | 21 | 22 | 41 | 42 multi-wave
  * fused kernel), "cohort_lds" / "cohort_seg" (portfolio cohort-sum kernel choice).  Returns
  * CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
@@ -107,6 +109,15 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
 int csm_momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
                        const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
                        double* const* NR);
+/*
+ * csm_momentum_multi that also writes, per look-back, ids[q][T_m][N] (uint16, host array of
+ * device pointers): each mom_J's fixed-map bucket id (as csm_signal_ids; 0xFFFF = NaN), so the
+ * sweep's decile pass (csm_deciles_ids on the [T_m * B][N] rows of a batch) reads 2-B ids and M
+ * only near the bin edges.  Same M / NR bits as csm_momentum_multi.
+ */
+int csm_momentum_multi_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                           const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
+                           double* const* NR, uint16_t* const* ids);
 
 /*
  * Time-chunked scan for panels with few assets: the months are split into C contiguous

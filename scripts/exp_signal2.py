@@ -36,7 +36,10 @@ def run(name):
     IDS = eng.empty((T_m, N), torch.int16)
     pair = 0 if name.startswith("nopair") else 1
     tune("signal_pair", pair)
-    tune("signal_store", 2 if name == "nostore" else 0)
+    tune("signal_store", 2 if name == "nostore" else 4 if name.startswith("noscanst") else
+         3 if name.startswith("noscan") else 1 if "_nt" in name else 0)
+    tune("signal_rr", 1 if "_rr" in name else 0)
+    tune("signal_bl", 1 if "_bl" in name else 0)
     tune("signal_nbuf", int(name.split("nbuf")[1][0]) if "nbuf" in name else 4)
     tune("signal_maxd23", 0 if "d24" in name else 1)
     tune("signal_db", int(name.split("db")[1]) if "db" in name else 0)
@@ -60,13 +63,13 @@ for rnd in range(6):
         if rnd:
             times[n].append(t)
 for k, v in (("signal_pair", 1), ("signal_store", 0), ("signal_nbuf", 4), ("signal_maxd23", 1), ("signal_db", 0),
-             ("signal_bwf", 1)):
+             ("signal_bwf", 0), ("signal_rr", 0), ("signal_bl", 0)):
     tune(k, v)
 eq = lambda a, b: bool(torch.equal(a.view(torch.int64), b.view(torch.int64)))
 base = outs["nopair" if "nopair" in outs else names[0]]
 same = {n: eq(outs[n][0], base[0]) and eq(outs[n][1], base[1]) and
         (outs[n][2] is None or base[2] is None or bool(torch.equal(outs[n][2], base[2])))
-        for n in names if n != "nostore"}
+        for n in names if n != "nostore" and not n.startswith("noscan")}
 alg = 8.0 * N * TD + 16.0 * N * T_m
 res = {n: round(float(np.median(t)), 4) for n, t in times.items()}
 print(json.dumps({"N": N, "T_d": TD, "k_signal_ms": res,

@@ -57,6 +57,45 @@ __global__ __launch_bounds__(64 * WPB) void mb_long(const double* __restrict__ P
   guard(acc, out);
 }
 
+// (b') long walk, 4 waves per block, + writes per 21-day "month": two 16-B stores per lane
+// (mom_J / next_ret shaped) and one 4-B store (bucket ids).  LOG = 0: row-major [T_m][N]
+// outputs (the engine's layout); LOG = 1: each block appends to its own contiguous region
+// (same bytes, sequential in time per block).
+template <int LOG>
+__global__ __launch_bounds__(256) void mb_long_w(const double* __restrict__ P, int64_t T_d, int64_t N, double* out,
+                                                 double* __restrict__ W1, double* __restrict__ W2, uint32_t* __restrict__ W3) {
+  const int64_t a0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (a0 >= N) return;
+  const int64_t T_m = (T_d + MD - 1) / MD;
+  const double* base = P + a0;
+  double acc = 0.0;
+  double2 A[MD], B[MD], C[MD];
+  auto ld = [&](double2 (&b)[MD], int64_t d0) {
+#pragma unroll
+    for (int k = 0; k < MD; ++k) { int64_t d = d0 + k < T_d ? d0 + k : T_d - 1; b[k] = *reinterpret_cast<const double2*>(base + d * N); }
+  };
+  auto use = [&](const double2 (&b)[MD], int64_t m) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < MD; ++k) { s0 += b[k].x; s1 += b[k].y; }
+    if (m >= T_m) return;
+    int64_t o;
+    if (LOG) o = ((int64_t)blockIdx.x * T_m + m) * 512 + 2 * threadIdx.x;
+    else o = m * N + a0;
+    *reinterpret_cast<double2*>(W1 + o) = make_double2(s0, s1);
+    *reinterpret_cast<double2*>(W2 + o) = make_double2(s1, s0);
+    W3[o / 2] = (uint32_t)(int)s0;
+  };
+  ld(A, 0); ld(B, MD);
+  int64_t m = 0;
+  for (int64_t d = 0; d < T_d; d += 3 * MD, m += 3) {
+    ld(C, d + 2 * MD); use(A, m);
+    ld(A, d + 3 * MD); use(B, m + 1);
+    ld(B, d + 4 * MD); use(C, m + 2);
+  }
+  guard(acc, out);
+}
+
 // (c) month-block chain pattern: wave (chunk x, block y) reads BM consecutive months of its
 // 128 assets with one month in flight while the previous one is consumed (2 buffers); the
 // grid is block-major (x = chunk fastest), so resident waves cover a band of months.
@@ -117,6 +156,14 @@ __global__ __launch_bounds__(64) void mb_chain3(const double* __restrict__ P, in
 extern "C" {
 // kind: 0 rows | 1..4 long G=1,2,4,8 | 5 long WPB=4 | 6..9 chain BM=2,4,8,16 | 10..12 chain3 BM=3,6,12
 // | 13,14 long WPB=4 G=2,4 | 15,16 long WPB=2 G=1,2 | 17 long WPB=4 G=3
+int mb2_launch_w(int log, const double* P, int64_t T_d, int64_t N, double* out, double* W1, double* W2,
+                 uint32_t* W3, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned ch = (unsigned)((N / 2 + 63) / 64);
+  if (log) hipLaunchKernelGGL(mb_long_w<1>, dim3((ch + 3) / 4), dim3(256), 0, st, P, T_d, N, out, W1, W2, W3);
+  else hipLaunchKernelGGL(mb_long_w<0>, dim3((ch + 3) / 4), dim3(256), 0, st, P, T_d, N, out, W1, W2, W3);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 int mb2_launch(int kind, const double* P, int64_t T_d, int64_t N, double* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if ((N % 2) != 0) return -3;

@@ -289,6 +289,27 @@ def test_signal_kernel_variants_bit_identical(engine, name):
             assert lib.csm_tune(b"signal_bwf", bwf) == 0
             check(engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True),
                   f"signal_bwf={bwf} nbuf={nbuf}")
+        # raw buffer loads (padding rows out of range), register scan rings, nontemporal
+        # stores, alone and combined, on the barrier-free blocks
+        for bl, rr, st, bwf, nbuf in ((1, 0, 0, 4, 2), (1, 0, 0, 4, 3), (0, 1, 0, 4, 2),
+                                      (0, 1, 0, 4, 3), (0, 1, 0, 4, 4), (0, 1, 0, 1, 2),
+                                      (1, 1, 0, 4, 2), (0, 0, 1, 4, 2), (1, 0, 1, 4, 2)):
+            for knob, v in ((b"signal_bl", bl), (b"signal_rr", rr), (b"signal_store", st),
+                            (b"signal_nbuf", nbuf), (b"signal_bwf", bwf)):
+                assert lib.csm_tune(knob, v) == 0
+            for J, skip in ((12, 1), (3, 0)):
+                got = engine.signal(Pd, ms, maxd, J, skip, with_pm=True, with_ret=True)
+                ref = base if (J, skip) == (12, 1) else None
+                if ref is None:
+                    for knob, v in ((b"signal_bl", 0), (b"signal_rr", 0), (b"signal_store", 0)):
+                        lib.csm_tune(knob, v)   # the clamped-load LDS-ring kernel
+                    ref = engine.signal(Pd, ms, maxd, J, skip, with_pm=True, with_ret=True)
+                for a, b in zip(got, ref):
+                    if a is not None:
+                        assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), \
+                            f"bl={bl} rr={rr} store={st} bwf={bwf} nbuf={nbuf} J={J} skip={skip}"
+        for knob, v in ((b"signal_bl", 1), (b"signal_rr", 0), (b"signal_store", 0)):
+            lib.csm_tune(knob, v)
         lib.csm_tune(b"signal_bwf", 0)
         lib.csm_tune(b"signal_nbuf", 4)
         assert lib.csm_tune(b"month_end_rows", maxd) == 0
@@ -296,7 +317,8 @@ def test_signal_kernel_variants_bit_identical(engine, name):
         assert bits_equal(PM.cpu().numpy(), base[0].cpu().numpy())
     finally:
         for knob, v in ((b"signal_mw", 0), (b"signal_bw", 1), (b"signal_store", 0),
-                        (b"month_end_rows", 0), (b"signal_bwf", 0), (b"signal_nbuf", 4)):
+                        (b"month_end_rows", 0), (b"signal_bwf", 0), (b"signal_nbuf", 4),
+                        (b"signal_bl", 1), (b"signal_rr", 0)):
             lib.csm_tune(knob, v)
 
 
