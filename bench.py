@@ -78,6 +78,9 @@ def parse():
                          "panels, C2, where launch gaps are a large share of the step)")
     ap.add_argument("--tune", action="append", default=[],
                     help="csm_tune key=value applied before the run (kernel A/B), repeatable")
+    ap.add_argument("--full-deciles", action="store_true",
+                    help="sweeps: overlapped returns of every decile (default: the two legs, "
+                         "all the summary table needs)")
     ap.add_argument("--no-decile-ids", action="store_true",
                     help="sweeps: rank from mom_J (streaming decile kernel) instead of the bucket "
                          "ids the multi-J scan writes (csm_momentum_multi_ids -> csm_deciles_ids)")
@@ -477,6 +480,19 @@ class TimedStages:
         return {k: (v[0] / steps, v[1] / steps) for k, v in agg.items()}
 
 
+def sweep_traffic(config, N, T_d, stage):
+    """HBM bytes per step of the dominant sweep stage from the committed PMC passes
+    (profiles/pmc_sweep_<config>.json, scripts/profile_sweep.sh), when they match this run."""
+    f = ROOT / "profiles" / f"pmc_sweep_{config}.json"
+    try:
+        pj = json.loads(f.read_text())
+        if pj.get("N") == N and pj.get("T_d") == T_d and pj.get("stage_label") == stage:
+            return pj.get("hbm_bytes_per_step")
+    except Exception:
+        pass
+    return None
+
+
 def sweep_main(args):
     """C3 / C5: the (J, K) sweep (SweepRunner) on one panel (C3, weak scaling: each rank its own
     panel) or on bootstrap panels (C5, strong scaling: the panels are split across ranks)."""
@@ -504,7 +520,8 @@ def sweep_main(args):
     apply_tunes(eng, args.tune)
     ts = TimedStages(eng)
     scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
-                             multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids)
+                             multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids,
+                             legs_only=not args.full_deciles)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":
@@ -581,7 +598,8 @@ def sweep_main(args):
                        "parallelism": f"{'panel' if args.config == 'c5' else 'replica'}-shard x{world}"},
             "roofline": {"bound": "hbm", "kernel": dname, "achieved": round(ach, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                         "traffic": None, "algorithmic_bytes_per_step": dbytes,
+                         "traffic": sweep_traffic(args.config, N, T_d, dname),
+                         "algorithmic_bytes_per_step": dbytes,
                          "avg_ms_per_step": round(dms, 4)},
             "pipeline_roofline": {"bound": "hbm", "achieved": round(alg_step / (ms_step * 1e-3) / 1e9, 1),
                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -28,6 +28,7 @@ EXPORTS = (
     "csm_last_present_month", "csm_portfolio_from_cohorts_multi", "csm_summary",
     "csm_shard_repair", "csm_signal_shard", "csm_shard_summary_state", "csm_momentum_multi",
     "csm_signal_ids", "csm_deciles_ids", "csm_pipeline", "csm_momentum_multi_ids",
+    "csm_cohort_sums_legs", "csm_portfolio_from_cohorts_legs",
 )
 
 
@@ -87,6 +88,10 @@ def _declare(lib):
         "csm_portfolio_from_cohorts_multi": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
                                                             _i32, _i32, _p, _f64, _f64, _f64, _p,
                                                             _p, _p, _p, _p, _p, _p, _p]),
+        "csm_cohort_sums_legs": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _p]),
+        "csm_portfolio_from_cohorts_legs": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
+                                                           _i32, _i32, _p, _f64, _f64, _f64, _p,
+                                                           _p, _p, _p, _p, _p, _p, _p, _p]),
         "csm_summary": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _f64, _p]),
         "csm_bootstrap": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64,
                                          _f64, _p, _p]),

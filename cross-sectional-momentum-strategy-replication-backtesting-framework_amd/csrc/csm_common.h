@@ -113,6 +113,15 @@ void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* 
                         int32_t* NV, int ablate, int64_t* tim, uint16_t* ids, int32_t* flg,
                         bool merged_only);
 
+// narrow rows with register-resident bucket ids (deciles_narrow.hip, RI mode): N even,
+// N <= deciles_narrow_reg_max_n(), 16-B aligned M / NR
+#define DEC_NREG_RI 5
+int deciles_narrow_reg_max_n();
+template <int NB>
+void launch_deciles_narrow_reg(int T_m, hipStream_t st, const double* M, const double* NR,
+                               int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
+                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
+
 // the same on narrow rows (deciles_narrow.hip: 1024 buckets = the fixed map's ids >> 3)
 template <int NB>
 void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,

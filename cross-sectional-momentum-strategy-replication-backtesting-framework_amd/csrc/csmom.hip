@@ -642,6 +642,105 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg(const double* __rest
   for (int q = 0; q < MJ_MAX; ++q)
     if (q < nJ && prev[q] >= 0) mj.NR[q][(int64_t)prev[q] * N + a] = NaN;
 }
+// Two adjacent assets per lane (a0 even): 16-B PM loads, mom_J / next_ret as one 16-B store
+// per row when both assets write the same row (as k_signal's scan_step_pair), ids as one 4-B
+// store: a wave moves 1 KiB per load / store instruction.  Same arithmetic per asset in the
+// same order as k_momentum_multi_reg: bit-identical outputs.  N even, 16-B aligned buffers.
+#define MJ2_CHUNK 8
+template <int RW>
+__global__ __launch_bounds__(256) void k_momentum_multi_reg2(const double* __restrict__ PM,
+                                                             int T_m, int64_t N, int nJ, int skip,
+                                                             MJSet mj) {
+  const int64_t a0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (a0 >= N) return;
+  const double NaN = qnan();
+  double f[2][RW];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int k = 0; k < RW; ++k) f[c][k] = NaN;
+  double pff[2] = {NaN, NaN};
+  double psff[2][MJ_MAX];
+  int prev[2][MJ_MAX], lo[MJ_MAX];
+#pragma unroll
+  for (int q = 0; q < MJ_MAX; ++q) {
+    psff[0][q] = psff[1][q] = NaN;
+    prev[0][q] = prev[1][q] = -1;
+    lo[q] = RW - mj.J[q] - skip;   // window = slots [lo, RW - skip)
+  }
+  const int hi = RW - skip;
+  for (int m0 = 0; m0 < T_m; m0 += MJ2_CHUNK) {
+    double2 buf[MJ2_CHUNK];
+#pragma unroll
+    for (int j = 0; j < MJ2_CHUNK; ++j)
+      buf[j] = (m0 + j < T_m) ? *reinterpret_cast<const double2*>(PM + (int64_t)(m0 + j) * N + a0)
+                              : make_double2(absent_val(), absent_val());
+#pragma unroll
+    for (int j = 0; j < MJ2_CHUNK; ++j) {
+      const int m = m0 + j;
+      if (m >= T_m) break;
+      const double xs[2] = {buf[j].x, buf[j].y};
+      const int64_t o = (int64_t)m * N + a0;
+      bool ab[2], xv[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const double x = xs[c];
+        ab[c] = is_absent(x);
+        xv[c] = x == x;
+        const double pnew = xv[c] ? x : pff[c];
+        const double ret = pnew / pff[c] - 1.0;
+        pff[c] = ab[c] ? pff[c] : pnew;
+#pragma unroll
+        for (int k = 0; k + 1 < RW; ++k) f[c][k] = ab[c] ? f[c][k] : f[c][k + 1];
+        f[c][RW - 1] = ab[c] ? f[c][RW - 1] : 1.0 + ret;
+      }
+#pragma unroll
+      for (int q = 0; q < MJ_MAX; ++q) {
+        if (q >= nJ) break;
+        double mom[2], vp[2];
+        int wp[2];
+        bool wc[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          double acc = 1.0;
+#pragma unroll
+          for (int k = 0; k < RW; ++k) acc = (k >= lo[q] && k < hi) ? acc * f[c][k] : acc;
+          mom[c] = ab[c] ? NaN : acc - 1.0;
+          const double ps_new = xv[c] ? xs[c] : psff[c][q];
+          wp[c] = (!ab[c] && prev[c][q] >= 0) ? prev[c][q] : -1;
+          vp[c] = ps_new / psff[c][q] - 1.0;
+          const bool ranked = mom[c] == mom[c];
+          wc[c] = !ranked;
+          psff[c][q] = ranked ? ps_new : psff[c][q];
+          prev[c][q] = ranked ? m : (ab[c] ? prev[c][q] : -1);
+        }
+        double* Mq = mj.M[q];
+        double* NRq = mj.NR[q];
+        *reinterpret_cast<double2*>(Mq + o) = make_double2(mom[0], mom[1]);
+        if (wp[0] >= 0 && wp[0] == wp[1]) {
+          *reinterpret_cast<double2*>(NRq + (int64_t)wp[0] * N + a0) = make_double2(vp[0], vp[1]);
+        } else {
+          if (wp[0] >= 0) NRq[(int64_t)wp[0] * N + a0] = vp[0];
+          if (wp[1] >= 0) NRq[(int64_t)wp[1] * N + a0 + 1] = vp[1];
+        }
+        if (wc[0] && wc[1]) {
+          *reinterpret_cast<double2*>(NRq + o) = make_double2(NaN, NaN);
+        } else {
+          if (wc[0]) NRq[o] = NaN;
+          if (wc[1]) NRq[o + 1] = NaN;
+        }
+        if (mj.IDS[q])
+          *reinterpret_cast<uint32_t*>(mj.IDS[q] + o) = csm_fid(mom[0]) | (csm_fid(mom[1]) << 16);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MJ_MAX; ++q)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (q < nJ && prev[c][q] >= 0) mj.NR[q][(int64_t)prev[c][q] * N + a0 + c] = NaN;
+}
+
 #define MJ_REG_W 16
 
 // =====================================================================================
@@ -1599,8 +1698,9 @@ static int g_tune_dec_ids = 0;
 // kernel fits two), so fewer loads are in flight per CU.  Measured C4 (461 dates): 0.57 vs
 // 0.33 ms; a 58-date shard: 0.235 vs 0.220 ms (profiles/r01/experiments/dec_reg_phases.log).
 static int g_tune_dec_reg = 0;
+static int g_tune_dec_nreg = 0;   // narrow rows <= 5120 assets: register-resident bucket ids (1 on)
 // csm_momentum_multi: 1 register shift ring when max(J) + skip <= 16, 0 the LDS ring
-static int g_tune_mj_reg = 1;
+static int g_tune_mj_reg = 2;   // 2: two assets per lane (C5 scan 37.7 -> 35.5 ms/step), 1: one
 // rows with at most this many assets take the narrow-row decile kernel (deciles_narrow.hip)
 static int64_t g_tune_dec_wave_max = 0;       // rows with at most this many assets: deciles_wave.hip
 static int64_t g_tune_dec_narrow_max = 16384;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
@@ -1619,8 +1719,9 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
   if (!strcmp(key, "dec_merge") && value >= 0 && value <= 2) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "dec_ids") && (value == 0 || value == 1)) { g_tune_dec_ids = value; return CSM_OK; }
-  if (!strcmp(key, "mj_reg") && (value == 0 || value == 1)) { g_tune_mj_reg = value; return CSM_OK; }
+  if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_reg") && value >= 0 && value <= 2) { g_tune_dec_reg = value; return CSM_OK; }
+  if (!strcmp(key, "dec_nreg") && (value == 0 || value == 1)) { g_tune_dec_nreg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
   if (!strcmp(key, "dec_wave_max") && value >= 0) { g_tune_dec_wave_max = value; return CSM_OK; }
   if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
@@ -1771,6 +1872,15 @@ static int momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N
   if (T_m == 0) return CSM_OK;
   const int tpb = SCAN_THREADS;
   const unsigned blocks = (unsigned)((N + tpb - 1) / tpb);
+  bool al = (N % 2) == 0 && aligned16(PM);
+  for (int q = 0; q < nJ; ++q)
+    al = al && aligned16(M[q]) && aligned16(NR[q]) && (!IDS || ((uintptr_t)IDS[q] & 3u) == 0);
+  if (W <= MJ_REG_W && g_tune_mj_reg == 2 && al) {   // register shift ring, two assets per lane
+    hipLaunchKernelGGL(k_momentum_multi_reg2<MJ_REG_W>, dim3((unsigned)((N / 2 + tpb - 1) / tpb)),
+                       dim3(tpb), 0, ctx->stream, PM, T_m, N, nJ, skip, mj);
+    LAUNCH_CHECK(ctx, "k_momentum_multi_reg2");
+    return CSM_OK;
+  }
   if (W <= MJ_REG_W && g_tune_mj_reg) {   // register shift ring
     hipLaunchKernelGGL(k_momentum_multi_reg<MJ_REG_W>, dim3(blocks), dim3(tpb), 0, ctx->stream,
                        PM, T_m, N, nJ, skip, mj);
@@ -2076,6 +2186,10 @@ static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, co
   }
   if (N <= g_tune_dec_wave_max && !ids) {     // the narrowest rows: one wave per row
     launch_deciles_wave<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
+    return;
+  }
+  if (N <= g_tune_dec_narrow_max && !ids && v2 && g_tune_dec_nreg && N <= deciles_narrow_reg_max_n()) {
+    launch_deciles_narrow_reg<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
     return;
   }
   if (N <= g_tune_dec_narrow_max && !ids) {   // rows of a few thousand assets (C2/C3/C5)

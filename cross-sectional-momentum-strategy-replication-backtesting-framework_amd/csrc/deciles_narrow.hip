@@ -9,6 +9,7 @@
 #define HB 1024
 #define CAP 1024     // candidates of the target buckets (refinement splits beyond)
 #define DEC_MINB 6   // 6 workgroups per CU (8: register spills, slower)
+#define DEC_MINB_RI 4   // register-id rows: 4 (6 spills)
 namespace dec_narrow {
 #include "deciles.inc"
 }  // namespace dec_narrow
@@ -25,6 +26,19 @@ void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, co
     hipLaunchKernelGGL((dec_narrow::k_deciles<NB, false, false>), dim3(T_m), dim3(DEC_THREADS), 0,
                        st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim, ids);
 }
+
+// rows of <= DEC_NREG_RI * 1024 assets (C5's 5k-asset bootstrap rows) with register-resident
+// bucket ids (RI mode): M is streamed once per row instead of up to three times; bit-identical
+// to the plain narrow kernel (lanes own the same cells)
+template <int NB>
+void launch_deciles_narrow_reg(int T_m, hipStream_t st, const double* M, const double* NR,
+                               int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
+                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim) {
+  hipLaunchKernelGGL((dec_narrow::k_deciles<NB, true, false, DEC_NREG_RI>), dim3(T_m),
+                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
+                     (uint16_t*)nullptr);
+}
+int deciles_narrow_reg_max_n() { return DEC_NREG_RI * 4 * DEC_THREADS; }
 
 // the fused sweep path on bucket ids (csm_momentum_multi_ids -> csm_deciles_ids on rows of
 // <= dec_narrow_max assets): merged pass, then the general PRE kernel for the rows it leaves
@@ -48,6 +62,9 @@ void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const d
                                               int64_t, int, const QTab&, int8_t*, double*,       \
                                               int32_t*, int32_t*, int, int64_t*, uint16_t*,       \
                                               int32_t*, bool);                                   \
+  template void launch_deciles_narrow_reg<NB>(int, hipStream_t, const double*, const double*,  \
+                                              int64_t, int, const QTab&, int8_t*, double*,       \
+                                              int32_t*, int32_t*, int, int64_t*);                \
   template void launch_deciles_narrow<NB>(bool, int, hipStream_t, const double*, const double*,  \
                                           int64_t, int, const QTab&, int8_t*, double*,           \
                                           int32_t*, int32_t*, int, int64_t*);

@@ -237,11 +237,14 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
 // contributes nothing): the gather loop needs no per-element bounds test.  Row stride:
 __host__ __device__ __forceinline__ int64_t seg_stride(int64_t N) { return ((N + 3) & ~3LL) + 128; }
 #define SEG_MAXN 7168   // VW sort stages 9 bytes per cell in LDS: <= 64 KB per workgroup
-template <int NB, bool VW>
+// LEGS: only the two legs (deciles 0 and NB - 1) are sorted -- the sweeps' long-short needs
+// nothing else -- the other deciles get empty segments.
+template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
     const int8_t* __restrict__ L, const double* __restrict__ W, int64_t N, int C,
     uint16_t* __restrict__ PERM, int32_t* __restrict__ OFF, double* __restrict__ WSRT,
     double* __restrict__ FWp) {
+  auto is_leg = [](int d) { return !LEGS || d == 0 || d == NB - 1; };
   const int64_t PS = seg_stride(N);
   // the row is staged in LDS first (all loads in flight at once), then both passes read LDS
   extern __shared__ double wl[];                  // VW: weights [N], then labels [N]
@@ -280,7 +283,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
     const int64_t a = a0 + lane;
     const int lab = a < q1 ? (int)ll[a] : -1;
 #pragma unroll
-    for (int d = 0; d < NB; ++d) cnt[d] += __popcll(__ballot(lab == d));
+    for (int d = 0; d < NB; ++d)
+      if (is_leg(d)) cnt[d] += __popcll(__ballot(lab == d));
   }
   if (lane == 0) {
 #pragma unroll
@@ -321,13 +325,20 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
   double ft = 0.0, fb = 0.0;
   for (int64_t a0 = q0; a0 < q1; a0 += 64) {
     const int64_t a = a0 + lane;
-    const int lab = a < q1 ? (int)ll[a] : -1;
-    uint64_t same = __ballot(lab >= 0);
+    int lab = a < q1 ? (int)ll[a] : -1;
+    if (LEGS && !is_leg(lab)) lab = -1;
+    uint64_t same;
+    if (LEGS) {   // two labels: one ballot each
+      const uint64_t m0 = __ballot(lab == 0), m1 = __ballot(lab == NB - 1);
+      same = lab == 0 ? m0 : m1;
+    } else {
+      same = __ballot(lab >= 0);
 #pragma unroll
-    for (int bb = 0; bb < NBITS; ++bb) {
-      const bool bit = (lab >> bb) & 1;
-      const uint64_t m = __ballot(bit);
-      same &= bit ? m : ~m;
+      for (int bb = 0; bb < NBITS; ++bb) {
+        const bool bit = (lab >> bb) & 1;
+        const uint64_t m = __ballot(bit);
+        same &= bit ? m : ~m;
+      }
     }
     int pos = -1;
     if (lab >= 0) {
@@ -373,11 +384,15 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
 // trip to L2 covers a typical segment.
 #define SEG_G 16
 #define SEG_MAXKD 512   // K * (n_bins + 1) offsets staged in LDS
-template <int NB, bool VW>
+// LEGS: the (age, leg) segments only (ND = 2 per age: deciles 0 and NB - 1); the partial
+// slots of the other deciles are not written (k_overlap skips them).
+template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const double* __restrict__ NR, const uint16_t* __restrict__ PERM,
     const int32_t* __restrict__ OFF, const double* __restrict__ WSRT, int T_m, int B, int64_t N,
     int K, int C, int Cs, int xcd, double* __restrict__ SWRp, double* __restrict__ SWp) {
+  constexpr int ND = LEGS ? 2 : NB;   // segments per age
+  auto dec_of = [](int e) { return LEGS ? (e ? NB - 1 : 0) : e; };
   extern __shared__ double rl[];   // the return row of month t (N values), NaN at slot N
   __shared__ int32_t offs[SEG_MAXKD];
   int c = 0;
@@ -402,8 +417,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   const int grp = tid / SEG_G, sl = tid % SEG_G;
   const int kmax = t + 1 < K ? t + 1 : K;
   if (c >= Cs) {   // chunks beyond the Cs working ones only hold zeros
-    for (int g = tid; g < K * NB; g += PF_THREADS) {
-      const int k = g / NB, d = g - k * NB;
+    for (int g = tid; g < K * ND; g += PF_THREADS) {
+      const int k = g / ND, d = dec_of(g - k * ND);
       const int64_t ob = ((tb * K + k) * C + c) * NB + d;
       SWRp[ob] = 0.0;
       SWp[ob] = 0.0;
@@ -422,9 +437,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   // working chunk c < Cs owns the segments g = c (mod Cs) whole and writes zeros for the
   // others (exact under the chunk-order sum of k_overlap); each working chunk stages the
   // whole return row, so Cs stays small
-  for (int g = tid; g < K * NB && Cs > 1; g += PF_THREADS) {
+  for (int g = tid; g < K * ND && Cs > 1; g += PF_THREADS) {
     if (g % Cs == c) continue;
-    const int k = g / NB, d = g - k * NB;
+    const int k = g / ND, d = dec_of(g - k * ND);
     const int64_t ob = ((tb * K + k) * C + c) * NB + d;
     SWRp[ob] = 0.0;
     SWp[ob] = 0.0;
@@ -442,7 +457,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   };
   auto seg_at = [&](int g) {
     Seg q;
-    const int k = g / NB, d = g - k * NB;
+    const int k = g / ND, d = dec_of(g - k * ND);
     q.ob = ((tb * K + k) * C + c) * NB + d;
     q.live = k < kmax;
     const int64_t srow = tb - (int64_t)(q.live ? k : 0) * B;
@@ -494,8 +509,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   };
   // two segments per group at a time: both segments' first trips of ids are in flight
   // together (a typical segment is one trip), then any further trips one by one
-  for (int g = c + grp * Cs; g < K * NB; g += 2 * gstep) {
-    const bool two = g + gstep < K * NB;
+  for (int g = c + grp * Cs; g < K * ND; g += 2 * gstep) {
+    const bool two = g + gstep < K * ND;
     const Seg q1 = seg_at(g), q2 = seg_at(two ? g + gstep : g);
     const int64_t a1 = q1.w0 + sl, a2 = q2.w0 + sl;
     uint64_t v1[U], v2[U];
@@ -888,12 +903,15 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
 __global__ __launch_bounds__(64) void k_overlap(
     const double* __restrict__ SWRp, const double* __restrict__ SWp, KSet ks, int Kmax, int C,
     int nb, const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
-    int64_t rows, double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST) {
+    int64_t rows, double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST,
+    int legs) {
   const int64_t tb = blockIdx.x;
   const int q = blockIdx.y;
   const int K = ks.K[q];
   const int d = threadIdx.x;
-  if (d < nb) {
+  if (legs && d < nb && d != 0 && d != nb - 1) {   // legs-only cohort sums: not computed
+    PR[(q * rows + tb) * nb + d] = qnan();
+  } else if (d < nb) {
     double acc = 0.0;
     int n = 0;
     for (int k = 0; k < K; ++k) {
@@ -928,10 +946,12 @@ __global__ __launch_bounds__(64) void k_overlap(
 }
 
 // one workgroup per (panel b, holding period q): the reference's long-short rule on PR[q].
+// need_full (legs-only accounting): set when a panel lacks one leg's column, where the rule
+// falls back to max - min over every decile (the caller reruns with every decile).
 __global__ __launch_bounds__(256) void k_ls(const double* __restrict__ PR, int T_m, int B, int nb,
                                             double* __restrict__ LS,
                                             const double* __restrict__ COST,
-                                            double* __restrict__ NET) {
+                                            double* __restrict__ NET, int32_t* __restrict__ need_full) {
   const int b = blockIdx.x;
   const int64_t qo = (int64_t)blockIdx.y * T_m * B;
   PR += qo * nb;
@@ -950,6 +970,7 @@ __global__ __launch_bounds__(256) void k_ls(const double* __restrict__ PR, int T
   if (hi) atomicOr(&has_hi, 1);
   __syncthreads();
   const bool both = has_lo && has_hi;
+  if (need_full && !both && threadIdx.x == 0) atomicOr(need_full, 1);
   for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
     const int64_t tb = (int64_t)t * B + b;
     const double* e = PR + tb * nb;
@@ -1074,7 +1095,7 @@ template <int NB>
 static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
                           const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
                           double* SWp, double* FWp, char* segws, int64_t perm_b, int64_t off_b,
-                          int64_t wsrt_b) {
+                          int64_t wsrt_b, bool legs = false) {
   const dim3 g((unsigned)(pl.C * T_m * B), 1u, pl.kpar ? (unsigned)K : 1u);
   if (g_tune_cohort_seg && segws && !pl.kpar && K * (NB + 1) <= SEG_MAXKD) {
     uint16_t* PERM = (uint16_t*)(segws + perm_b);
@@ -1086,7 +1107,21 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     const dim3 g1((unsigned)(T_m * B)),
         g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(pl.C * T_m * B));
     const size_t lds = (size_t)(N + 1) * sizeof(double);
-    if (W) {
+    if (legs) {
+      if (W) {
+        hipLaunchKernelGGL((k_label_sort<NB, true, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N,
+                           pl.C, PERM, OFF, WSRT, FWp);
+        hipLaunchKernelGGL((k_cohort_seg<NB, true, true>), g2, dim3(PF_THREADS), lds, st, NR,
+                           (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
+                           N, K, pl.C, Cs, xcd, SWRp, SWp);
+      } else {
+        hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N,
+                           pl.C, PERM, OFF, WSRT, FWp);
+        hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR,
+                           (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
+                           N, K, pl.C, Cs, xcd, SWRp, SWp);
+      }
+    } else if (W) {
       hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
       hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR,
@@ -1170,8 +1205,9 @@ int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bin
   return pf_layout(T_m, B, N, n_bins, K).bytes;
 }
 
-int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
-                    int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, void* workspace) {
+static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,
+                       int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
+                       void* workspace, bool legs) {
   int r = prep(ctx);
   if (r) return r;
   if (!L || !NR || !workspace || T_m < 0 || B < 1 || N <= 0 || Kmax < 1 || Kmax > TO_MAXK ||
@@ -1183,7 +1219,7 @@ int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const doubl
   double* ws = (double*)workspace;
   hipStream_t st = ctx->stream;
   switch (n_bins) {
-#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b); break;
+#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b, legs); break;
     PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20) PF_CASE(30)
 #undef PF_CASE
     default:
@@ -1196,12 +1232,27 @@ int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const doubl
   return CSM_OK;
 }
 
-int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double* W,
-                                     int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
-                                     int32_t Kmax, int32_t nK, const int32_t* Ks,
-                                     double half_spread, double k_impact, double aum,
-                                     const double* ADV, const double* SIG, double* PR, double* LS,
-                                     double* TURN, double* COST, double* NET, void* workspace) {
+int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
+                    int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, void* workspace) {
+  return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, false);
+}
+
+int csm_cohort_sums_legs(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,
+                         int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
+                         void* workspace) {
+  if (N > SEG_MAXN)
+    return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_legs: rows of <= %d assets (N=%lld)", SEG_MAXN,
+                   (long long)N);
+  return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, true);
+}
+
+static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W,
+                                  int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
+                                  int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                  double half_spread, double k_impact, double aum,
+                                  const double* ADV, const double* SIG, double* PR, double* LS,
+                                  double* TURN, double* COST, double* NET, void* workspace,
+                                  bool legs, int32_t* need_full) {
   int r = prep(ctx);
   if (r) return r;
   bool ks_ok = Ks && nK >= 1;
@@ -1245,14 +1296,37 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
                        (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks, Kmax,
                        lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
                        (const double*)(ws + lay.cost), lay.p.Ct, (int64_t)lay.rows, PRq, TURNq,
-                       COSTq);
+                       COSTq, legs ? 1 : 0);
     LAUNCH_CHECK(ctx, "k_overlap");
     hipLaunchKernelGGL(k_ls, dim3((unsigned)B, (unsigned)ks.n), dim3(256), 0, st,
                        (const double*)PRq, T_m, B, n_bins, LS + q0 * rb, (const double*)COSTq,
-                       NETq);
+                       NETq, legs ? need_full : nullptr);
     LAUNCH_CHECK(ctx, "k_ls");
   }
   return CSM_OK;
+}
+
+int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double* W,
+                                     int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
+                                     int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                     double half_spread, double k_impact, double aum,
+                                     const double* ADV, const double* SIG, double* PR, double* LS,
+                                     double* TURN, double* COST, double* NET, void* workspace) {
+  return portfolio_from_cohorts(ctx, L, W, T_m, B, N, n_bins, Kmax, nK, Ks, half_spread, k_impact,
+                                aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace, false, nullptr);
+}
+
+int csm_portfolio_from_cohorts_legs(csm_ctx* ctx, const int8_t* L, const double* W,
+                                    int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
+                                    int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                    double half_spread, double k_impact, double aum,
+                                    const double* ADV, const double* SIG, double* PR, double* LS,
+                                    double* TURN, double* COST, double* NET, void* workspace,
+                                    int32_t* need_full) {
+  if (!need_full)
+    return set_err(ctx, CSM_E_INVAL, "csm_portfolio_from_cohorts_legs: need_full is required");
+  return portfolio_from_cohorts(ctx, L, W, T_m, B, N, n_bins, Kmax, nK, Ks, half_spread, k_impact,
+                                aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace, true, need_full);
 }
 
 int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, int32_t T_m,

@@ -504,9 +504,15 @@ class Engine:
 
     def portfolio_multi(self, L, NR, n_bins=10, Ks=(1,), W=None, B=1, half_spread=0.0005,
                         k_impact=0.1, aum=0.0, ADV=None, SIG=None, with_costs=True,
-                        workspace=None, return_stacked=False):
+                        workspace=None, return_stacked=False, legs_only=False, need_full=None):
         """One cohort-sum pass (csm_cohort_sums, Kmax = max(Ks)) shared by the accounting of
-        every holding period K in Ks (csm_portfolio_from_cohorts).  Returns {K: PortfolioOut}."""
+        every holding period K in Ks (csm_portfolio_from_cohorts).  Returns {K: PortfolioOut}.
+        legs_only (rows of <= 7168 assets): sort and sum only deciles 0 and n_bins - 1
+        (csm_cohort_sums_legs / csm_portfolio_from_cohorts_legs): LS / TURN / COST / NET bit for
+        bit the full path's, PR NaN outside the legs.  When a panel lacks one leg's column (the
+        long-short rule then needs every decile) the full path is rerun (one device sync); with
+        need_full (device int32 [1], caller-zeroed) the flag is left there instead, no sync, and
+        the caller reruns with legs_only=False when it is set."""
         T_m, BN = L.shape
         if B < 1 or BN % B:
             raise ValueError(f"row width {BN} is not B={B} panels")
@@ -518,21 +524,31 @@ class Engine:
                 _need(t, nm, torch.float64, (T_m, BN), self.device)
         Ks = [int(k) for k in Ks]
         Kmax = max(Ks)
+        legs_only = bool(legs_only) and N <= 7168
         nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, N, int(n_bins), Kmax))
         if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
             workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
-        self._call("csm_cohort_sums", _ptr(L), _ptr(NR), _ptr(W), T_m, int(B), N, int(n_bins),
-                   Kmax, _ptr(workspace))
+        self._call("csm_cohort_sums_legs" if legs_only else "csm_cohort_sums", _ptr(L), _ptr(NR),
+                   _ptr(W), T_m, int(B), N, int(n_bins), Kmax, _ptr(workspace))
         nK = len(Ks)
         PR, LS = self.empty((nK, T_m, B, n_bins)), self.empty((nK, T_m, B))
         TURN = self.empty((nK, T_m, B)) if with_costs else None
         COST = self.empty((nK, T_m, B)) if with_costs else None
         NET = self.empty((nK, T_m, B)) if with_costs else None
         ks = (ctypes.c_int32 * nK)(*Ks)
-        self._call("csm_portfolio_from_cohorts_multi", _ptr(L), _ptr(W), T_m, int(B), N,
-                   int(n_bins), Kmax, nK, ctypes.cast(ks, ctypes.c_void_p), float(half_spread),
-                   float(k_impact), float(aum), _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS),
-                   _ptr(TURN), _ptr(COST), _ptr(NET), _ptr(workspace))
+        args = (_ptr(L), _ptr(W), T_m, int(B), N, int(n_bins), Kmax, nK,
+                ctypes.cast(ks, ctypes.c_void_p), float(half_spread), float(k_impact), float(aum),
+                _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS), _ptr(TURN), _ptr(COST), _ptr(NET),
+                _ptr(workspace))
+        if legs_only:
+            flag = (torch.zeros(1, dtype=torch.int32, device=self.device) if need_full is None
+                    else need_full)
+            self._call("csm_portfolio_from_cohorts_legs", *args, _ptr(flag))
+            if need_full is None and int(flag.item()):   # a panel lacks a leg's column
+                return self.portfolio_multi(L, NR, n_bins, Ks, W, B, half_spread, k_impact, aum,
+                                            ADV, SIG, with_costs, workspace, return_stacked)
+        else:
+            self._call("csm_portfolio_from_cohorts_multi", *args)
         pick = lambda x, q: None if x is None else x[q]
         res = {K: PortfolioOut(PR=PR[q], LS=LS[q], TURN=pick(TURN, q), COST=pick(COST, q),
                                NET=pick(NET, q)) for q, K in enumerate(Ks)}

@@ -95,6 +95,10 @@ class SweepConfig:
     # rows from them (csm_momentum_multi_ids -> csm_deciles_ids): 2-B ids per cell instead of
     # up to three passes over mom_J; same labels
     decile_ids: bool = True
+    # accounting of the two legs only (deciles 0 and n_bins - 1): the summary table (LS, TURN,
+    # COST, NET) is bit for bit the full path's; the per-strategy series' PR holds the legs
+    # (NaN elsewhere).  False: every decile's overlapped return
+    legs_only: bool = True
     extra: dict = field(default_factory=dict)
 
     @property
@@ -118,6 +122,15 @@ class SweepRunner:
     def run_batch(self, PMb: torch.Tensor, B: int, W=None, ADV=None, SIG=None):
         """PMb [T_m][B*N] month prices of B panels -> summary [B][S][F] and the per-strategy
         long-short series {(J, K): PortfolioOut}."""
+        c = self.cfg
+        legs = c.legs_only and hasattr(self.st, "summary")
+        flag = torch.zeros(1, dtype=torch.int32, device=PMb.device) if legs else None
+        out = self._run_batch(PMb, B, W, ADV, SIG, flag)
+        if legs and int(flag.item()):   # a panel lacks a leg's column: every decile (rare)
+            out = self._run_batch(PMb, B, W, ADV, SIG, None)
+        return out
+
+    def _run_batch(self, PMb, B, W, ADV, SIG, flag):
         c, st = self.cfg, self.st
         T_m, BN = PMb.shape
         N = BN // B
@@ -154,7 +167,11 @@ class SweepRunner:
             del M, IDS
             L = L.reshape(T_m, BN)
             if hasattr(st, "summary"):   # device path: one cohort pass for every K of this J,
-                outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)
+                if flag is not None:
+                    kw2 = dict(kw, legs_only=True, need_full=flag)
+                else:
+                    kw2 = kw
+                outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw2)
                 summ_j = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # summaries on device
                 for q, K in enumerate(c.Ks):
                     summ[(J, K)] = summ_j[q]

@@ -45,7 +45,8 @@ int csm_abi_version(void);
  * general kernel for the rows it leaves | 0: the general kernel only | 2: test hook, the merged
  * kernel only -- rows it leaves are not written), "dec_reg" (0 off | 1 when T_m <= CUs | 2 always: register-resident bucket ids,
  * bit-identical), "dec_narrow_max" (widest row for the narrow-row decile kernel),
- * "mj_reg" (csm_momentum_multi: 1 register shift ring when max(J) + skip <= 16, the default;
+ * "mj_reg" (csm_momentum_multi: 2 register shift ring with two assets per lane (16-B rows;
+ * even N, aligned buffers), 1 register shift ring when max(J) + skip <= 16, the default;
  * 0 the shared-memory ring), "month_end_rows" (0 off | max month days: one-shot month-end
  * kernel), "signal_bw" (1|2|4 waves per fused-kernel workgroup), "signal_bwf" (0 auto:
  * 4 waves x 2 month buffers when N >= 92160, else 1 | 1..4 waves per fused-kernel workgroup with
@@ -323,6 +324,27 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
                                      double half_spread, double k_impact, double aum,
                                      const double* ADV, const double* SIG, double* PR, double* LS,
                                      double* TURN, double* COST, double* NET, void* workspace);
+
+/*
+ * Legs-only accounting for sweeps whose outputs are the long-short statistics (SweepRunner:
+ * LS / TURN / COST / NET per strategy): csm_cohort_sums_legs sorts and sums only the two legs
+ * (deciles 0 and n_bins - 1; rows of <= 7168 assets), csm_portfolio_from_cohorts_legs takes the
+ * multi-K accounting from them -- LS, TURN, COST and NET equal the full path's bit for bit, PR
+ * holds the two legs (NaN elsewhere).  The reference's long-short rule needs every decile only
+ * when a panel lacks one leg's column (run_demo.py:60-65): then *need_full (device int32, set to
+ * 0 by the caller) becomes 1 and the caller reruns the full csm_cohort_sums /
+ * csm_portfolio_from_cohorts_multi.
+ */
+int csm_cohort_sums_legs(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,
+                         int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
+                         void* workspace);
+int csm_portfolio_from_cohorts_legs(csm_ctx* ctx, const int8_t* L, const double* W,
+                                    int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
+                                    int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                    double half_spread, double k_impact, double aum,
+                                    const double* ADV, const double* SIG, double* PR, double* LS,
+                                    double* TURN, double* COST, double* NET, void* workspace,
+                                    int32_t* need_full);
 
 /*
  * Performance summary per (strategy, panel) of stacked long-short series (LS, and the

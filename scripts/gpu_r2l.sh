@@ -1,0 +1,11 @@
+#!/bin/bash
+# narrow register-id decile rows: tests + C5 A/B (ids path vs streaming vs register ids)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_pipeline.py -m gpu -x -q --timeout 200 --timeout-method thread -k "narrow" > gpurun_out/gpu_tests_nreg.log 2>&1
+rc=$?; tail -1 gpurun_out/gpu_tests_nreg.log; [ $rc -eq 0 ] || exit $rc
+for v in "--no-decile-ids --tune dec_nreg=1" "" "--no-decile-ids"; do
+  timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline $v > gpurun_out/bench_c5_nreg.log 2>&1
+  rc=$?; echo "[$v]"; grep -o '"ms_per_step": [0-9.]*\|"stage_ms": {[^}]*}' gpurun_out/bench_c5_nreg.log | tr '\n' ' '; echo; [ $rc -eq 0 ] || exit $rc
+done

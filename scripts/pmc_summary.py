@@ -61,6 +61,13 @@ def main():
     ap.add_argument("--emit", nargs="*", default=[])
     ap.add_argument("--emit-dir", default=None)
     ap.add_argument("--source", default="", help="where the committed summary will live")
+    ap.add_argument("--stage", default=None,
+                    help="sweeps: NAME=k1,k2,... -> pmc_sweep_<config>.json with the stage's HBM "
+                         "bytes per step (all dispatches of those kernels / --step-runs)")
+    ap.add_argument("--stage-label", default="", help="the bench's stage_ms key of that stage")
+    ap.add_argument("--config", default="")
+    ap.add_argument("--step-runs", type=int, default=0,
+                    help="steps the PMC runs executed (warmup + steps)")
     a = ap.parse_args()
     stats = read_stats(os.path.join(a.prof_dir, "trace"))
     fetch = read_counters(os.path.join(a.prof_dir, "pmc_fetch"))
@@ -90,6 +97,16 @@ def main():
                    "source": a.source}
             with open(os.path.join(a.emit_dir or a.prof_dir, f"pmc_{k}.json"), "w") as fh:
                 json.dump(out, fh, indent=1)
+    if a.stage and a.step_runs > 0:
+        name, ks = a.stage.split("=")
+        ks = ks.split(",")
+        tot = sum(kern[k]["hbm_bytes_corrected"] * kern[k]["dispatches"] for k in ks if k in kern)
+        out = {"config": a.config, "N": a.N, "T_d": a.T_d, "stage": name,
+               "stage_label": a.stage_label, "kernels": ks, "step_runs": a.step_runs,
+               "hbm_bytes_per_step": tot / a.step_runs, "source": a.source}
+        with open(os.path.join(a.emit_dir or a.prof_dir, f"pmc_sweep_{a.config}.json"), "w") as fh:
+            json.dump(out, fh, indent=1)
+        print(json.dumps(out))
     print(json.dumps({k: (v["hbm_bytes_corrected"], stats.get(k, {}).get("avg_ns"))
                       for k, v in kern.items()}))
 

@@ -437,7 +437,7 @@ def test_momentum_multi_equals_per_J_scans(engine, name, Js, skip):
     J bit for bit -- M and the J-dependent NR -- including > 4 look-backs (two launches)."""
     z = load_golden(name)
     PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
-    for mj_reg in (1, 0):   # register shift ring (max J + skip <= 16) and the LDS ring
+    for mj_reg in (2, 1, 0):   # register shift ring (two assets per lane / one) and the LDS ring
         assert engine.lib.csm_tune(b"mj_reg", mj_reg) == 0
         try:
             outs = engine.momentum_multi(PM, Js, skip)

@@ -297,18 +297,31 @@ def _month_panel(N, T_m, seed):
     return pm
 
 
+MJ_REG_DEFAULT = 1
+
+
 def test_momentum_multi_ids_bit_identical(engine):
     """The id-writing multi-J scan: M / NR equal the plain multi-J scan bit for bit, and every
     id is the fixed map of its mom_J."""
     pm = _month_panel(3_000, 300, 5)
     PM = _up(pm)
     Js = (3, 6, 9, 12)
-    plain = engine.momentum_multi(PM, Js, 1)
-    with_ids = engine.momentum_multi(PM, Js, 1, with_ids=True)
-    for (M0, NR0), (M1, NR1, IDS) in zip(plain, with_ids):
-        assert bits_equal(M1.cpu().numpy(), M0.cpu().numpy())
-        assert bits_equal(NR1.cpu().numpy(), NR0.cpu().numpy())
-        assert np.array_equal(IDS.cpu().numpy().view(np.uint16), fixed_ids(M0.cpu().numpy()))
+    lib = engine.lib
+    try:
+        assert lib.csm_tune(b"mj_reg", 1) == 0
+        plain = engine.momentum_multi(PM, Js, 1)
+        for mj_reg in (2, 1, 0):   # two assets per lane, one, the LDS ring
+            assert lib.csm_tune(b"mj_reg", mj_reg) == 0
+            with_ids = engine.momentum_multi(PM, Js, 1, with_ids=True)
+            for (M0, NR0), (M1, NR1, IDS) in zip(plain, with_ids):
+                assert bits_equal(M1.cpu().numpy(), M0.cpu().numpy()), mj_reg
+                assert bits_equal(NR1.cpu().numpy(), NR0.cpu().numpy()), mj_reg
+                assert np.array_equal(IDS.cpu().numpy().view(np.uint16), fixed_ids(M0.cpu().numpy()))
+            for (M0, NR0), (M1, NR1) in zip(plain, engine.momentum_multi(PM, Js, 1)):
+                assert bits_equal(M1.cpu().numpy(), M0.cpu().numpy()), mj_reg
+                assert bits_equal(NR1.cpu().numpy(), NR0.cpu().numpy()), mj_reg
+    finally:
+        lib.csm_tune(b"mj_reg", MJ_REG_DEFAULT)
 
 
 @pytest.mark.parametrize("width", [4_000, 5_000, 16_384])
@@ -353,3 +366,31 @@ def test_sweep_batch_ids_equal_streaming(engine):
     a, _ = SweepRunner(engine, SweepConfig()).run_batch(PMb, B)
     b, _ = SweepRunner(engine, SweepConfig(decile_ids=False)).run_batch(PMb, B)
     assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+@pytest.mark.parametrize("width", [1_000, 4_000, 5_000, 5_120])
+def test_narrow_register_ids_bit_identical(engine, width):
+    """dec_nreg (rows <= 5120 assets keep their bucket ids in registers, M streamed once): labels,
+    counts, ranked rows and decile means equal the plain narrow kernel's bit for bit, and the
+    labels the oracle's qcut, on every stress case."""
+    lib = engine.lib
+    rng = np.random.default_rng(width + 1)
+    x = np.stack([_stress_row(c, n=width) for c in MERGE_CASES + ["lognormal_mild"] * 3])
+    nr = rng.normal(0.01, 0.1, x.shape)
+    nr[rng.random(x.shape) < 0.03] = np.nan
+    M, NR = _up(x), _up(nr)
+    base = engine.deciles(M, NR, 10, with_nv=True)
+    try:
+        assert lib.csm_tune(b"dec_nreg", 1) == 0
+        got = engine.deciles(M, NR, 10, with_nv=True)
+        lab_only = engine.deciles(M, None, 10)[0]
+    finally:
+        lib.csm_tune(b"dec_nreg", 0)
+    for a, b in zip(got, base):
+        if a.dtype == torch.float64:
+            assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+        else:
+            assert torch.equal(a, b)
+    assert torch.equal(lab_only, got[0])
+    refL = np.stack([_oracle_labels(x[r]) for r in range(x.shape[0])])
+    assert np.array_equal(got[0].cpu().numpy(), refL)

@@ -339,3 +339,55 @@ def test_portfolio_many_rows(engine, mode):
     _close(out.PR, ref["PR"], "PR")
     _close(out.TURN, ref["TURN"], "TURN")
     _close(out.NET, ref["NET"], "NET")
+
+
+@pytest.mark.parametrize("vw", [False, True])
+@pytest.mark.parametrize("B,n_bins", [(1, 10), (6, 10), (4, 3)])
+def test_legs_only_equals_full(engine, vw, B, n_bins):
+    """Legs-only accounting (csm_cohort_sums_legs + csm_portfolio_from_cohorts_legs: only
+    deciles 0 and n_bins - 1 sorted and summed) gives the full path's LS / TURN / COST / NET bit
+    for bit and its PR on the two legs; the other deciles are NaN."""
+    L, NR, _, PM = _labels(engine, "c1")
+    if n_bins != 10:
+        _, M, NR = engine.momentum(PM, 12, 1)
+        L, _, _, _ = engine.deciles(M, None, n_bins)
+    T_m, N = L.shape
+    W = _up(np.abs(PM.cpu().numpy()) * 1e6) if vw else None
+    if B > 1:
+        rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 5 * i, axis=1) for i in range(B)],
+                                     axis=1).reshape(T_m, B * N))
+        L, NR = rep(L), rep(NR)
+        W = rep(W) if vw else None
+    rng = np.random.default_rng(B)
+    ADV = _up(rng.uniform(1e5, 1e8, (T_m, B * N)))
+    kw = dict(Ks=(3, 6, 12), W=W, B=B, aum=5e6, ADV=ADV)
+    full = engine.portfolio_multi(L, NR, n_bins, **kw)
+    legs = engine.portfolio_multi(L, NR, n_bins, legs_only=True, **kw)
+    for K in (3, 6, 12):
+        for f in ("LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(legs[K], f).cpu().numpy(), getattr(full[K], f).cpu().numpy()), (K, f)
+        a, b = legs[K].PR.cpu().numpy(), full[K].PR.cpu().numpy()
+        for d in (0, n_bins - 1):
+            assert bits_equal(a[..., d], b[..., d]), (K, d)
+        assert np.isnan(a[..., 1:n_bins - 1]).all()
+
+
+def test_legs_only_falls_back_when_a_leg_column_is_missing(engine):
+    """A panel whose top decile never occurs: the long-short rule takes max - min over every
+    decile (run_demo.py:60-65), so the legs-only call reruns the full accounting -- the result
+    equals the full path bit for bit, PR included -- and the sweep's deferred flag does too."""
+    L, NR, _, _ = _labels(engine, "c1")
+    Lh = L.cpu().numpy().copy()
+    Lh[Lh == 9] = 8
+    L2 = _up(Lh)
+    full = engine.portfolio_multi(L2, NR, 10, Ks=(3, 12))
+    legs = engine.portfolio_multi(L2, NR, 10, Ks=(3, 12), legs_only=True)
+    for K in (3, 12):
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(legs[K], f).cpu().numpy(), getattr(full[K], f).cpu().numpy()), (K, f)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    engine.portfolio_multi(L2, NR, 10, Ks=(3, 12), legs_only=True, need_full=flag)
+    assert int(flag.item()) == 1
+    flag.zero_()
+    engine.portfolio_multi(L, NR, 10, Ks=(3, 12), legs_only=True, need_full=flag)
+    assert int(flag.item()) == 0

@@ -72,7 +72,7 @@ def test_tune_keys_documented_in_header_are_accepted():
     cases = {b"signal_vec": ([1, 2], 2), b"signal_nbuf": ([2, 3, 4], 4), b"dec_ablate": ([0, 1], 0),
              b"signal_bwf": ([0, 1, 2, 3, 4], 0),
              b"dec_ids": ([0, 1], 0), b"dec_reg": ([0, 1, 2], 0),
-             b"dec_narrow_max": ([0, 16384], 16384), b"mj_reg": ([0, 1], 1),
+             b"dec_narrow_max": ([0, 16384], 16384), b"mj_reg": ([0, 1, 2], 1),
              b"signal_store": ([0, 1, 2, 3, 4], 0), b"signal_rr": ([0, 1], 0),
              b"signal_bl": ([0, 1], 1)}
     for key, (vals, default) in cases.items():
