@@ -122,7 +122,7 @@ void launch_deciles_narrow_reg(int T_m, hipStream_t st, const double* M, const d
                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                                int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
 
-// the same on narrow rows (deciles_narrow.hip: 1024 buckets = the fixed map's ids >> 3)
+// the same on narrow rows (deciles_npre.hip: 2048 buckets = the fixed map's ids >> 2)
 template <int NB>
 void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,

@@ -1998,15 +1998,21 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   // raw buffer loads (padding rows out of range): rows of at most 2 GiB / 32
   const bool bl = bwf_ok && g_tune_signal_bl && N * 8 * 32 < ((int64_t)1 << 31) &&
                   bwf == 4 && (nbf == 2 || nbf == 3);
-  const int bw = noscan ? 4 : bwf_ok ? bwf
+  // speculative shards: the same 4-wave x 2-buffer blocks with buffer loads when they apply
+  const bool sh4 = sh && vec == 2 && max_month_days <= 23 && g_tune_signal_maxd23 && bwf == 4 &&
+                   nbf == 2 && g_tune_signal_bl && N * 8 * 32 < ((int64_t)1 << 31) &&
+                   g_tune_signal_store == 0 && g_tune_signal_pair && g_tune_signal_bw == 1;
+  const int bw = noscan ? 4 : sh4 ? 4 : bwf_ok ? bwf
                      : (!sh && !tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
   const size_t lds = rr ? 0 : (size_t)W * 64 * vec * bw * sizeof(double) +
-                     (sh ? (size_t)3 * 64 * vec * sizeof(int) : 0);
+                     (sh ? (size_t)3 * 64 * vec * bw * sizeof(int) : 0);
   const unsigned blocks = (unsigned)((N / vec + 64 * bw - 1) / (64 * bw));
   const void* fn = nullptr;
 #define SIG(MD, V, NB) (const void*)k_signal<MD, V, NB, false>
 #define SIGT(MD, NB) (const void*)k_signal<MD, 2, NB, true>
-  if (sh)
+  if (sh4)
+    fn = (const void*)k_signal<23, 2, 2, false, 0, 4, true, true, false, 0, true>;
+  else if (sh)
     fn = max_month_days <= 24
              ? (vec == 2 ? (const void*)k_signal<24, 2, 4, false, 0, 1, true>
                          : (const void*)k_signal<24, 1, 4, false, 0, 1, true>)

@@ -40,28 +40,7 @@ void launch_deciles_narrow_reg(int T_m, hipStream_t st, const double* M, const d
 }
 int deciles_narrow_reg_max_n() { return DEC_NREG_RI * 4 * DEC_THREADS; }
 
-// the fused sweep path on bucket ids (csm_momentum_multi_ids -> csm_deciles_ids on rows of
-// <= dec_narrow_max assets): merged pass, then the general PRE kernel for the rows it leaves
-template <int NB>
-void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
-                               int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim,
-                               uint16_t* ids, int32_t* flg, bool merged_only) {
-  if (flg)
-    hipLaunchKernelGGL((dec_narrow::k_deciles<NB, true, true, 0, true, true>), dim3(T_m),
-                       dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
-                       ids, flg);
-  if (flg && merged_only) return;
-  hipLaunchKernelGGL((dec_narrow::k_deciles<NB, true, true, 0, true, false>), dim3(T_m),
-                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
-                     ids, flg);
-}
-
 #define INST(NB)                                                                              \
-  template void launch_deciles_pre_narrow<NB>(int, hipStream_t, const double*, const double*,  \
-                                              int64_t, int, const QTab&, int8_t*, double*,       \
-                                              int32_t*, int32_t*, int, int64_t*, uint16_t*,       \
-                                              int32_t*, bool);                                   \
   template void launch_deciles_narrow_reg<NB>(int, hipStream_t, const double*, const double*,  \
                                               int64_t, int, const QTab&, int8_t*, double*,       \
                                               int32_t*, int32_t*, int, int64_t*);                \

@@ -1,0 +1,46 @@
+// deciles_npre.hip -- the sweeps' decile pass on bucket ids (csm_momentum_multi_ids ->
+// csm_deciles_ids on rows of <= dec_narrow_max assets): the narrow-row kernel of
+// csrc/deciles.inc in PRE mode with 2048 buckets (the fixed map's ids >> 2).  Finer than the
+// streaming narrow kernel's 1024 so that fewer cells share an edge's bucket: each of those costs
+// a scattered 8-B read of mom_J (a cache line of HBM traffic).  Own translation unit: builds in
+// parallel with the others.
+#include "csm_common.h"
+
+#define DEC_THREADS 256
+#define HB 2048
+#define CAP 1024
+#define DEC_MINB 6
+namespace dec_npre {
+#include "deciles.inc"
+}  // namespace dec_npre
+
+// the fused sweep path on bucket ids (csm_momentum_multi_ids -> csm_deciles_ids on rows of
+// <= dec_narrow_max assets): merged pass, then the general PRE kernel for the rows it leaves
+template <int NB>
+void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
+                               int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
+                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim,
+                               uint16_t* ids, int32_t* flg, bool merged_only) {
+  if (flg)
+    hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, 0, true, true>), dim3(T_m),
+                       dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
+                       ids, flg);
+  if (flg && merged_only) return;
+  hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, 0, true, false>), dim3(T_m),
+                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
+                     ids, flg);
+}
+
+#define INST(NB)                                                                              \
+  template void launch_deciles_pre_narrow<NB>(int, hipStream_t, const double*, const double*,  \
+                                              int64_t, int, const QTab&, int8_t*, double*,       \
+                                              int32_t*, int32_t*, int, int64_t*, uint16_t*,       \
+                                              int32_t*, bool);
+INST(0)
+INST(2)
+INST(3)
+INST(4)
+INST(5)
+INST(10)
+INST(20)
+#undef INST

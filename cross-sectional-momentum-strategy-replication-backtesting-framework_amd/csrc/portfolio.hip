@@ -8,8 +8,8 @@
 //   k_turnover     one workgroup per (asset chunk, t, b): aggregate leg weights of the K
 //                  overlapping cohorts at t and t - 1, |dw| summed into turnover and into the
 //                  spread + square-root-impact cost of src/execution_models.py:4-12 (E4, E5)
-//   k_overlap      one workgroup per (t, b): chunk partials summed in chunk order, cohort
-//                  means -> overlapped decile returns (E2), turnover / cost totals
+//   k_overlap      one thread per (K, t, b, decile): chunk partials summed in chunk order,
+//                  cohort means -> overlapped decile returns (E2), turnover / cost totals
 //   k_ls           one workgroup per panel: the reference's long-short rule
 //                  (run_demo.py:60-67) per panel (E3), net = long-short - cost
 //
@@ -564,15 +564,19 @@ __device__ __forceinline__ void load_labels(const int8_t* __restrict__ p, int* l
 __device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INFINITY) ? x : 0.0; }
 
 // GEN = false: the steady rows only (every (K, leg) window full), GEN = true: the others (the
-// first months, empty cohorts); two launches so the steady kernel keeps few registers.
+// first months, empty cohorts); two launches so the steady kernel keeps few registers.  The
+// steady launch (one workgroup per (chunk, row)) appends the (chunk, row) ids it leaves to a
+// work list; the general launch is a small persistent grid that walks that list (every
+// workgroup reaches the list's end), so the steady rows cost it nothing.
 template <bool VW, bool IMP, bool GEN>
-__global__ __launch_bounds__(PF_THREADS) void k_turnover(
-    const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
-    int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
-    int Ct, double half_spread, double k_impact, double aum, const double* __restrict__ ADV,
-    const double* __restrict__ SIG, double* __restrict__ TURNp, double* __restrict__ COSTp) {
-  const int c = (int)(blockIdx.x % (unsigned)Ct);
-  const int tb = (int)(blockIdx.x / (unsigned)Ct);
+__device__ __forceinline__ void turnover_body(
+    int bid, const int8_t* __restrict__ L, const double* __restrict__ W,
+    const double* __restrict__ FWp, int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins,
+    int Cf, int64_t CH, int Ct, double half_spread, double k_impact, double aum,
+    const double* __restrict__ ADV, const double* __restrict__ SIG, double* __restrict__ TURNp,
+    double* __restrict__ COSTp, int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count) {
+  const int c = bid % Ct;
+  const int tb = bid / Ct;
   const int rows = T_m * B;
   const int t = tb / B, b = tb - t * B;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -631,7 +635,10 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
   };
   bool all_full = true;
   for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
-  if (all_full == GEN) return;   // the other launch's row
+  if (!GEN && !all_full) {   // the general launch's row: onto its work list
+    if (tid == 0) gen_list[atomicAdd(gen_count, 1)] = bid;
+    return;
+  }
   if (!GEN && CNT && (N & 3) == 0) {
     // steady state, 4 cells per lane per word (SWAR byte compares on the label words)
     const uint32_t topw = (uint32_t)dtop * 0x01010101u;
@@ -896,22 +903,50 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
   }
 }
 
+template <bool VW, bool IMP, bool GEN>
+__global__ __launch_bounds__(PF_THREADS) void k_turnover(
+    const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
+    int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
+    int Ct, double half_spread, double k_impact, double aum, const double* __restrict__ ADV,
+    const double* __restrict__ SIG, double* __restrict__ TURNp, double* __restrict__ COSTp,
+    int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count) {
+  if (!GEN) {
+    turnover_body<VW, IMP, false>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH, Ct,
+                                  half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp, gen_list,
+                                  gen_count);
+  } else {
+    const int n = *(volatile int32_t*)gen_count;   // written by the previous launch
+    for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
+      turnover_body<VW, IMP, true>(gen_list[i], L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH,
+                                   Ct, half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp,
+                                   gen_list, gen_count);
+      __syncthreads();   // the shared tables are rebuilt for the next row
+    }
+  }
+}
+
+
 // ------------------------------------------------------------------------------ E2, E3
-// one 64-lane workgroup per (t, b, holding period q of the K set): lane d < nb combines decile
-// d over the chunks and the cohorts; lane 0 also totals the turnover / cost partials.  Output
+// one thread per (holding period q of the K set, t, b, decile d): combines decile d over the
+// chunks and the cohorts; the d = 0 thread also totals the turnover / cost partials.  Output
 // q lands at offset q * rows of the [nK][T_m][B] stacks (PR: [nK][T_m][B][nb]).
-__global__ __launch_bounds__(64) void k_overlap(
+__global__ __launch_bounds__(256) void k_overlap(
     const double* __restrict__ SWRp, const double* __restrict__ SWp, KSet ks, int Kmax, int C,
     int nb, const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
     int64_t rows, double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST,
     int legs) {
-  const int64_t tb = blockIdx.x;
-  const int q = blockIdx.y;
+  // one thread per output (q, t, b, d), in PR's layout (flat grid: the one-workgroup-per-row
+  // version was 64-lane workgroups with nb lanes busy, dispatch-bound at sweep sizes)
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)ks.n * rows * nb) return;
+  const int d = (int)(g % nb);
+  const int64_t qtb = g / nb;
+  const int q = (int)(qtb / rows);
+  const int64_t tb = qtb - (int64_t)q * rows;
   const int K = ks.K[q];
-  const int d = threadIdx.x;
-  if (legs && d < nb && d != 0 && d != nb - 1) {   // legs-only cohort sums: not computed
+  if (legs && d != 0 && d != nb - 1) {   // legs-only cohort sums: not computed
     PR[(q * rows + tb) * nb + d] = qnan();
-  } else if (d < nb) {
+  } else {
     double acc = 0.0;
     int n = 0;
     for (int k = 0; k < K; ++k) {
@@ -1159,6 +1194,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
 struct PfLayout {
   PfPlan p;
   int64_t rows, swr, sw, fw, fwt, turn, cost, bytes;
+  int64_t gen_b;                     // byte offset: int32 count + [rows * Ct] general-row work list
   bool seg;                          // label-sort buffers present (N <= SEG_MAXN)
   int64_t perm_b, off_b, wsrt_b;     // byte offsets: uint16 [rows][N], int32 [rows][nb+1], f64 [rows][N]
 };
@@ -1174,6 +1210,8 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   l.turn = l.fwt + l.rows * 2;                              // [TO_MAXQ][rows][Ct]
   l.cost = l.turn + (int64_t)TO_MAXQ * l.rows * l.p.Ct;
   l.bytes = (l.cost + (int64_t)TO_MAXQ * l.rows * l.p.Ct) * 8 + 256;
+  l.gen_b = (l.bytes + 255) / 256 * 256;
+  l.bytes = l.gen_b + (1 + l.rows * l.p.Ct) * 4 + 256;
   l.seg = N <= SEG_MAXN;
   l.perm_b = l.off_b = l.wsrt_b = 0;
   if (l.seg) {
@@ -1276,15 +1314,20 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
     for (int q = 0; q < TO_MAXQ; ++q) ks.K[q] = q < ks.n ? Ks[q0 + q] : 1;
     if (costs) {
       const bool imp = ADV && aum > 0.0;
+      int32_t* gen_count = (int32_t*)((char*)workspace + lay.gen_b);
+      int32_t* gen_list = gen_count + 1;
+      HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
+      const int64_t nblk = lay.p.Ct * lay.rows;
+      const unsigned gen_grid = (unsigned)std::min<int64_t>(nblk, 2048);
       for (int gen = 0; gen < 2; ++gen) {
         auto kern = gen ? (W ? (imp ? k_turnover<true, true, true> : k_turnover<true, false, true>)
                              : (imp ? k_turnover<false, true, true> : k_turnover<false, false, true>))
                         : (W ? (imp ? k_turnover<true, true, false> : k_turnover<true, false, false>)
                              : (imp ? k_turnover<false, true, false> : k_turnover<false, false, false>));
-        hipLaunchKernelGGL(kern, dim3((unsigned)(lay.p.Ct * lay.rows)), dim3(PF_THREADS), 0, st,
+        hipLaunchKernelGGL(kern, dim3(gen ? gen_grid : (unsigned)nblk), dim3(PF_THREADS), 0, st,
                            L, W, (const double*)(ws + lay.fwt), T_m, B, N, ks, Kmax, n_bins, 1,
                            lay.p.CHt, lay.p.Ct, half_spread, k_impact, aum, ADV, SIG,
-                           ws + lay.turn, ws + lay.cost);
+                           ws + lay.turn, ws + lay.cost, gen_list, gen_count);
       }
       LAUNCH_CHECK(ctx, "k_turnover");
     }
@@ -1292,7 +1335,8 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
     double* COSTq = COST ? COST + q0 * rb : nullptr;
     double* NETq = NET ? NET + q0 * rb : nullptr;
     double* PRq = PR + q0 * rb * n_bins;
-    hipLaunchKernelGGL(k_overlap, dim3((unsigned)lay.rows, (unsigned)ks.n), dim3(64), 0, st,
+    hipLaunchKernelGGL(k_overlap, dim3((unsigned)(((int64_t)ks.n * lay.rows * n_bins + 255) / 256)),
+                       dim3(256), 0, st,
                        (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks, Kmax,
                        lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
                        (const double*)(ws + lay.cost), lay.p.Ct, (int64_t)lay.rows, PRq, TURNq,

@@ -81,6 +81,31 @@ def test_fused_shards_sparse_panel(engine, G):
     assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
 
 
+@pytest.mark.parametrize("G", [2, 7])
+@pytest.mark.parametrize("J,skip", [(12, 1), (3, 0)])
+def test_fused_shards_four_wave_blocks(engine, G, J, skip):
+    """The shard signal kernel on the C4 configuration (4 barrier-free waves per workgroup,
+    2 month buffers, raw buffer loads; chosen by default at >= 92,160 assets, forced here) on a
+    gappy panel: equal to the one-GPU pass bit for bit."""
+    from oracle.synth_np import make_panel
+    from csmom.distributed import virtual_shards
+    pan = make_panel(1_000, 2600, seed=13, nan_day=0.05, absent_month=0.2, nan_month=0.1,
+                     cents=True)
+    P, ms = _up(pan["P"]), pan["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), J, skip, 10, with_ret=True)
+    lib = engine.lib
+    try:
+        assert lib.csm_tune(b"signal_bwf", 4) == 0 and lib.csm_tune(b"signal_nbuf", 2) == 0
+        M, NR, L, EW, CNT, LS = virtual_shards(engine, P, ms, G, J, skip, 10, fused=True)
+    finally:
+        lib.csm_tune(b"signal_bwf", 0)
+        lib.csm_tune(b"signal_nbuf", 4)
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L)
+    assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+
+
 def test_shard_repair_rewrites_ret(engine):
     """With R requested, the repaired R of a shard equals the carried scan's R."""
     z = load_golden("edge")
