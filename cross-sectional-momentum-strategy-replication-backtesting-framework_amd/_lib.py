@@ -28,7 +28,8 @@ EXPORTS = (
     "csm_last_present_month", "csm_portfolio_from_cohorts_multi", "csm_summary",
     "csm_shard_repair", "csm_signal_shard", "csm_shard_summary_state", "csm_momentum_multi",
     "csm_signal_ids", "csm_deciles_ids", "csm_pipeline", "csm_momentum_multi_ids",
-    "csm_cohort_sums_legs", "csm_portfolio_from_cohorts_legs",
+    "csm_cohort_sums_legs", "csm_portfolio_from_cohorts_legs", "csm_signal_shard_ids",
+    "csm_shard_repair_ids",
 )
 
 
@@ -107,6 +108,10 @@ def _declare(lib):
                                             _p, _p, _p]),
         "csm_signal_shard": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p,
                                             _p, _p, _p, _p]),
+        "csm_signal_shard_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32,
+                                                _p, _p, _p, _p, _p, _p]),
+        "csm_shard_repair_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _p,
+                                                _p, _p, _p, _p, _p]),
         "csm_shard_summary_state": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p,
                                                    _p]),
         "csm_signal_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _p,

@@ -1593,7 +1593,7 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
     int T_m, int64_t N, int J, int skip,
     const double* __restrict__ carry, const double* __restrict__ next_pm,
     const double* __restrict__ st, double* __restrict__ R, double* __restrict__ M,
-    double* __restrict__ NR) {
+    double* __restrict__ NR, uint16_t* __restrict__ IDS) {
   extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][W][REPAIR_THREADS]
   const int W = J + skip, RS = REPAIR_THREADS;
   const int tid = threadIdx.x;
@@ -1625,7 +1625,8 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
       const int m = m0 + j;
       if (m >= T_m || done) break;
       const double x = buf[j];
-      scan_step(t, x, m, rt, RS, W, J, N, a, R, M, NR);
+      const double mom = scan_step(t, x, m, rt, RS, W, J, N, a, R, M, NR);
+      if (IDS) IDS[(int64_t)m * N + a] = (uint16_t)csm_fid(mom);   // the rewritten cell's bucket id
       scan_shadow(f, x, m, rf, RS, W, J);
       if (!is_absent(x)) ++seen;
       conv = same();
@@ -2116,6 +2117,16 @@ int csm_signal_shard(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                        max_month_days, J, skip, PM, R, M, NR, nullptr, nullptr, state, true);
 }
 
+int csm_signal_shard_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                         const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                         int32_t J, int32_t skip, double* PM, double* R, double* M, double* NR,
+                         double* state, uint16_t* ids) {
+  if (!ids || (N % 4) != 0 || ((uintptr_t)ids & 7u) != 0)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_shard_ids: needs ids, N %% 4 == 0, 8-B aligned ids");
+  return signal_launch(ctx, "csm_signal_shard_ids", false, P, T_d, N, month_start, T_m,
+                       max_month_days, J, skip, PM, R, M, NR, nullptr, nullptr, state, true, ids);
+}
+
 int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
                      const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
                      int32_t skip, double* PM, double* R, double* M, double* NR,
@@ -2411,10 +2422,10 @@ int csm_shard_summary_state(csm_ctx* ctx, const double* P, const int64_t* month_
   return CSM_OK;
 }
 
-int csm_shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_start, const double* PM,
+static int shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_start, const double* PM,
                      int32_t T_m, int64_t N, int32_t J, int32_t skip, const double* carry,
                      const double* next_pm, const double* state, double* R, double* M,
-                     double* NR) {
+                     double* NR, uint16_t* ids) {
   int r = prep(ctx);
   if (r) return r;
   if (!P || !month_start || !PM || !carry || !next_pm || !state || !M || !NR || N <= 0 ||
@@ -2428,9 +2439,26 @@ int csm_shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_start, 
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_shard_repair, dim3((unsigned)((N + REPAIR_THREADS - 1) / REPAIR_THREADS)),
                      dim3(REPAIR_THREADS), lds, ctx->stream, PM, P, month_start, T_m, N, J, skip,
-                     carry, next_pm, state, R, M, NR);
+                     carry, next_pm, state, R, M, NR, ids);
   LAUNCH_CHECK(ctx, "k_shard_repair");
   return CSM_OK;
+}
+
+int csm_shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_start, const double* PM,
+                     int32_t T_m, int64_t N, int32_t J, int32_t skip, const double* carry,
+                     const double* next_pm, const double* state, double* R, double* M,
+                     double* NR) {
+  return shard_repair(ctx, P, month_start, PM, T_m, N, J, skip, carry, next_pm, state, R, M, NR,
+                      nullptr);
+}
+
+int csm_shard_repair_ids(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                         const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                         const double* carry, const double* next_pm, const double* state,
+                         double* R, double* M, double* NR, uint16_t* ids) {
+  if (!ids) return set_err(ctx, CSM_E_INVAL, "csm_shard_repair_ids: ids is NULL");
+  return shard_repair(ctx, P, month_start, PM, T_m, N, J, skip, carry, next_pm, state, R, M, NR,
+                      ids);
 }
 
 int64_t csm_momentum_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip,

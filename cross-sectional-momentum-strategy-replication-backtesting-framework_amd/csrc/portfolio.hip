@@ -568,7 +568,7 @@ __device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INF
 // steady launch (one workgroup per (chunk, row)) appends the (chunk, row) ids it leaves to a
 // work list; the general launch is a small persistent grid that walks that list (every
 // workgroup reaches the list's end), so the steady rows cost it nothing.
-template <bool VW, bool IMP, bool GEN>
+template <bool VW, bool IMP, bool GEN, bool BM = false>
 __device__ __forceinline__ void turnover_body(
     int bid, const int8_t* __restrict__ L, const double* __restrict__ W,
     const double* __restrict__ FWp, int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins,
@@ -782,7 +782,7 @@ __device__ __forceinline__ void turnover_body(
         }
       }
       }
-    } else
+    } else if constexpr (!BM) {
     for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS)
     for (int64_t a = a4; a < a4 + cw && a < a1; ++a) {
       double adv = 0.0, unit_sig = 0.02;
@@ -858,6 +858,7 @@ __device__ __forceinline__ void turnover_body(
         }
       }
     }
+    }
   }
   __shared__ double red[PF_WAVES][2 * TO_MAXQ];
   __shared__ uint32_t cred[PF_WAVES][1 + 2 * TO_MAXQ];
@@ -903,7 +904,9 @@ __device__ __forceinline__ void turnover_body(
   }
 }
 
-template <bool VW, bool IMP, bool GEN>
+// BM (general launch, equal weight, every K <= 31): only the bit-mask path is compiled, so the
+// kernel keeps the registers of that path (the dense path's arrays would double them).
+template <bool VW, bool IMP, bool GEN, bool BM = false>
 __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
     int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
@@ -917,7 +920,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
   } else {
     const int n = *(volatile int32_t*)gen_count;   // written by the previous launch
     for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
-      turnover_body<VW, IMP, true>(gen_list[i], L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH,
+      turnover_body<VW, IMP, true, BM>(gen_list[i], L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH,
                                    Ct, half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp,
                                    gen_list, gen_count);
       __syncthreads();   // the shared tables are rebuilt for the next row
@@ -1320,8 +1323,12 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
       const int64_t nblk = lay.p.Ct * lay.rows;
       const unsigned gen_grid = (unsigned)std::min<int64_t>(nblk, 2048);
       for (int gen = 0; gen < 2; ++gen) {
+        int kq = 0;
+        for (int q = 0; q < ks.n; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;
         auto kern = gen ? (W ? (imp ? k_turnover<true, true, true> : k_turnover<true, false, true>)
-                             : (imp ? k_turnover<false, true, true> : k_turnover<false, false, true>))
+                             : (imp ? k_turnover<false, true, true>
+                                    : (kq <= 31 && (N & 3) == 0 ? k_turnover<false, false, true, true>
+                                                                : k_turnover<false, false, true>)))
                         : (W ? (imp ? k_turnover<true, true, false> : k_turnover<true, false, false>)
                              : (imp ? k_turnover<false, true, false> : k_turnover<false, false, false>));
         hipLaunchKernelGGL(kern, dim3(gen ? gen_grid : (unsigned)nblk), dim3(PF_THREADS), 0, st,

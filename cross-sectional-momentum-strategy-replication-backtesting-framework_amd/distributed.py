@@ -100,15 +100,21 @@ class DateShardPipeline:
             T_m = month_start_local.numel() - 1
             self._check_months(T_m)
             if self.G == 1:
+                if _shard_ids(st, P_local, month_start_local) is not None:   # = csm_pipeline
+                    _, _, M, NR, ids = st.signal_ids(P_local, month_start_local, max_month_days,
+                                                     J, s)
+                    return self._rank_and_gather(M, NR, ids)
                 _, _, M, NR = st.signal(P_local, month_start_local, max_month_days, J, s)
                 return self._rank_and_gather(M, NR)
+            ids = _shard_ids(st, P_local, month_start_local)
             PM, _, M, NR, state = st.signal_shard(P_local, month_start_local, max_month_days,
-                                                  J, s)
+                                                  J, s, **({} if ids is None else {"ids": ids}))
             summary = st.shard_summary(PM, J, s, state=state)
             summaries = all_gather_stack(summary, self.group)          # collective 1
             carry, next_pm = st.fold_carry(summaries, self.rank, J, s)
-            st.shard_repair(PM, carry, next_pm, state, M, NR, J, s)
-            return self._rank_and_gather(M, NR)
+            st.shard_repair(PM, carry, next_pm, state, M, NR, J, s,
+                            **({} if ids is None else {"ids": ids}))
+            return self._rank_and_gather(M, NR, ids)
         PM, _ = st.month_end(P_local, month_start_local)
         self._check_months(PM.shape[0])
         summary = st.shard_summary(PM, J, s)
@@ -120,10 +126,13 @@ class DateShardPipeline:
         _, M, NR = st.momentum(PM, J, s, carry=carry, next_pm=next_pm)
         return self._rank_and_gather(M, NR)
 
-    def _rank_and_gather(self, M, NR) -> ShardResult:
+    def _rank_and_gather(self, M, NR, ids=None) -> ShardResult:
         st, nb = self.st, self.n_bins
         T_m = M.shape[0]
-        L, EW, CNT, _ = st.deciles(M, NR, nb)
+        if ids is not None:   # rank from the bucket ids the shard pass wrote
+            L, EW, CNT, _ = st.deciles_ids(M, NR, ids, nb)
+        else:
+            L, EW, CNT, _ = st.deciles(M, NR, nb)
         if self.G > 1:
             pad_ew = torch.full((self.Tmax, nb), float("nan"), dtype=EW.dtype, device=EW.device)
             pad_cnt = torch.zeros((self.Tmax, nb), dtype=CNT.dtype, device=CNT.device)
@@ -138,6 +147,17 @@ class DateShardPipeline:
             CNT = torch.cat(cns, 0).to(torch.int32).contiguous()
         LS = st.long_short(EW, CNT)
         return ShardResult(M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS)
+
+
+def _shard_ids(stages, P, month_start):
+    """An id buffer for the fused shard pass when the stages rank from bucket ids: the engine,
+    on the rows csm_pipeline ranks from ids too (N % 4 == 0, wider than the 16,384-asset
+    narrow-row kernels), so a sharded run's decile means are the one-GPU pipeline's bit for bit.
+    None: rank from mom_J."""
+    T_d, N = P.shape
+    if not getattr(stages, "shard_ids", False) or N % 4 or N <= 16384:
+        return None
+    return torch.empty((month_start.numel() - 1, N), dtype=torch.int16, device=P.device)
 
 
 def virtual_shards(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, fused=False):
@@ -157,23 +177,31 @@ def virtual_shards(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, fuse
         msl = torch.from_numpy(ms[m0:m1 + 1] - d0).to(dev)
         if fused:
             maxd = int(np.diff(ms[m0:m1 + 1]).max()) if m1 > m0 else 1
-            PM, _, M, NR, state = stages.signal_shard(P[d0:d1].contiguous(), msl, maxd, J, skip)
-            outs.append((M, NR, state))
+            Pg = P[d0:d1].contiguous()
+            ids = _shard_ids(stages, Pg, msl)
+            PM, _, M, NR, state = stages.signal_shard(Pg, msl, maxd, J, skip,
+                                                      **({} if ids is None else {"ids": ids}))
+            outs.append((M, NR, state, ids))
         else:
             PM, _ = stages.month_end(P[d0:d1].contiguous(), msl)
-            outs.append((None, None, None))
+            outs.append((None, None, None, None))
         PMs.append(PM)
     summaries = torch.stack([stages.shard_summary(PM, J, skip, state=outs[g][2])
                              for g, PM in enumerate(PMs)])
     Ms, NRs, Ls, EWs, CNTs = [], [], [], [], []
     for g, PM in enumerate(PMs):
         carry, next_pm = stages.fold_carry(summaries, g, J, skip)
+        ids = None
         if fused:
-            M, NR, state = outs[g]
-            stages.shard_repair(PM, carry, next_pm, state, M, NR, J, skip)
+            M, NR, state, ids = outs[g]
+            stages.shard_repair(PM, carry, next_pm, state, M, NR, J, skip,
+                                **({} if ids is None else {"ids": ids}))
         else:
             _, M, NR = stages.momentum(PM, J, skip, carry=carry, next_pm=next_pm)
-        L, EW, CNT, _ = stages.deciles(M, NR, n_bins)
+        if ids is not None:
+            L, EW, CNT, _ = stages.deciles_ids(M, NR, ids, n_bins)
+        else:
+            L, EW, CNT, _ = stages.deciles(M, NR, n_bins)
         Ms.append(M); NRs.append(NR); Ls.append(L); EWs.append(EW); CNTs.append(CNT)
     EW = torch.cat(EWs).contiguous()
     CNT = torch.cat(CNTs).contiguous()

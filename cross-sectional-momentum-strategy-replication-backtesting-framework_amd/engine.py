@@ -94,6 +94,8 @@ class ShardState:
 class Engine:
     """Signal (J, skip) -> per-date n_bins labels -> equal-weight long-short, on one GPU."""
 
+    shard_ids = True   # the fused date-shard pass writes bucket ids and ranks from them
+
     def __init__(self, device: int | str | torch.device = 0):
         if not torch.cuda.is_available():
             raise RuntimeError("csmom.Engine needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -644,11 +646,12 @@ class Engine:
         return carry, next_pm
 
     def signal_shard(self, P, month_start, max_month_days, J=12, skip=1, with_ret=False,
-                     out=None):
+                     out=None, ids=None):
         """csm_signal_shard: the fused pass over this date shard from an empty scan state
         (speculative; shard_repair fixes it once the carry is known).  Returns
         (PM, R, M, NR, ShardState); PM holds only the shard's first / last J + skip + 8
-        months (the rest are re-derived from P where needed)."""
+        months (the rest are re-derived from P where needed).  ids (int16 [T_m][N], N % 4 ==
+        0): also the fixed-map bucket id of every mom_J (csm_signal_shard_ids)."""
         T_d, N = P.shape
         T_m = month_start.numel() - 1
         _need(P, "P", torch.float64, (T_d, N), self.device)
@@ -659,12 +662,18 @@ class Engine:
             state = self.empty((5, N))
         else:
             PM, R, M, NR, state = out
-        self._call("csm_signal_shard", _ptr(P), T_d, N, _ptr(month_start), T_m,
-                   int(max_month_days), int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR),
-                   _ptr(state))
+        if ids is not None:
+            _need(ids, "ids", torch.int16, (T_m, N), self.device)
+            self._call("csm_signal_shard_ids", _ptr(P), T_d, N, _ptr(month_start), T_m,
+                       int(max_month_days), int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M),
+                       _ptr(NR), _ptr(state), _ptr(ids))
+        else:
+            self._call("csm_signal_shard", _ptr(P), T_d, N, _ptr(month_start), T_m,
+                       int(max_month_days), int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M),
+                       _ptr(NR), _ptr(state))
         return PM, R, M, NR, ShardState(state, P, month_start)
 
-    def shard_repair(self, PM, carry, next_pm, state, M, NR, J, skip, R=None):
+    def shard_repair(self, PM, carry, next_pm, state, M, NR, J, skip, R=None, ids=None):
         """csm_shard_repair: turn the outputs of signal_shard (M, NR, R rewritten in place)
         into those of the scan from `carry`, and finish the pending rows with `next_pm` (both
         from fold_carry)."""
@@ -677,9 +686,15 @@ class Engine:
         for t, nm in ((M, "M"), (NR, "NR"), (R, "R")):
             if t is not None:
                 _need(t, nm, torch.float64, (T_m, N), self.device)
-        self._call("csm_shard_repair", _ptr(state.P), _ptr(state.month_start), _ptr(PM), T_m, N,
-                   int(J), int(skip), _ptr(carry), _ptr(next_pm), _ptr(state.t), _ptr(R),
-                   _ptr(M), _ptr(NR))
+        if ids is not None:   # rewrite the ids of the rewritten cells too
+            _need(ids, "ids", torch.int16, (T_m, N), self.device)
+            self._call("csm_shard_repair_ids", _ptr(state.P), _ptr(state.month_start), _ptr(PM),
+                       T_m, N, int(J), int(skip), _ptr(carry), _ptr(next_pm), _ptr(state.t),
+                       _ptr(R), _ptr(M), _ptr(NR), _ptr(ids))
+        else:
+            self._call("csm_shard_repair", _ptr(state.P), _ptr(state.month_start), _ptr(PM),
+                       T_m, N, int(J), int(skip), _ptr(carry), _ptr(next_pm), _ptr(state.t),
+                       _ptr(R), _ptr(M), _ptr(NR))
         return M, NR
 
     def sync(self):

@@ -279,6 +279,19 @@ int csm_shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_start, 
                      int32_t T_m, int64_t N, int32_t J, int32_t skip, const double* carry,
                      const double* next_pm, const double* state, double* R, double* M,
                      double* NR);
+/*
+ * The speculative shard pass with bucket ids (for csm_deciles_ids): csm_signal_shard that also
+ * writes ids[T_m][N] like csm_signal_ids (N % 4 == 0, 8-B aligned), and csm_shard_repair that
+ * rewrites the id of every cell it rewrites.  Same M / NR / R bits as the plain calls.
+ */
+int csm_signal_shard_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                         const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                         int32_t J, int32_t skip, double* PM, double* R, double* M, double* NR,
+                         double* state, uint16_t* ids);
+int csm_shard_repair_ids(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                         const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                         const double* carry, const double* next_pm, const double* state,
+                         double* R, double* M, double* NR, uint16_t* ids);
 
 /*
  * Portfolio accounting beyond the reference's K = 1 equal-weight case (SURVEY 8(f) rank 2;

@@ -60,6 +60,16 @@ def main():
         L, EW, CNT, _ = eng.deciles(M, NR, nb)
         return eng.long_short(EW, CNT), M, NR, L
 
+    IDS = torch.empty((p1.month_start.numel() - 1, N), dtype=torch.int16, device=dev)
+
+    def fused_ids():   # the shard pass writes bucket ids; repair rewrites them; deciles on ids
+        PM, _, M, NR, st = eng.signal_shard(p1.P, p1.month_start, maxd, J, skip, ids=IDS)
+        S1 = eng.shard_summary(PM, J, skip, state=st)
+        carry, npm = eng.fold_carry(torch.stack([S0, S1]), 1, J, skip)
+        eng.shard_repair(PM, carry, npm, st, M, NR, J, skip, ids=IDS)
+        L, EW, CNT, _ = eng.deciles_ids(M, NR, IDS, nb)
+        return eng.long_short(EW, CNT), M, NR, L
+
     def staged():
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
         ev[0].record()
@@ -80,12 +90,13 @@ def main():
                  "deciles"]
         return {n: round(ev[i].elapsed_time(ev[i + 1]), 4) for i, n in enumerate(names)}
 
-    fns = dict(single=single, unfused=unfused, fused=fused)
+    fns = dict(single=single, unfused=unfused, fused=fused, fused_ids=fused_ids)
     for f in fns.values():
         f()
     torch.cuda.synchronize()
     _, Mu, NRu, Lu = unfused()
     _, Mf, NRf, Lf = fused()
+    _, Mi, NRi, Li = fused_ids()
     torch.cuda.synchronize()
 
     def bits(a, b):
@@ -93,8 +104,9 @@ def main():
         na, nb_ = torch.isnan(a.view(torch.float64)), torch.isnan(b.view(torch.float64))
         return bool(torch.equal(na, nb_) and torch.equal(a[~na], b[~nb_]))
 
-    equal = dict(M=bits(Mf, Mu), NR=bits(NRf, NRu), L=bool(torch.equal(Lf, Lu)))
-    del Mu, NRu, Lu, Mf, NRf, Lf
+    equal = dict(M=bits(Mf, Mu), NR=bits(NRf, NRu), L=bool(torch.equal(Lf, Lu)),
+                 M_ids=bits(Mi, Mu), L_ids=bool(torch.equal(Li, Lu)))
+    del Mu, NRu, Lu, Mf, NRf, Lf, Mi, NRi, Li
     times = {k: [] for k in fns}
     for _ in range(reps):
         for k, f in fns.items():

@@ -106,6 +106,28 @@ def test_fused_shards_four_wave_blocks(engine, G, J, skip):
     assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
 
 
+@pytest.mark.parametrize("G", [2, 5])
+def test_fused_shards_bucket_ids(engine, G):
+    """Rows wider than the narrow-row kernels: the shard pass writes bucket ids, the repair
+    rewrites those of the cells it replays, each shard ranks from its ids -- equal to the
+    one-GPU csm_pipeline (which ranks from ids too) bit for bit, decile means included."""
+    from oracle.synth_np import make_panel
+    from csmom.distributed import virtual_shards
+    pan = make_panel(20_000, 1_400, seed=17, with_volume=False, nan_day=0.03, absent_month=0.05,
+                     nan_month=0.05, cents=True)
+    P, ms = _up(pan["P"]), pan["month_start"].astype(np.int64)
+    out = engine.pipeline(P, _up(ms), 12, 1, 10)
+    M, NR, L, EW, CNT, LS = virtual_shards(engine, P, ms, G, 12, 1, 10, fused=True)
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L)
+    assert torch.equal(CNT, out.CNT)
+    assert bits_equal(EW.cpu().numpy(), out.EW.cpu().numpy())
+    assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+    ref = O.pipeline(pan["P"], ms, 12, 1, 10)
+    assert np.array_equal(L.cpu().numpy(), ref["L"])
+
+
 def test_shard_repair_rewrites_ret(engine):
     """With R requested, the repaired R of a shard equals the carried scan's R."""
     z = load_golden("edge")
