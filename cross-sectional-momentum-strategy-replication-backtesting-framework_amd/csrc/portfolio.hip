@@ -635,8 +635,8 @@ __device__ __forceinline__ void turnover_body(
   };
   bool all_full = true;
   for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
-  if (!GEN && !all_full) {   // the general launch's row: onto its work list
-    if (tid == 0) gen_list[atomicAdd(gen_count, 1)] = bid;
+  if (all_full == GEN) {   // the other launch's row
+    if (!GEN && gen_list && tid == 0) gen_list[atomicAdd(gen_count, 1)] = bid;   // onto its work list
     return;
   }
   if (!GEN && CNT && (N & 3) == 0) {
@@ -917,6 +917,10 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     turnover_body<VW, IMP, false>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH, Ct,
                                   half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp, gen_list,
                                   gen_count);
+  } else if (!gen_list) {   // full grid: the steady rows' workgroups exit after the prologue
+    turnover_body<VW, IMP, true, BM>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf,
+                                     CH, Ct, half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp,
+                                     gen_list, gen_count);
   } else {
     const int n = *(volatile int32_t*)gen_count;   // written by the previous launch
     for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
@@ -1085,6 +1089,8 @@ __global__ __launch_bounds__(256) void k_bootstrap_panel(const double* __restric
 static int g_tune_cohort_lds = 1;
 // 1: label-sorted segment gathers (k_label_sort + k_cohort_seg) where N <= SEG_MAXN
 static int g_tune_cohort_seg = 1;
+// turnover's general rows: 0 full second grid, 1 work list, 2 work list above 8192 workgroups
+static int g_tune_turn_list = 2;
 
 struct PfPlan {
   int C, kpar, Ct;
@@ -1238,6 +1244,10 @@ int csm_tune_portfolio(const char* key, int value) {
     g_tune_cohort_seg = value;
     return CSM_OK;
   }
+  if (key && !strcmp(key, "turn_list") && value >= 0 && value <= 2) {
+    g_tune_turn_list = value;
+    return CSM_OK;
+  }
   return CSM_E_INVAL;
 }
 
@@ -1317,11 +1327,14 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
     for (int q = 0; q < TO_MAXQ; ++q) ks.K[q] = q < ks.n ? Ks[q0 + q] : 1;
     if (costs) {
       const bool imp = ADV && aum > 0.0;
-      int32_t* gen_count = (int32_t*)((char*)workspace + lay.gen_b);
-      int32_t* gen_list = gen_count + 1;
-      HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
       const int64_t nblk = lay.p.Ct * lay.rows;
-      const unsigned gen_grid = (unsigned)std::min<int64_t>(nblk, 2048);
+      // general rows: a work list for big grids (turn_list 1, or 2 = auto above 8192
+      // workgroups), else a second full grid whose steady workgroups exit early
+      const bool use_list = g_tune_turn_list == 1 || (g_tune_turn_list == 2 && nblk > 8192);
+      int32_t* gen_count = use_list ? (int32_t*)((char*)workspace + lay.gen_b) : nullptr;
+      int32_t* gen_list = use_list ? gen_count + 1 : nullptr;
+      if (use_list) HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
+      const unsigned gen_grid = use_list ? (unsigned)std::min<int64_t>(nblk, 2048) : (unsigned)nblk;
       for (int gen = 0; gen < 2; ++gen) {
         int kq = 0;
         for (int q = 0; q < ks.n; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;

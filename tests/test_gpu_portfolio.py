@@ -391,3 +391,24 @@ def test_legs_only_falls_back_when_a_leg_column_is_missing(engine):
     flag.zero_()
     engine.portfolio_multi(L, NR, 10, Ks=(3, 12), legs_only=True, need_full=flag)
     assert int(flag.item()) == 0
+
+
+@pytest.mark.parametrize("vw", [False, True])
+def test_turnover_general_rows_list_equals_full_grid(engine, vw):
+    """Turnover's general rows (first months, empty cohorts) through the work list or through a
+    second full grid: identical bits (each row is computed by one workgroup either way)."""
+    L, NR, _, PM = _labels(engine, "c1")
+    W = _up(np.abs(PM.cpu().numpy()) * 1e6) if vw else None
+    rng = np.random.default_rng(3)
+    ADV = _up(rng.uniform(1e5, 1e8, L.shape))
+    lib = engine.lib
+    got = {}
+    try:
+        for mode in (0, 1):
+            assert lib.csm_tune(b"turn_list", mode) == 0
+            got[mode] = engine.portfolio_multi(L, NR, 10, Ks=(3, 6, 12), W=W, aum=5e6, ADV=ADV)
+    finally:
+        lib.csm_tune(b"turn_list", 2)
+    for K in (3, 6, 12):
+        for f in ("TURN", "COST", "NET", "LS"):
+            assert bits_equal(getattr(got[0][K], f).cpu().numpy(), getattr(got[1][K], f).cpu().numpy()), (K, f)

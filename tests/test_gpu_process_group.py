@@ -35,13 +35,13 @@ def _free_port():
     return p
 
 
-def _panel():
+def _panel(n=N_ASSETS, days=N_DAYS):
     from oracle.synth_np import make_panel
-    return make_panel(N_ASSETS, N_DAYS, seed=SEED, start="1990-01-01", with_volume=False,
+    return make_panel(n, days, seed=SEED, start="1990-01-01", with_volume=False,
                       nan_day=0.02, absent_month=0.01, nan_month=0.005, cents=True)
 
 
-def _date_worker(rank, world, port, J, skip, q):
+def _date_worker(rank, world, port, J, skip, n, days, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -49,7 +49,7 @@ def _date_worker(rank, world, port, J, skip, q):
         import csmom
         from csmom.distributed import DateShardPipeline, month_partition
         eng = csmom.Engine(0)
-        pan = _panel()
+        pan = _panel(n, days)
         ms = pan["month_start"].astype(np.int64)
         parts = month_partition(len(ms) - 1, world)
         m0, m1 = parts[rank]
@@ -90,14 +90,21 @@ def _spawn(target, world, *args):
     return sorted(res, key=lambda t: t[0])
 
 
-@pytest.mark.parametrize("J,skip", [(12, 1), (3, 0)])
-def test_date_shards_two_processes_equal_one_process(engine, J, skip):
-    res = _spawn(_date_worker, 2, J, skip)
-    pan = _panel()
+@pytest.mark.parametrize("J,skip,n,days", [(12, 1, N_ASSETS, N_DAYS), (3, 0, N_ASSETS, N_DAYS),
+                                           (12, 1, 20_000, 1_400)])
+def test_date_shards_two_processes_equal_one_process(engine, J, skip, n, days):
+    """2 ranks (gloo, both on cuda:0) run the fused shard pass, collectives included; equal to
+    one process bit for bit.  The 20,000-asset case ranks from bucket ids on every rank and is
+    compared with the one-GPU csm_pipeline (ids too)."""
+    res = _spawn(_date_worker, 2, J, skip, n, days)
+    pan = _panel(n, days)
     ms_h = pan["month_start"].astype(np.int64)
-    one = engine.run(torch.from_numpy(pan["P"]).to(engine.device),
-                     torch.from_numpy(ms_h).to(engine.device), J, skip, 10,
-                     max_month_days=int(np.diff(ms_h).max()), fused=True)
+    Pd = torch.from_numpy(pan["P"]).to(engine.device)
+    msd = torch.from_numpy(ms_h).to(engine.device)
+    if n > 16384:
+        one = engine.pipeline(Pd, msd, J, skip, 10)
+    else:
+        one = engine.run(Pd, msd, J, skip, 10, max_month_days=int(np.diff(ms_h).max()), fused=True)
     M = np.concatenate([r[1] for r in res])
     NR = np.concatenate([r[2] for r in res])
     L = np.concatenate([r[3] for r in res])
