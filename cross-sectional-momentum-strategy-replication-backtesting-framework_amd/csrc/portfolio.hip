@@ -1089,8 +1089,9 @@ __global__ __launch_bounds__(256) void k_bootstrap_panel(const double* __restric
 static int g_tune_cohort_lds = 1;
 // 1: label-sorted segment gathers (k_label_sort + k_cohort_seg) where N <= SEG_MAXN
 static int g_tune_cohort_seg = 1;
-// turnover's general rows: 0 full second grid, 1 work list, 2 work list above 8192 workgroups
-static int g_tune_turn_list = 2;
+// turnover's general rows: 0 full second grid, 1 work list (C5 112.0 -> 108.9, C3 1.438 ->
+// 1.405 ms/step same box), 2 work list above 8192 workgroups
+static int g_tune_turn_list = 1;
 
 struct PfPlan {
   int C, kpar, Ct;

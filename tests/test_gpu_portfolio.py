@@ -408,7 +408,7 @@ def test_turnover_general_rows_list_equals_full_grid(engine, vw):
             assert lib.csm_tune(b"turn_list", mode) == 0
             got[mode] = engine.portfolio_multi(L, NR, 10, Ks=(3, 6, 12), W=W, aum=5e6, ADV=ADV)
     finally:
-        lib.csm_tune(b"turn_list", 2)
+        lib.csm_tune(b"turn_list", 1)
     for K in (3, 6, 12):
         for f in ("TURN", "COST", "NET", "LS"):
             assert bits_equal(getattr(got[0][K], f).cpu().numpy(), getattr(got[1][K], f).cpu().numpy()), (K, f)
