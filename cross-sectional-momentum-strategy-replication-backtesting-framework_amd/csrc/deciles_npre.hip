@@ -8,8 +8,9 @@
 
 #define DEC_THREADS 256
 #define HB 2048
-#define CAP 1024
-#define DEC_MINB 6
+#define CAP 512
+#define DEC_MINB 4   // the general kernel and the merged pass with decile sums: no spills
+#define DEC_MINB_MG0 8   // labels-only merged pass: 59 VGPRs, 20 KB LDS -> 8 workgroups per CU
 namespace dec_npre {
 #include "deciles.inc"
 }  // namespace dec_npre
