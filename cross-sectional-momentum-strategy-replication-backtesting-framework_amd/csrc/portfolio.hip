@@ -377,6 +377,68 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
   }
 }
 
+// Legs-only label sort for equal weights, ONE WAVE PER FORMATION ROW (4 rows per workgroup, no
+// block barriers): 4-label words per lane, leg counts by SWAR byte compares, then ranks from
+// one ballot per byte lane and leg -- the same ascending-asset segments, sentinels, offsets and
+// leg totals as k_label_sort<NB, false, true>, so every later sum is bit-identical.  N % 4 == 0.
+__device__ __forceinline__ uint32_t byte_eq0(uint32_t z) {   // 0x80 in each byte of z that is 0
+  return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+}
+template <int NB>
+__global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
+    const int8_t* __restrict__ L, int64_t N, int C, int64_t rows, uint16_t* __restrict__ PERM,
+    int32_t* __restrict__ OFF, double* __restrict__ FWp) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * PF_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;   // no barriers below
+  const int64_t PS = seg_stride(N);
+  const uint32_t* L4 = reinterpret_cast<const uint32_t*>(L + row * N);
+  const int nw = (int)(N >> 2);
+  const uint32_t topw = (uint32_t)(NB - 1) * 0x01010101u;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int nb0 = 0, nt0 = 0;   // per-lane counts: bottom (decile 0), top (decile NB - 1)
+  for (int w0 = 0; w0 < nw; w0 += 64) {
+    const int wi = w0 + lane;
+    const uint32_t v = wi < nw ? L4[wi] : 0xFFFFFFFFu;
+    nb0 += __popc(byte_eq0(v));
+    nt0 += __popc(byte_eq0(v ^ topw));
+  }
+  for (int o = 32; o > 0; o >>= 1) { nb0 += __shfl_xor(nb0, o, 64); nt0 += __shfl_xor(nt0, o, 64); }
+  const int rb = (nb0 + 3) & ~3, rt = (nt0 + 3) & ~3;
+  uint16_t* Pr = PERM + row * PS;
+  if (lane <= NB) OFF[row * (NB + 1) + lane] = lane == 0 ? 0 : (lane < NB ? rb : rb + rt);
+  if (lane < rb - nb0) Pr[nb0 + lane] = (uint16_t)N;               // sentinel ids
+  if (lane < rt - nt0) Pr[rb + nt0 + lane] = (uint16_t)N;
+  for (int i = lane; i < 2 * C; i += 64) {   // leg totals in chunk 0 (leg 0 = top), zeros elsewhere
+    const int c = i >> 1, leg = i & 1;
+    FWp[(row * C + c) * 2 + leg] = c == 0 ? (double)(leg == 0 ? nt0 : nb0) : 0.0;
+  }
+  int pb = 0, pt = rb;   // next position of each leg's segment
+  for (int w0 = 0; w0 < nw; w0 += 64) {
+    const int wi = w0 + lane;
+    const uint32_t v = wi < nw ? L4[wi] : 0xFFFFFFFFu;
+    const uint32_t eb = byte_eq0(v), et = byte_eq0(v ^ topw);
+    int bb = pb, bt = pt;   // this lane's first position of each leg
+    int totb = 0, tott = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint64_t mb = __ballot((eb >> (8 * e + 7)) & 1u), mt = __ballot((et >> (8 * e + 7)) & 1u);
+      bb += __popcll(mb & lt);
+      bt += __popcll(mt & lt);
+      totb += __popcll(mb);
+      tott += __popcll(mt);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {   // lane-major then byte order = ascending asset id
+      const uint16_t a = (uint16_t)(4 * wi + e);
+      if ((eb >> (8 * e + 7)) & 1u) Pr[bb++] = a;
+      if ((et >> (8 * e + 7)) & 1u) Pr[bt++] = a;
+    }
+    pb += totb;
+    pt += tott;
+  }
+}
+
 // 16-lane groups, one (age, decile) segment per group at a time: a short reduction (4 steps)
 // per segment instead of a 64-lane one, and four segments per wave instruction.  The segment
 // offsets of all K formation rows are fetched into LDS with the return row, and a group reads
@@ -1092,6 +1154,8 @@ static int g_tune_cohort_seg = 1;
 // turnover's general rows: 0 full second grid, 1 work list (C5 112.0 -> 108.9, C3 1.438 ->
 // 1.405 ms/step same box), 2 work list above 8192 workgroups
 static int g_tune_turn_list = 1;
+// legs-only equal-weight label sort: 1 one wave per row (k_label_sort_legs_ew), 0 a workgroup per row
+static int g_tune_sort_wave = 1;
 
 struct PfPlan {
   int C, kpar, Ct;
@@ -1160,8 +1224,12 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                            (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
                            N, K, pl.C, Cs, xcd, SWRp, SWp);
       } else {
-        hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N,
-                           pl.C, PERM, OFF, WSRT, FWp);
+        if ((N & 3) == 0 && g_tune_sort_wave)   // one wave per row (C5's equal-weight legs)
+          hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
+                             dim3(PF_THREADS), 0, st, L, N, pl.C, (int64_t)T_m * B, PERM, OFF, FWp);
+        else
+          hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N,
+                             pl.C, PERM, OFF, WSRT, FWp);
         hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR,
                            (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
                            N, K, pl.C, Cs, xcd, SWRp, SWp);
@@ -1243,6 +1311,10 @@ int csm_tune_portfolio(const char* key, int value) {
   }
   if (key && !strcmp(key, "cohort_seg") && (value == 0 || value == 1)) {
     g_tune_cohort_seg = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "sort_wave") && (value == 0 || value == 1)) {
+    g_tune_sort_wave = value;
     return CSM_OK;
   }
   if (key && !strcmp(key, "turn_list") && value >= 0 && value <= 2) {

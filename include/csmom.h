@@ -56,7 +56,8 @@ int csm_abi_version(void);
  * rows by raw buffer loads, padding rows out of range; bit-identical), "signal_mw" (0 | 21 | 22 | 41 | 42 multi-wave
  * fused kernel), "cohort_lds" / "cohort_seg" (portfolio cohort-sum kernel choice),
  * "turn_list" (turnover's general rows: 0 a full second grid, 1 a work list, the default,
- * 2 the work list above 8192 workgroups).  Returns
+ * 2 the work list above 8192 workgroups), "sort_wave" (legs-only equal-weight label sort: 1 one
+ * wave per formation row, the default | 0 a workgroup per row).  Returns
  * CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with

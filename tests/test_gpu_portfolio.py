@@ -412,3 +412,29 @@ def test_turnover_general_rows_list_equals_full_grid(engine, vw):
     for K in (3, 6, 12):
         for f in ("TURN", "COST", "NET", "LS"):
             assert bits_equal(getattr(got[0][K], f).cpu().numpy(), getattr(got[1][K], f).cpu().numpy()), (K, f)
+
+
+@pytest.mark.parametrize("B,n_bins", [(1, 10), (6, 10), (4, 3), (3, 2)])
+def test_legs_label_sort_one_wave_per_row_bit_identical(engine, B, n_bins):
+    """The one-wave-per-row legs label sort (equal weights) against the workgroup-per-row one:
+    identical portfolio outputs bit for bit (same segments, sentinels, offsets, leg totals)."""
+    L, NR, _, PM = _labels(engine, "c1")
+    if n_bins != 10:
+        _, M, NR = engine.momentum(PM, 12, 1)
+        L, _, _, _ = engine.deciles(M, None, n_bins)
+    T_m, N = L.shape
+    if B > 1:
+        rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 3 * i, axis=1) for i in range(B)],
+                                     axis=1).reshape(T_m, B * N))
+        L, NR = rep(L), rep(NR)
+    lib = engine.lib
+    got = {}
+    try:
+        for mode in (1, 0):
+            assert lib.csm_tune(b"sort_wave", mode) == 0
+            got[mode] = engine.portfolio_multi(L, NR, n_bins, Ks=(3, 12), B=B, legs_only=True)
+    finally:
+        lib.csm_tune(b"sort_wave", 1)
+    for K in (3, 12):
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
