@@ -1163,6 +1163,9 @@ struct PfPlan {
 };
 
 // Enough workgroups to fill 256 CUs several times over, chunks of >= PF_CHUNK_MIN assets.
+// turnover workgroups wanted per launch (the row split into chunks to reach it); A/B knob
+// "turn_want" -- set it before the portfolio workspace is sized
+static int64_t g_tune_turn_want = 4096;
 static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
   PfPlan p;
   const int64_t rows = (int64_t)T_m * B;
@@ -1178,7 +1181,7 @@ static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
   C = C < 1 ? 1 : (C > cmax ? cmax : C);
   p.C = (int)C;
   p.CH = (N + C - 1) / C;
-  int64_t Ct = (want + rows - 1) / rows;
+  int64_t Ct = (g_tune_turn_want + rows - 1) / rows;   // turnover chunks
   Ct = Ct < 1 ? 1 : (Ct > cmax ? cmax : Ct);
   const int64_t cmin = (N + 65471) / 65472;       // < 65536 cells per chunk (packed counts)
   Ct = Ct < cmin ? cmin : Ct;
@@ -1311,6 +1314,10 @@ int csm_tune_portfolio(const char* key, int value) {
   }
   if (key && !strcmp(key, "cohort_seg") && (value == 0 || value == 1)) {
     g_tune_cohort_seg = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "turn_want") && value >= 1) {
+    g_tune_turn_want = value;
     return CSM_OK;
   }
   if (key && !strcmp(key, "sort_wave") && (value == 0 || value == 1)) {

@@ -57,7 +57,9 @@ int csm_abi_version(void);
  * fused kernel), "cohort_lds" / "cohort_seg" (portfolio cohort-sum kernel choice),
  * "turn_list" (turnover's general rows: 0 a full second grid, 1 a work list, the default,
  * 2 the work list above 8192 workgroups), "sort_wave" (legs-only equal-weight label sort: 1 one
- * wave per formation row, the default | 0 a workgroup per row).  Returns
+ * wave per formation row, the default | 0 a workgroup per row), "turn_want" (turnover
+ * workgroups wanted per launch, default 4096: rows split into chunks to reach it; set before
+ * sizing the portfolio workspace).  Returns
  * CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
