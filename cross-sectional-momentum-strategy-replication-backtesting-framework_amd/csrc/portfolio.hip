@@ -448,14 +448,16 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
 #define SEG_MAXKD 512   // K * (n_bins + 1) offsets staged in LDS
 // LEGS: the (age, leg) segments only (ND = 2 per age: deciles 0 and NB - 1); the partial
 // slots of the other deciles are not written (k_overlap skips them).
+#define SEG_STAGE_U 12
 template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const double* __restrict__ NR, const uint16_t* __restrict__ PERM,
     const int32_t* __restrict__ OFF, const double* __restrict__ WSRT, int T_m, int B, int64_t N,
-    int K, int C, int Cs, int xcd, double* __restrict__ SWRp, double* __restrict__ SWp) {
+    int K, int C, int Cs, int xcd, int stage2, double* __restrict__ SWRp, double* __restrict__ SWp) {
   constexpr int ND = LEGS ? 2 : NB;   // segments per age
   auto dec_of = [](int e) { return LEGS ? (e ? NB - 1 : 0) : e; };
-  extern __shared__ double rl[];   // the return row of month t (N values), NaN at slot N
+  // the return row of month t (N values), NaN at slot N
+  extern __shared__ __attribute__((aligned(16))) double rl[];
   __shared__ int32_t offs[SEG_MAXKD];
   int c = 0;
   int64_t tb;
@@ -492,8 +494,29 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const int k = i / (NB + 1), e = i - k * (NB + 1);
     offs[i] = OFF[(tb - (int64_t)k * B) * (NB + 1) + e];
   }
+  if ((N & 1) == 0 && stage2) {
+    // 16-B loads, up to SEG_STAGE_U per lane issued before any LDS store: a 6144-value row
+    // in flight at once (row starts are 16-B aligned for even N)
+    const int NP = (int)(N >> 1);
+    const double2* src = reinterpret_cast<const double2*>(NRr);
+    double2* dst = reinterpret_cast<double2*>(rl);
+    for (int i0 = tid; i0 < NP; i0 += PF_THREADS * SEG_STAGE_U) {
+      double2 v[SEG_STAGE_U];
+#pragma unroll
+      for (int u = 0; u < SEG_STAGE_U; ++u) {
+        const int i = i0 + u * PF_THREADS;
+        v[u] = i < NP ? src[i] : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < SEG_STAGE_U; ++u) {
+        const int i = i0 + u * PF_THREADS;
+        if (i < NP) dst[i] = v[u];
+      }
+    }
+  } else {
 #pragma unroll 8
-  for (int a = tid; a < (int)N; a += PF_THREADS) rl[a] = NRr[a];
+    for (int a = tid; a < (int)N; a += PF_THREADS) rl[a] = NRr[a];
+  }
   if (tid == 0) rl[N] = qnan();
   __syncthreads();
   // working chunk c < Cs owns the segments g = c (mod Cs) whole and writes zeros for the
@@ -1049,6 +1072,56 @@ __global__ __launch_bounds__(256) void k_overlap(
   }
 }
 
+// k_overlap with one thread per (t, b, decile d) serving every K of the set: the cohort terms
+// of ages 0..Kmax-1 are read once (trips of OV_TRIP ages in flight, instead of one dependent
+// load pair per age and K) and K's result is taken when the running sum reaches age K - 1 --
+// the same terms summed in the same order as k_overlap, so PR / TURN / COST are bit-identical.
+// Single-chunk cohort plans only (C == 1: C5's 30000-row batches); chunked plans (C3) keep
+// k_overlap, whose K-parallel grid hides the chunk loop better (0.71 vs 0.89 ms portfolio).
+#define OV_TRIP 8
+__global__ __launch_bounds__(256) void k_overlap_rows(
+    const double* __restrict__ SWRp, const double* __restrict__ SWp, KSet ks, int Kmax,
+    int nb, const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
+    int64_t rows, double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST,
+    int legs) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= rows * nb) return;
+  const int d = (int)(g % nb);
+  const int64_t tb = g / nb;
+  if (legs && d != 0 && d != nb - 1) {   // legs-only cohort sums: not computed
+    for (int q = 0; q < ks.n; ++q) PR[((int64_t)q * rows + tb) * nb + d] = qnan();
+  } else {
+    double acc = 0.0;
+    int n = 0;
+    for (int k0 = 0; k0 < Kmax; k0 += OV_TRIP) {
+      double xs[OV_TRIP], ys[OV_TRIP];
+#pragma unroll
+      for (int u = 0; u < OV_TRIP; ++u) {   // one partial per (age, decile): loads first
+        const int64_t o = (tb * Kmax + (k0 + u < Kmax ? k0 + u : 0)) * nb + d;
+        xs[u] = k0 + u < Kmax ? 0.0 + SWRp[o] : 0.0;   // 0.0 + x: k_overlap's chunk sum of one
+        ys[u] = k0 + u < Kmax ? 0.0 + SWp[o] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < OV_TRIP; ++u) {
+        const int k = k0 + u;
+        if (k >= Kmax) break;
+        if (ys[u] > 0.0) { acc += xs[u] / ys[u]; ++n; }
+        for (int q = 0; q < ks.n; ++q)
+          if (ks.K[q] == k + 1) PR[((int64_t)q * rows + tb) * nb + d] = n > 0 ? acc / (double)n : qnan();
+      }
+    }
+  }
+  if (d == 0 && TURNp) {
+    for (int q = 0; q < ks.n; ++q) {
+      const int64_t to = ((int64_t)q * rows + tb) * Ct;
+      double x = 0.0, y = 0.0;
+      for (int c = 0; c < Ct; ++c) { x += TURNp[to + c]; y += COSTp[to + c]; }
+      if (TURN) TURN[(int64_t)q * rows + tb] = x;
+      if (COST) COST[(int64_t)q * rows + tb] = y;
+    }
+  }
+}
+
 // one workgroup per (panel b, holding period q): the reference's long-short rule on PR[q].
 // need_full (legs-only accounting): set when a panel lacks one leg's column, where the rule
 // falls back to max - min over every decile (the caller reruns with every decile).
@@ -1156,6 +1229,11 @@ static int g_tune_cohort_seg = 1;
 static int g_tune_turn_list = 1;
 // legs-only equal-weight label sort: 1 one wave per row (k_label_sort_legs_ew), 0 a workgroup per row
 static int g_tune_sort_wave = 1;
+// 1: k_cohort_seg stages its return row with 16-B loads, a whole row in flight; 0: 8-B loop
+static int g_tune_seg_stage2 = 1;
+// 1: k_overlap_rows (one thread per (t, b, decile) serving every K of the set) for single-chunk
+// cohort plans, 0: k_overlap always
+static int g_tune_overlap_rows = 1;
 
 struct PfPlan {
   int C, kpar, Ct;
@@ -1225,7 +1303,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                            pl.C, PERM, OFF, WSRT, FWp);
         hipLaunchKernelGGL((k_cohort_seg<NB, true, true>), g2, dim3(PF_THREADS), lds, st, NR,
                            (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
-                           N, K, pl.C, Cs, xcd, SWRp, SWp);
+                           N, K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
       } else {
         if ((N & 3) == 0 && g_tune_sort_wave)   // one wave per row (C5's equal-weight legs)
           hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
@@ -1235,20 +1313,20 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                              pl.C, PERM, OFF, WSRT, FWp);
         hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR,
                            (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
-                           N, K, pl.C, Cs, xcd, SWRp, SWp);
+                           N, K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
       }
     } else if (W) {
       hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
       hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR,
                          (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, Cs, xcd, SWRp, SWp);
+                         K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
     } else {
       hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
       hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR,
                          (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, Cs, xcd, SWRp, SWp);
+                         K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
     }
     return;
   }
@@ -1322,6 +1400,14 @@ int csm_tune_portfolio(const char* key, int value) {
   }
   if (key && !strcmp(key, "sort_wave") && (value == 0 || value == 1)) {
     g_tune_sort_wave = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "seg_stage2") && (value == 0 || value == 1)) {
+    g_tune_seg_stage2 = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "overlap_rows") && (value == 0 || value == 1)) {
+    g_tune_overlap_rows = value;
     return CSM_OK;
   }
   if (key && !strcmp(key, "turn_list") && value >= 0 && value <= 2) {
@@ -1435,6 +1521,14 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
     double* COSTq = COST ? COST + q0 * rb : nullptr;
     double* NETq = NET ? NET + q0 * rb : nullptr;
     double* PRq = PR + q0 * rb * n_bins;
+    if (g_tune_overlap_rows && lay.p.C == 1)   // chunked plans (C3): k_overlap 0.71 vs 0.89 ms
+      hipLaunchKernelGGL(k_overlap_rows, dim3((unsigned)(((int64_t)lay.rows * n_bins + 255) / 256)),
+                         dim3(256), 0, st,
+                         (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks, Kmax,
+                         n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
+                         (const double*)(ws + lay.cost), lay.p.Ct, (int64_t)lay.rows, PRq, TURNq,
+                         COSTq, legs ? 1 : 0);
+    else
     hipLaunchKernelGGL(k_overlap, dim3((unsigned)(((int64_t)ks.n * lay.rows * n_bins + 255) / 256)),
                        dim3(256), 0, st,
                        (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks, Kmax,

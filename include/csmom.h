@@ -59,7 +59,10 @@ int csm_abi_version(void);
  * 2 the work list above 8192 workgroups), "sort_wave" (legs-only equal-weight label sort: 1 one
  * wave per formation row, the default | 0 a workgroup per row), "turn_want" (turnover
  * workgroups wanted per launch, default 4096: rows split into chunks to reach it; set before
- * sizing the portfolio workspace).  Returns
+ * sizing the portfolio workspace), "overlap_rows" (cohort -> PR combine: 1 one thread per
+ * (month, panel, decile) serving every K of the set when the cohort plan has one chunk, the
+ * default | 0 one per (K, month, panel, decile)), "seg_stage2" (segment cohort sums: 1 the
+ * return row staged with 16-B loads, the default | 0 an 8-B loop).  Returns
  * CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with

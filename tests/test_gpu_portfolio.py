@@ -438,3 +438,37 @@ def test_legs_label_sort_one_wave_per_row_bit_identical(engine, B, n_bins):
     for K in (3, 12):
         for f in ("PR", "LS", "TURN", "COST", "NET"):
             assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
+
+
+@pytest.mark.parametrize("B,legs,vw,Ks", [(1, False, False, (3, 6, 12)), (1, True, False, (12, 3)),
+                                          (16, True, False, (3, 6, 9, 12)),
+                                          (16, False, True, (1, 9, 9)), (4, False, True, (12, 2, 5))])
+def test_overlap_rows_bit_identical(engine, B, legs, vw, Ks):
+    """k_overlap_rows (one thread per (t, b, decile) for every K of the set; trips of 8 ages)
+    against k_overlap (one thread per (K, t, b, decile)): PR / LS / TURN / COST / NET bit for
+    bit on single-chunk plans (B = 16), repeated and unsorted K sets, legs-only and full
+    accounting, equal and value weights; chunked plans (B = 1, 4: C > 1) keep k_overlap in
+    both modes.  Also the 16-B row staging of k_cohort_seg (seg_stage2) against the 8-B loop."""
+    L, NR, _, _ = _labels(engine, "c1")
+    T_m, N = L.shape
+    if B > 1:
+        rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 5 * i, axis=1) for i in range(B)],
+                                     axis=1).reshape(T_m, B * N))
+        L, NR = rep(L), rep(NR)
+    W = None
+    if vw:
+        g = np.random.default_rng(7)
+        W = _up(g.uniform(0.5, 2.0, size=(T_m, B * N)))
+    lib = engine.lib
+    got = {}
+    try:
+        for mode in (1, 0):
+            assert lib.csm_tune(b"overlap_rows", mode) == 0
+            assert lib.csm_tune(b"seg_stage2", mode) == 0
+            got[mode] = engine.portfolio_multi(L, NR, 10, Ks=Ks, B=B, W=W, legs_only=legs)
+    finally:
+        lib.csm_tune(b"overlap_rows", 1)
+        lib.csm_tune(b"seg_stage2", 1)
+    for K in set(Ks):
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)

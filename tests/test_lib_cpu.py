@@ -72,14 +72,19 @@ def test_tune_keys_documented_in_header_are_accepted():
     cases = {b"signal_vec": ([1, 2], 2), b"signal_nbuf": ([2, 3, 4], 4), b"dec_ablate": ([0, 1], 0),
              b"signal_bwf": ([0, 1, 2, 3, 4], 0),
              b"dec_ids": ([0, 1], 0), b"dec_reg": ([0, 1, 2], 0),
-             b"dec_narrow_max": ([0, 16384], 16384), b"mj_reg": ([0, 1, 2], 1),
+             b"dec_narrow_max": ([0, 16384], 16384), b"mj_reg": ([0, 1, 2], 2),
              b"signal_store": ([0, 1, 2, 3, 4], 0), b"signal_rr": ([0, 1], 0),
-             b"signal_bl": ([0, 1], 1)}
+             b"signal_bl": ([0, 1], 1), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
+             b"turn_list": ([0, 1, 2], 1), b"sort_wave": ([0, 1], 1),
+             b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
+             b"seg_stage2": ([0, 1], 1)}
     for key, (vals, default) in cases.items():
         for v in vals:
             assert lib.csm_tune(key, v) == 0, (key, v)
         assert lib.csm_tune(key, default) == 0
     assert lib.csm_tune(b"dec_reg", 3) != 0
     assert lib.csm_tune(b"signal_vec", 3) != 0
+    assert lib.csm_tune(b"overlap_rows", 2) != 0
+    assert lib.csm_tune(b"turn_want", 0) != 0
     assert lib.csm_tune(b"no_such_knob", 1) != 0
     assert lib.csm_tune(None, 1) != 0
