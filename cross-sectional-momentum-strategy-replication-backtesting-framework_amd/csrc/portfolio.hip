@@ -458,7 +458,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   auto dec_of = [](int e) { return LEGS ? (e ? NB - 1 : 0) : e; };
   // the return row of month t (N values), NaN at slot N
   extern __shared__ __attribute__((aligned(16))) double rl[];
-  __shared__ int32_t offs[SEG_MAXKD];
+  // then the K * (NB + 1) segment offsets, in the same dynamic allocation: sized to the launch,
+  // so a 5k-asset row's workgroup needs 40.5 KB and four fit a CU (a fixed 2 KB table made 3)
+  int32_t* offs = reinterpret_cast<int32_t*>(rl + N + 1);
   int c = 0;
   int64_t tb;
   int t;
@@ -1296,7 +1298,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     const int Cs = (int)std::min<int64_t>(pl.C, std::max<int64_t>(1, (1024 + rows - 1) / rows));
     const dim3 g1((unsigned)(T_m * B)),
         g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(pl.C * T_m * B));
-    const size_t lds = (size_t)(N + 1) * sizeof(double);
+    const size_t lds = (size_t)(N + 1) * sizeof(double) + (size_t)K * (NB + 1) * sizeof(int32_t);
     if (legs) {
       if (W) {
         hipLaunchKernelGGL((k_label_sort<NB, true, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N,
