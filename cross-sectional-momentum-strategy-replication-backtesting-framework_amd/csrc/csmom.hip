@@ -1716,7 +1716,8 @@ int csm_tune(const char* key, int value) {
   if (!key) return CSM_E_INVAL;
   if (!strcmp(key, "cohort_lds") || !strcmp(key, "cohort_seg") || !strcmp(key, "turn_list") ||
       !strcmp(key, "sort_wave") || !strcmp(key, "turn_want") ||
-      !strcmp(key, "overlap_rows") || !strcmp(key, "seg_stage2"))
+      !strcmp(key, "overlap_rows") || !strcmp(key, "seg_stage2") ||
+      !strcmp(key, "turn_gen_grid") || !strcmp(key, "turn_prep"))
     return csm_tune_portfolio(key, value);
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_nbuf") && (value == 2 || value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }

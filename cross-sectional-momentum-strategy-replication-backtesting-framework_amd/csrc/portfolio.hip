@@ -655,13 +655,65 @@ __device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INF
 // steady launch (one workgroup per (chunk, row)) appends the (chunk, row) ids it leaves to a
 // work list; the general launch is a small persistent grid that walks that list (every
 // workgroup reaches the list's end), so the steady rows cost it nothing.
+// Per-row turnover factors for the steady equal-weight launch, computed once per row instead
+// of in every workgroup's prologue (two barriers and a dependent load round each): one thread
+// per row (t, b) forms, with the prologue's own arithmetic, inv_s = 1 / (leg total of the
+// cohort formed at s) for s = t and s = t - K_q, sk = 1 / K_u of month t, and the full-leg mask
+// (bit 2q + leg: K non-empty cohorts in both windows).  TPv [rows][TP_STRIDE]: per leg
+// [inv_t, inv_{t-K_0..3}], then sk [q][leg].
+#define TP_STRIDE (2 * (TO_MAXQ + 1) + 2 * TO_MAXQ)
+__global__ __launch_bounds__(256) void k_turn_prep(const double* __restrict__ FWt, int T_m,
+                                                   int B, KSet ks, double* __restrict__ TPv,
+                                                   uint32_t* __restrict__ TPm) {
+  const int64_t tb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tb >= (int64_t)T_m * B) return;
+  const int t = (int)(tb / B), b = (int)(tb - (int64_t)t * B);
+  int kq = 0;
+  for (int q = 0; q < ks.n; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;
+  int k1[TO_MAXQ][2], k0[TO_MAXQ][2];
+  double* tp = TPv + tb * TP_STRIDE;
+#pragma unroll
+  for (int q = 0; q < TO_MAXQ; ++q) k1[q][0] = k1[q][1] = k0[q][0] = k0[q][1] = 0;
+  for (int j = 0; j <= kq; ++j) {
+    const int s = t - j;
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      double tot = 0.0;
+      if (s >= 0) tot += FWt[((int64_t)s * B + b) * 2 + li];
+      const double v = tot > 0.0 ? 1.0 / tot : 0.0;
+      if (j == 0) tp[li * (TO_MAXQ + 1)] = v;
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q) {
+        if (q >= ks.n) break;
+        const int K = ks.K[q];
+        if (j == K) tp[li * (TO_MAXQ + 1) + 1 + q] = v;
+        k1[q][li] += (j < K && v > 0.0) ? 1 : 0;
+        k0[q][li] += (j >= 1 && j <= K && t >= 1 && v > 0.0) ? 1 : 0;
+      }
+    }
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < TO_MAXQ; ++q) {
+    if (q >= ks.n) break;
+    const int K = ks.K[q];
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      tp[2 * (TO_MAXQ + 1) + 2 * q + li] = k1[q][li] > 0 ? 1.0 / (double)k1[q][li] : 0.0;
+      m |= (k1[q][li] == K && k0[q][li] == K) ? (1u << (2 * q + li)) : 0u;
+    }
+  }
+  TPm[tb] = m;
+}
+
 template <bool VW, bool IMP, bool GEN, bool BM = false>
 __device__ __forceinline__ void turnover_body(
     int bid, const int8_t* __restrict__ L, const double* __restrict__ W,
     const double* __restrict__ FWp, int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins,
     int Cf, int64_t CH, int Ct, double half_spread, double k_impact, double aum,
     const double* __restrict__ ADV, const double* __restrict__ SIG, double* __restrict__ TURNp,
-    double* __restrict__ COSTp, int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count) {
+    double* __restrict__ COSTp, int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count,
+    const double* __restrict__ TPv = nullptr, const uint32_t* __restrict__ TPm = nullptr) {
   const int c = bid % Ct;
   const int tb = bid / Ct;
   const int rows = T_m * B;
@@ -670,6 +722,10 @@ __device__ __forceinline__ void turnover_body(
   __shared__ double inv[2][TO_MAXK + 1];      // [leg][j]: 1/total of cohort s = t - j (0 = empty)
   __shared__ double sk[TO_MAXQ][2][2];        // [q][leg][month t, t-1]: 1/K_u (0 if none)
   __shared__ int full[TO_MAXQ][2];
+  // steady equal-weight rows with k_turn_prep's factors: no prologue, the row's label loads
+  // start at once (the factors are per-row uniforms, read where they are used)
+  const bool pre = !GEN && !VW && !IMP && TPm != nullptr && (N & 3) == 0;
+  if (!pre) {
   for (int j = tid; j <= Kmax; j += PF_THREADS) {
     const int s = t - j;
 #pragma unroll
@@ -692,6 +748,7 @@ __device__ __forceinline__ void turnover_body(
     full[q][li] = (k1 == K && k0 == K) ? 1 : 0;
   }
   __syncthreads();
+  }
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
   const int64_t rt = ((int64_t)t * B + b) * N;
@@ -721,7 +778,12 @@ __device__ __forceinline__ void turnover_body(
     }
   };
   bool all_full = true;
-  for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
+  if (pre) {
+    const uint32_t need = (1u << (2 * nq)) - 1u;   // bit 2q + leg
+    all_full = (TPm[tb] & need) == need;
+  } else {
+    for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
+  }
   if (all_full == GEN) {   // the other launch's row
     if (!GEN && gen_list && tid == 0) gen_list[atomicAdd(gen_count, 1)] = bid;   // onto its work list
     return;
@@ -978,12 +1040,15 @@ __device__ __forceinline__ void turnover_body(
       }
 #pragma unroll
       for (int li = 0; li < 2; ++li) {
-        if (!full[q][li]) continue;
+        if (!pre && !full[q][li]) continue;   // (pre: only all-full rows get here)
         const uint32_t n1 = (S1 >> (16 * li)) & 0xFFFFu, n0 = (S0 >> (16 * li)) & 0xFFFFu,
                        nb = (SB >> (16 * li)) & 0xFFFFu;
-        const double i1 = inv[li][0], i0 = inv[li][K];
+        const double* tp = pre ? TPv + tb * TP_STRIDE : nullptr;
+        const double i1 = pre ? tp[li * (TO_MAXQ + 1)] : inv[li][0];
+        const double i0 = pre ? tp[li * (TO_MAXQ + 1) + 1 + q] : inv[li][K];
+        const double skq = pre ? tp[2 * (TO_MAXQ + 1) + 2 * q + li] : sk[q][li][0];
         x += ((double)(n1 - nb) * i1 + (double)(n0 - nb) * i0 + (double)nb * fabs(i1 - i0)) *
-             sk[q][li][0];
+             skq;
       }
     }
     TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.5 * x;
@@ -999,11 +1064,12 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover(
     int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
     int Ct, double half_spread, double k_impact, double aum, const double* __restrict__ ADV,
     const double* __restrict__ SIG, double* __restrict__ TURNp, double* __restrict__ COSTp,
-    int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count) {
+    int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count,
+    const double* __restrict__ TPv, const uint32_t* __restrict__ TPm) {
   if (!GEN) {
     turnover_body<VW, IMP, false>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH, Ct,
                                   half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp, gen_list,
-                                  gen_count);
+                                  gen_count, TPv, TPm);
   } else if (!gen_list) {   // full grid: the steady rows' workgroups exit after the prologue
     turnover_body<VW, IMP, true, BM>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf,
                                      CH, Ct, half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp,
@@ -1233,6 +1299,10 @@ static int g_tune_turn_list = 1;
 static int g_tune_sort_wave = 1;
 // 1: k_cohort_seg stages its return row with 16-B loads, a whole row in flight; 0: 8-B loop
 static int g_tune_seg_stage2 = 1;
+// workgroups of the persistent general-row turnover launch (walking the work list)
+static int64_t g_tune_turn_gen_grid = 8192;   // C5 portfolio: 512 49.1, 2048 40.1, 8192 39.5 ms
+// 1: k_turn_prep computes the steady equal-weight rows' factors once per row; 0: in-workgroup
+static int g_tune_turn_prep = 1;
 // 1: k_overlap_rows (one thread per (t, b, decile) serving every K of the set) for single-chunk
 // cohort plans, 0: k_overlap always
 static int g_tune_overlap_rows = 1;
@@ -1356,6 +1426,7 @@ struct PfLayout {
   PfPlan p;
   int64_t rows, swr, sw, fw, fwt, turn, cost, bytes;
   int64_t gen_b;                     // byte offset: int32 count + [rows * Ct] general-row work list
+  int64_t tp_b, tpm_b;               // byte offsets: k_turn_prep's per-row factors and masks
   bool seg;                          // label-sort buffers present (N <= SEG_MAXN)
   int64_t perm_b, off_b, wsrt_b;     // byte offsets: uint16 [rows][N], int32 [rows][nb+1], f64 [rows][N]
 };
@@ -1373,6 +1444,9 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   l.bytes = (l.cost + (int64_t)TO_MAXQ * l.rows * l.p.Ct) * 8 + 256;
   l.gen_b = (l.bytes + 255) / 256 * 256;
   l.bytes = l.gen_b + (1 + l.rows * l.p.Ct) * 4 + 256;
+  l.tp_b = (l.bytes + 255) / 256 * 256;                    // k_turn_prep: f64 [rows][TP_STRIDE]
+  l.tpm_b = l.tp_b + l.rows * TP_STRIDE * 8;               // then u32 [rows] full-leg masks
+  l.bytes = l.tpm_b + l.rows * 4 + 256;
   l.seg = N <= SEG_MAXN;
   l.perm_b = l.off_b = l.wsrt_b = 0;
   if (l.seg) {
@@ -1402,6 +1476,14 @@ int csm_tune_portfolio(const char* key, int value) {
   }
   if (key && !strcmp(key, "sort_wave") && (value == 0 || value == 1)) {
     g_tune_sort_wave = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "turn_prep") && (value == 0 || value == 1)) {
+    g_tune_turn_prep = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "turn_gen_grid") && value >= 1) {
+    g_tune_turn_gen_grid = value;
     return CSM_OK;
   }
   if (key && !strcmp(key, "seg_stage2") && (value == 0 || value == 1)) {
@@ -1502,7 +1584,15 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
       int32_t* gen_count = use_list ? (int32_t*)((char*)workspace + lay.gen_b) : nullptr;
       int32_t* gen_list = use_list ? gen_count + 1 : nullptr;
       if (use_list) HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
-      const unsigned gen_grid = use_list ? (unsigned)std::min<int64_t>(nblk, 2048) : (unsigned)nblk;
+      const unsigned gen_grid = use_list ? (unsigned)std::min<int64_t>(nblk, g_tune_turn_gen_grid)
+                                         : (unsigned)nblk;
+      // steady equal-weight rows take their factors from k_turn_prep (no per-workgroup prologue)
+      const bool prep = g_tune_turn_prep && !W && !imp && (N & 3) == 0;
+      double* TPv = prep ? (double*)((char*)workspace + lay.tp_b) : nullptr;
+      uint32_t* TPm = prep ? (uint32_t*)((char*)workspace + lay.tpm_b) : nullptr;
+      if (prep)
+        hipLaunchKernelGGL(k_turn_prep, dim3((unsigned)((lay.rows + 255) / 256)), dim3(256), 0, st,
+                           (const double*)(ws + lay.fwt), T_m, B, ks, TPv, TPm);
       for (int gen = 0; gen < 2; ++gen) {
         int kq = 0;
         for (int q = 0; q < ks.n; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;
@@ -1515,7 +1605,8 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
         hipLaunchKernelGGL(kern, dim3(gen ? gen_grid : (unsigned)nblk), dim3(PF_THREADS), 0, st,
                            L, W, (const double*)(ws + lay.fwt), T_m, B, N, ks, Kmax, n_bins, 1,
                            lay.p.CHt, lay.p.Ct, half_spread, k_impact, aum, ADV, SIG,
-                           ws + lay.turn, ws + lay.cost, gen_list, gen_count);
+                           ws + lay.turn, ws + lay.cost, gen_list, gen_count,
+                           (const double*)TPv, (const uint32_t*)TPm);
       }
       LAUNCH_CHECK(ctx, "k_turnover");
     }

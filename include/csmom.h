@@ -62,7 +62,10 @@ int csm_abi_version(void);
  * sizing the portfolio workspace), "overlap_rows" (cohort -> PR combine: 1 one thread per
  * (month, panel, decile) serving every K of the set when the cohort plan has one chunk, the
  * default | 0 one per (K, month, panel, decile)), "seg_stage2" (segment cohort sums: 1 the
- * return row staged with 16-B loads, the default | 0 an 8-B loop).  Returns
+ * return row staged with 16-B loads, the default | 0 an 8-B loop), "turn_gen_grid" (workgroups
+ * of the persistent general-row turnover launch, default 8192), "turn_prep" (steady equal-weight
+ * turnover rows: 1 factors from a once-per-row k_turn_prep, the default | 0 each workgroup's
+ * own prologue).  Returns
  * CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with

@@ -472,3 +472,30 @@ def test_overlap_rows_bit_identical(engine, B, legs, vw, Ks):
     for K in set(Ks):
         for f in ("PR", "LS", "TURN", "COST", "NET"):
             assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
+
+
+@pytest.mark.parametrize("B,legs,Ks", [(1, False, (3, 6, 12)), (16, True, (3, 6, 9, 12)),
+                                       (6, True, (12, 1)), (16, False, (2, 2, 7))])
+def test_turn_prep_bit_identical(engine, B, legs, Ks):
+    """Steady equal-weight turnover rows with k_turn_prep's once-per-row factors (turn_prep 1)
+    against each workgroup's own prologue (0): TURN / COST / NET / LS bit for bit, including
+    the first months (general rows, routed by the prepared full-leg masks)."""
+    L, NR, _, _ = _labels(engine, "c1")
+    T_m, N = L.shape
+    assert N % 4 == 0
+    if B > 1:
+        rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 7 * i, axis=1) for i in range(B)],
+                                     axis=1).reshape(T_m, B * N))
+        L, NR = rep(L), rep(NR)
+    lib = engine.lib
+    got = {}
+    try:
+        for mode in (1, 0):
+            assert lib.csm_tune(b"turn_prep", mode) == 0
+            got[mode] = engine.portfolio_multi(L, NR, 10, Ks=Ks, B=B, legs_only=legs)
+    finally:
+        lib.csm_tune(b"turn_prep", 1)
+    for K in set(Ks):
+        for f in ("TURN", "COST", "NET", "LS"):
+            assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
+        assert np.isfinite(got[1][K].TURN.cpu().numpy()[-1]).all()

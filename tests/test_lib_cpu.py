@@ -77,7 +77,8 @@ def test_tune_keys_documented_in_header_are_accepted():
              b"signal_bl": ([0, 1], 1), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
              b"turn_list": ([0, 1, 2], 1), b"sort_wave": ([0, 1], 1),
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
-             b"seg_stage2": ([0, 1], 1)}
+             b"seg_stage2": ([0, 1], 1), b"turn_gen_grid": ([1, 2048], 8192),
+             b"turn_prep": ([0, 1], 1)}
     for key, (vals, default) in cases.items():
         for v in vals:
             assert lib.csm_tune(key, v) == 0, (key, v)
