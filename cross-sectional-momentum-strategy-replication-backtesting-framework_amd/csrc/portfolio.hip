@@ -1059,7 +1059,10 @@ __device__ __forceinline__ void turnover_body(
 // BM (general launch, equal weight, every K <= 31): only the bit-mask path is compiled, so the
 // kernel keeps the registers of that path (the dense path's arrays would double them).
 template <bool VW, bool IMP, bool GEN, bool BM = false>
-__global__ __launch_bounds__(PF_THREADS) void k_turnover(
+#ifndef TO_MINB_BM
+#define TO_MINB_BM 1   // general equal-weight rows: workgroups per CU the VGPR budget must allow
+#endif
+__global__ __launch_bounds__(PF_THREADS, BM ? TO_MINB_BM : 1) void k_turnover(
     const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
     int T_m, int B, int64_t N, KSet ks, int Kmax, int n_bins, int Cf, int64_t CH,
     int Ct, double half_spread, double k_impact, double aum, const double* __restrict__ ADV,

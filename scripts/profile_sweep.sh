@@ -18,6 +18,6 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_
 rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/pmc_write.log"; echo "FATAL write rc=$rc"; exit $rc; }
 python3 scripts/pmc_summary.py "$OUT" --N 5000 --T_d 6522 --workload "bench.py --config $CFG" \
   --source "profiles/$TAG/${CFG}_pmc_summary.json" --config "$CFG" --step-runs $NRUN \
-  --stage "portfolio=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turnover,k_overlap,k_ls" \
+  --stage "portfolio=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turn_prep,k_turnover,k_overlap,k_overlap_rows,k_ls" \
   --stage-label "portfolio(k_cohort+k_turnover+k_overlap+k_ls)"
 echo "profile_sweep done"
