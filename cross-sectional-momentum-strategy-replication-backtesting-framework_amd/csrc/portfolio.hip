@@ -877,16 +877,23 @@ __device__ __forceinline__ void turnover_body(
       // as the dense loop below)
       const uint32_t topw = (uint32_t)dtop * 0x01010101u;
       auto beq = [](uint32_t z) { return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u; };
-      for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS) {
+      // ages whose cohort is empty on both legs contribute nothing (their bits add inv 0.0,
+      // and a leg with an empty age in either window is not full, so its counts are unused):
+      // their label loads are skipped (the first months of a panel: most ages are empty)
+      uint32_t amask = 0;
+      for (int j = 0; j <= jmax; ++j) amask |= (inv[0][j] != 0.0 || inv[1][j] != 0.0) ? 1u << j : 0u;
+      for (int64_t a4 = a0 + cw * tid; a4 < a1 && amask; a4 += cw * PF_THREADS) {
         uint32_t mt4[4] = {0, 0, 0, 0}, mb4[4] = {0, 0, 0, 0};
         if (cw == 4) {
           // the 4 cells' labels of 8 ages per trip as label words, all loads in flight
           for (int j0 = 0; j0 <= jmax; j0 += 8) {
+            if (!((amask >> j0) & 0xFFu)) continue;
             uint32_t wv[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-              wv[u] = j0 + u <= jmax ? *(const uint32_t*)(L + rt - (int64_t)(j0 + u) * rowstep + a4)
-                                     : 0xFFFFFFFFu;
+              wv[u] = (j0 + u <= jmax && ((amask >> (j0 + u)) & 1u))
+                          ? *(const uint32_t*)(L + rt - (int64_t)(j0 + u) * rowstep + a4)
+                          : 0xFFFFFFFFu;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
               const uint32_t et = beq(wv[u] ^ topw) >> 7, eb = beq(wv[u]) >> 7;   // bits 0,8,16,24
