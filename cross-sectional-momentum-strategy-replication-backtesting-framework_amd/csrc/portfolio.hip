@@ -396,12 +396,20 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
   const int nw = (int)(N >> 2);
   const uint32_t topw = (uint32_t)(NB - 1) * 0x01010101u;
   const uint64_t lt = (1ull << lane) - 1ull;
+  // the whole row in registers (N <= SEG_MAXN: at most LS_RW words per lane), every load in
+  // flight at once, read once for both passes
+  constexpr int LS_RW = (SEG_MAXN / 4 + 63) / 64;
+  uint32_t vr[LS_RW];
+#pragma unroll
+  for (int k = 0; k < LS_RW; ++k) {
+    const int wi = k * 64 + lane;
+    vr[k] = wi < nw ? L4[wi] : 0xFFFFFFFFu;
+  }
   int nb0 = 0, nt0 = 0;   // per-lane counts: bottom (decile 0), top (decile NB - 1)
-  for (int w0 = 0; w0 < nw; w0 += 64) {
-    const int wi = w0 + lane;
-    const uint32_t v = wi < nw ? L4[wi] : 0xFFFFFFFFu;
-    nb0 += __popc(byte_eq0(v));
-    nt0 += __popc(byte_eq0(v ^ topw));
+#pragma unroll
+  for (int k = 0; k < LS_RW; ++k) {
+    nb0 += __popc(byte_eq0(vr[k]));
+    nt0 += __popc(byte_eq0(vr[k] ^ topw));
   }
   for (int o = 32; o > 0; o >>= 1) { nb0 += __shfl_xor(nb0, o, 64); nt0 += __shfl_xor(nt0, o, 64); }
   const int rb = (nb0 + 3) & ~3, rt = (nt0 + 3) & ~3;
@@ -414,9 +422,11 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
     FWp[(row * C + c) * 2 + leg] = c == 0 ? (double)(leg == 0 ? nt0 : nb0) : 0.0;
   }
   int pb = 0, pt = rb;   // next position of each leg's segment
-  for (int w0 = 0; w0 < nw; w0 += 64) {
-    const int wi = w0 + lane;
-    const uint32_t v = wi < nw ? L4[wi] : 0xFFFFFFFFu;
+#pragma unroll
+  for (int k = 0; k < LS_RW; ++k) {
+    if (k * 64 >= nw) break;
+    const int wi = k * 64 + lane;
+    const uint32_t v = vr[k];
     const uint32_t eb = byte_eq0(v), et = byte_eq0(v ^ topw);
     int bb = pb, bt = pt;   // this lane's first position of each leg
     int totb = 0, tott = 0;
