@@ -51,7 +51,7 @@ REFERENCE_PANDAS = {"value": 1.41e6, "unit": "asset-days/s", "cores": 1, "kind":
                              "BASELINE.md, C4 proxy 1e8 asset-days, extrapolated linearly"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -87,7 +87,17 @@ def parse():
     ap.add_argument("--per-j-scan", action="store_true",
                     help="C5: one scan per J instead of every J of a wide batch from one scan "
                          "(csm_momentum_multi, the default)")
-    return ap.parse_args()
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group: nccl (= RCCL over xGMI, one GPU per rank) or gloo "
+                         "(device tensors staged through host memory; the 1-GPU rehearsal of the "
+                         "multi-rank path, tests/test_gpu_bench_ranks.py)")
+    ap.add_argument("--collective", default="torch", choices=["torch", "csm"],
+                    help="N>1 date shards: the all-gathers through torch.distributed, or through "
+                         "libcsmom.so's own RCCL communicator (csm_allgather, the C-ABI path)")
+    ap.add_argument("--dump", default=None,
+                    help="rank 0 saves the pass's results (.npz: LS / EW / CNT, or the sweep's "
+                         "summary table) for comparison with a 1-GPU run")
+    return ap.parse_args(argv)
 
 
 def apply_tunes(eng, tunes):
@@ -156,27 +166,82 @@ def cpu_baseline_sweep(config: str, n_assets: int, days: int, start: str):
                        f"on {B} panels x {n_assets} assets x {T_m} months, {dt:.1f} s")
 
 
-def main():
-    args = parse()
+def dist_setup(args):
+    """(world, rank, device) from the torchrun environment; the process group for N > 1 on
+    args.backend (nccl = RCCL, one GPU per rank; gloo = host-staged, the 1-GPU rehearsal)."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N>1 must be launched with torchrun (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1 and not dist.is_initialized():
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, dev
+
+
+def allreduce_host(vals, op, dev):
+    """Reduce a few host floats over all ranks (max / sum); device tensors for RCCL, host
+    tensors for gloo."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return list(vals)
+    on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor(list(vals), dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=op)
+    return [float(x) for x in t.cpu().tolist()]
+
+
+def dist_close():
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def lib_sha256():
+    import hashlib
+    import csmom
+    return hashlib.sha256(Path(csmom.lib_path()).read_bytes()).hexdigest()
+
+
+def committed_profile(config, N, T_d, lib_hash):
+    """The committed rocprofv3 evidence for this workload (profiles/<round>/<config>_profile.json,
+    scripts/profile.sh): per-kernel average durations from --kernel-trace --stats of the bench
+    command and HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes.  Used only
+    when it was taken on THIS build of libcsmom.so (sha256) at this workload, else None."""
+    for f in sorted((ROOT / "profiles").glob(f"r*/{config}_profile.json"), reverse=True):
+        try:
+            pj = json.loads(f.read_text())
+        except Exception:
+            continue
+        if pj.get("N") == N and pj.get("T_d") == T_d and pj.get("lib_sha256") == lib_hash:
+            pj["path"] = str(f.relative_to(ROOT))
+            return pj
+    return None
+
+
+def main(argv=None):
+    args = parse(argv)
     if args.config in SWEEP_CONFIGS:
         return sweep_main(args)
     import torch
     import torch.distributed as dist
 
     import csmom
-    from csmom.distributed import DateShardPipeline
+    from csmom.distributed import CsmCollective, DateShardPipeline
     from csmom.synth import make_device_panel, shard_calendar
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torchrun (one process per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, dev = dist_setup(args)
+    local = dev.index
 
     cfg = dict(CONFIGS[args.config])
     N = args.assets or cfg["N"]
@@ -194,8 +259,9 @@ def main():
     max_days = int(np.diff(ms_host).max())
     min_days = int(np.diff(ms_host)[1:-1].min()) if len(ms_host) > 3 else 1 << 30   # interior months
     fused = eng.use_fused(panel.P, None, max_days)
+    coll = CsmCollective(eng) if world > 1 and args.collective == "csm" else None
     pipe = (DateShardPipeline(eng, months, J, skip, nb,
-                              fused=fused and args.shard_mode == "fused")
+                              fused=fused and args.shard_mode == "fused", collective=coll)
             if world > 1 else None)
     PM = None if fused else eng.empty((T_m, N))
     M, NR = eng.empty((T_m, N)), eng.empty((T_m, N))
@@ -284,10 +350,7 @@ def main():
         for k in range(args.steps):
             step(step_events[k])
         torch.cuda.synchronize()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = allreduce_host([elapsed], dist.ReduceOp.MAX if world > 1 else None, dev)[0]
 
     if world == 1:
         for ev in step_events:
@@ -296,34 +359,41 @@ def main():
         stage_ms[:] = np.nan
 
     # decile match vs the oracle (metric: "decile match %"): the oracle's qcut on the engine's
-    # mom_J for every date (or --match-dates evenly spaced ones), labels compared cell by cell
-    match = None
-    if rank == 0:
-        from oracle import csmom_oracle as O
-        if world > 1:
-            r = pipe.run(panel.P, panel.month_start, max_days)
-            Mh, Lh = r.M, r.L
-        else:
-            Mh, Lh = M, L
-        if args.match_dates > 0:
-            dates = sorted({int(x) for x in np.linspace(0, T_m - 1, args.match_dates)})
-        else:
-            dates = list(range(T_m))
-        tot = ok = 0
-        for t0 in range(0, len(dates), 64):
-            blk = dates[t0:t0 + 64]
-            mrows = Mh[blk].cpu().numpy()
-            lrows = Lh[blk].cpu().numpy()
-            for row, got in zip(mrows, lrows):
-                ref = np.full(N, -1, dtype=np.int8)
-                v = ~np.isnan(row)
-                if v.any():
-                    lab = O.qcut_labels(row[v], nb)
-                    ref[v] = np.where(np.isnan(lab), -1, lab).astype(np.int8)
-                ok += int((got == ref).sum())
-                tot += N
-        match = dict(pct=100.0 * ok / tot, sample=f"{len(dates)} of {T_m} dates x {N} assets: "
-                                                  f"oracle qcut of the engine's mom_J")
+    # mom_J for every date (or --match-dates evenly spaced ones), labels compared cell by cell.
+    # N > 1: EVERY rank runs the (collective-bearing) pass and checks its own months; the
+    # counts are summed over the ranks.
+    from oracle import csmom_oracle as O
+    if world > 1:
+        res = pipe.run(panel.P, panel.month_start, max_days)
+        Mh, Lh, LSh, EWh, CNTh = res.M, res.L, res.LS, res.EW, res.CNT
+    else:
+        Mh, Lh, LSh, EWh, CNTh = M, L, LS, EW, CNT
+    if args.match_dates > 0:
+        dates = sorted({int(x) for x in np.linspace(0, T_m - 1, args.match_dates)})
+    else:
+        dates = list(range(T_m))
+    tot = ok = 0
+    for t0 in range(0, len(dates), 64):
+        blk = dates[t0:t0 + 64]
+        mrows = Mh[blk].cpu().numpy()
+        lrows = Lh[blk].cpu().numpy()
+        for row, got in zip(mrows, lrows):
+            ref = np.full(N, -1, dtype=np.int8)
+            v = ~np.isnan(row)
+            if v.any():
+                lab = O.qcut_labels(row[v], nb)
+                ref[v] = np.where(np.isnan(lab), -1, lab).astype(np.int8)
+            ok += int((got == ref).sum())
+            tot += N
+    ok, tot, ndates = allreduce_host([ok, tot, len(dates)],
+                                     dist.ReduceOp.SUM if world > 1 else None, dev)
+    tm_all = sum(pipe.months) if pipe is not None else T_m
+    match = dict(pct=100.0 * ok / tot,
+                 sample=f"{int(ndates)} of {tm_all} dates x {N} assets"
+                        f"{f' (all {world} ranks)' if world > 1 else ''}: oracle qcut of the "
+                        f"engine's mom_J")
+    if rank == 0 and args.dump:
+        np.savez(args.dump, LS=LSh.cpu().numpy(), EW=EWh.cpu().numpy(), CNT=CNTh.cpu().numpy())
 
     ms_per_step = 1000.0 * elapsed / args.steps
     units = N * T_d * world if args.scaling == "weak" else N * total_days
@@ -341,19 +411,21 @@ def main():
                 kname = "k_month_end"
                 alg_me = 8.0 * N * T_d + 8.0 * N * T_m          # read P once, write PM once
             achieved = alg_me / (me_ms * 1e-3) / 1e9
-            traffic = None
-            pmc = ROOT / "profiles" / f"pmc_{kname}.json"
-            if pmc.exists():
-                try:
-                    pj = json.loads(pmc.read_text())
-                    if pj.get("N") == N and pj.get("T_d") == T_d:
-                        traffic = pj.get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
+            # the committed rocprofv3 run of this exact bench command on this build (else null)
+            prof = committed_profile(args.config, N, T_d, lib_sha256())
+            pk = (prof or {}).get("kernels", {}).get(kname, {})
+            traffic = pk.get("hbm_bytes_per_launch")
             roofline = dict(bound="hbm", kernel=kname, achieved=round(achieved, 1),
                             peak=HBM_PEAK_GBS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
                             traffic=traffic, algorithmic_bytes_per_launch=alg_me,
                             avg_launch_ms=round(me_ms, 4))
+            if pk.get("avg_ns"):
+                # the same roofline from the committed profile's kernel average: a reader
+                # recomputes it from profiles/ (alg bytes / avg_ns / peak)
+                roofline["profile_frac"] = round(alg_me / (pk["avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+                roofline["profile_avg_launch_ms"] = round(pk["avg_ns"] * 1e-6, 4)
+                roofline["profile"] = dict(path=prof["path"], commit=prof.get("git_head"),
+                                           box_note="rocprofv3 run on another box than this line")
         pipe_gbs = alg_pipe * world / (ms_per_step * 1e-3) / 1e9
         out = {
             "metric": "asset-periods backtested/sec (1/2/4/8 GPU) + % HBM peak BW; decile match %",
@@ -397,9 +469,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_assets, T_d, cfg["start"])
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    dist_close()
+    return out
 
 
 class TimedStages:
@@ -482,15 +553,27 @@ class TimedStages:
 
 def sweep_traffic(config, N, T_d, stage):
     """HBM bytes per step of the dominant sweep stage from the committed PMC passes
-    (profiles/pmc_sweep_<config>.json, scripts/profile_sweep.sh), when they match this run."""
-    f = ROOT / "profiles" / f"pmc_sweep_{config}.json"
-    try:
-        pj = json.loads(f.read_text())
-        if pj.get("N") == N and pj.get("T_d") == T_d and pj.get("stage_label") == stage:
-            return pj.get("hbm_bytes_per_step")
-    except Exception:
-        pass
+    (profiles/<round>/<config>_profile.json, scripts/profile.sh), only when they were taken on
+    THIS build of libcsmom.so at this workload and name this stage; else None."""
+    pj = committed_profile(config, N, T_d, lib_sha256())
+    st = (pj or {}).get("stage", {})
+    if st.get("label") == stage:
+        return st.get("hbm_bytes_per_step")
     return None
+
+
+def sweep_profile(config, N, T_d, stage, alg_bytes):
+    """profile_frac of the dominant stage from the committed rocprofv3 kernel averages (the
+    stage's kernels' device time per step), with the profile's path and commit."""
+    pj = committed_profile(config, N, T_d, lib_sha256())
+    st = (pj or {}).get("stage", {})
+    if st.get("label") != stage or not st.get("ns_per_step"):
+        return {}
+    ms = st["ns_per_step"] * 1e-6
+    return {"profile_frac": round(alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "profile_avg_ms_per_step": round(ms, 4),
+            "profile": {"path": pj["path"], "commit": pj.get("git_head"),
+                        "box_note": "rocprofv3 run on another box than this line"}}
 
 
 def sweep_main(args):
@@ -502,15 +585,8 @@ def sweep_main(args):
     import csmom
     from csmom.synth import bday_calendar, make_device_panel
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N>1 must be launched with torchrun (one process per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, dev = dist_setup(args)
+    local = dev.index
     cfg = dict(SWEEP_CONFIGS[args.config])
     N = args.assets or cfg["N"]
     T_d = args.days or cfg["days"]
@@ -569,11 +645,9 @@ def sweep_main(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = allreduce_host([elapsed], dist.ReduceOp.MAX if world > 1 else None, dev)[0]
     stages = ts.stage_report(args.steps)
+    line = None
     if rank == 0:
         dom = max(stages.items(), key=lambda kv: kv[1][0])
         dname, (dms, dbytes) = dom
@@ -599,6 +673,7 @@ def sweep_main(args):
             "roofline": {"bound": "hbm", "kernel": dname, "achieved": round(ach, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                          "traffic": sweep_traffic(args.config, N, T_d, dname),
+                         **sweep_profile(args.config, N, T_d, dname, dbytes),
                          "algorithmic_bytes_per_step": dbytes,
                          "avg_ms_per_step": round(dms, 4)},
             "pipeline_roofline": {"bound": "hbm", "achieved": round(alg_step / (ms_step * 1e-3) / 1e9, 1),
@@ -612,10 +687,11 @@ def sweep_main(args):
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_sweep(args.config, 1500 if args.config == "c3" else 1000,
                                                       T_d, cfg["start"])
+        if args.dump:
+            np.savez(args.dump, table=res)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    dist_close()
+    return line
 
 
 if __name__ == "__main__":

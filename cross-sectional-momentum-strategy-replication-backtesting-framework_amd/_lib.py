@@ -15,23 +15,9 @@ PKG_DIR = Path(__file__).resolve().parent
 CSM_OK = 0
 CSM_E_INVAL = -1
 CSM_E_HIP = -2
+CSM_E_RCCL = -3
+UNIQUE_ID_BYTES = 128
 ABSENT_BITS = 0x7FF4000000000001
-
-EXPORTS = (
-    "csm_abi_version", "csm_create", "csm_destroy", "csm_last_error", "csm_set_stream",
-    "csm_sync", "csm_month_end", "csm_momentum", "csm_deciles", "csm_long_short",
-    "csm_shard_summary", "csm_fold_carry", "csm_signal", "csm_momentum_chunked",
-    "csm_momentum_chunked_workspace", "csm_tune", "csm_signal_tiled", "csm_tile_panel",
-    "csm_tiled_size", "csm_portfolio", "csm_portfolio_workspace", "csm_bootstrap",
-    "csm_cohort_sums", "csm_portfolio_from_cohorts", "csm_turnover_features",
-    "csm_double_sort_labels", "csm_tune_ptr", "csm_next_present",
-    "csm_last_present_month", "csm_portfolio_from_cohorts_multi", "csm_summary",
-    "csm_shard_repair", "csm_signal_shard", "csm_shard_summary_state", "csm_momentum_multi",
-    "csm_signal_ids", "csm_deciles_ids", "csm_pipeline", "csm_momentum_multi_ids",
-    "csm_cohort_sums_legs", "csm_portfolio_from_cohorts_legs", "csm_signal_shard_ids",
-    "csm_shard_repair_ids",
-)
-
 
 class CsmUnavailable(RuntimeError):
     """libcsmom.so is missing or failed to load (the engine has no CPU fallback)."""
@@ -55,76 +41,81 @@ _i64 = ctypes.c_int64
 _f64 = ctypes.c_double
 
 
-def _declare(lib):
-    sig = {
-        "csm_abi_version": (ctypes.c_int, []),
-        "csm_tune": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
-        "csm_tune_ptr": (ctypes.c_int, [ctypes.c_char_p, _p]),
-        "csm_next_present": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _p, _p]),
-        "csm_last_present_month": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _p]),
-        "csm_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
-        "csm_destroy": (ctypes.c_int, [_p]),
-        "csm_last_error": (ctypes.c_char_p, [_p]),
-        "csm_set_stream": (ctypes.c_int, [_p, _p]),
-        "csm_sync": (ctypes.c_int, [_p]),
-        "csm_month_end": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i32, _p, _p]),
-        "csm_momentum": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p]),
-        "csm_momentum_multi": (ctypes.c_int, [_p, _p, _i32, _i64, _p, _i32, _i32, _p, _p]),
-        "csm_momentum_multi_ids": (ctypes.c_int, [_p, _p, _i32, _i64, _p, _i32, _i32, _p, _p, _p]),
-        "csm_signal": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
-                                      _p, _p, _p]),
-        "csm_signal_tiled": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p,
+# ctypes prototypes of every entry point include/csmom.h declares (tests/test_abi_boundary.py
+# checks them against the header's parameter lists)
+SIGNATURES = {
+    "csm_abi_version": (ctypes.c_int, []),
+    "csm_tune": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "csm_tune_ptr": (ctypes.c_int, [ctypes.c_char_p, _p]),
+    "csm_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "csm_destroy": (ctypes.c_int, [_p]),
+    "csm_last_error": (ctypes.c_char_p, [_p]),
+    "csm_set_stream": (ctypes.c_int, [_p, _p]),
+    "csm_sync": (ctypes.c_int, [_p]),
+    "csm_month_end": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i32, _p, _p]),
+    "csm_momentum": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p]),
+    "csm_momentum_multi": (ctypes.c_int, [_p, _p, _i32, _i64, _p, _i32, _i32, _p, _p]),
+    "csm_momentum_multi_ids": (ctypes.c_int, [_p, _p, _i32, _i64, _p, _i32, _i32, _p, _p, _p]),
+    "csm_signal": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _p,
+                                  _p, _p, _p]),
+    "csm_portfolio_workspace": (ctypes.c_int64, [_i32, _i32, _i64, _i32, _i32]),
+    "csm_portfolio": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _f64, _f64,
+                                     _f64, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "csm_cohort_sums": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _p]),
+    "csm_portfolio_from_cohorts": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32, _i32,
+                                                  _i32, _f64, _f64, _f64, _p, _p, _p, _p,
+                                                  _p, _p, _p, _p]),
+    "csm_turnover_features": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p,
+                                             _p]),
+    "csm_double_sort_labels": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p]),
+    "csm_portfolio_from_cohorts_multi": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
+                                                        _i32, _i32, _p, _f64, _f64, _f64, _p,
+                                                        _p, _p, _p, _p, _p, _p, _p]),
+    "csm_cohort_sums_legs": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _p]),
+    "csm_portfolio_from_cohorts_legs": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
+                                                       _i32, _i32, _p, _f64, _f64, _f64, _p,
+                                                       _p, _p, _p, _p, _p, _p, _p, _p]),
+    "csm_summary": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _f64, _p]),
+    "csm_bootstrap": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64,
+                                     _f64, _p, _p]),
+    "csm_momentum_chunked": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _i32, _p, _p, _p,
+                                            _p, _p]),
+    "csm_momentum_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),
+    "csm_deciles": (ctypes.c_int, [_p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
+    "csm_long_short": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p]),
+    "csm_shard_summary": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p]),
+    "csm_fold_carry": (ctypes.c_int, [_p, _p, _i32, _i32, _i64, _i32, _i32, _p, _p]),
+    "csm_shard_repair": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p,
+                                        _p, _p, _p]),
+    "csm_signal_shard": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p,
+                                        _p, _p, _p, _p]),
+    "csm_signal_shard_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32,
+                                            _p, _p, _p, _p, _p, _p]),
+    "csm_shard_repair_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _p,
                                             _p, _p, _p, _p, _p]),
-        "csm_tiled_size": (ctypes.c_int64, [_i64, _i64]),
-        "csm_portfolio_workspace": (ctypes.c_int64, [_i32, _i32, _i64, _i32, _i32]),
-        "csm_portfolio": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _f64, _f64,
-                                         _f64, _p, _p, _p, _p, _p, _p, _p, _p]),
-        "csm_cohort_sums": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _p]),
-        "csm_portfolio_from_cohorts": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32, _i32,
-                                                      _i32, _f64, _f64, _f64, _p, _p, _p, _p,
-                                                      _p, _p, _p, _p]),
-        "csm_turnover_features": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p,
-                                                 _p]),
-        "csm_double_sort_labels": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i64, _i32, _p, _p]),
-        "csm_portfolio_from_cohorts_multi": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
-                                                            _i32, _i32, _p, _f64, _f64, _f64, _p,
-                                                            _p, _p, _p, _p, _p, _p, _p]),
-        "csm_cohort_sums_legs": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _p]),
-        "csm_portfolio_from_cohorts_legs": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
-                                                           _i32, _i32, _p, _f64, _f64, _f64, _p,
-                                                           _p, _p, _p, _p, _p, _p, _p, _p]),
-        "csm_summary": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _f64, _p]),
-        "csm_bootstrap": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64,
-                                         _f64, _p, _p]),
-        "csm_tile_panel": (ctypes.c_int, [_p, _p, _i64, _i64, _p]),
-        "csm_momentum_chunked": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _i32, _p, _p, _p,
-                                                _p, _p]),
-        "csm_momentum_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),
-        "csm_deciles": (ctypes.c_int, [_p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
-        "csm_long_short": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p]),
-        "csm_shard_summary": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _p]),
-        "csm_fold_carry": (ctypes.c_int, [_p, _p, _i32, _i32, _i64, _i32, _i32, _p, _p]),
-        "csm_shard_repair": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p,
-                                            _p, _p, _p]),
-        "csm_signal_shard": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p,
-                                            _p, _p, _p, _p]),
-        "csm_signal_shard_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32,
-                                                _p, _p, _p, _p, _p, _p]),
-        "csm_shard_repair_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _p,
-                                                _p, _p, _p, _p, _p]),
-        "csm_shard_summary_state": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p,
-                                                   _p]),
-        "csm_signal_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _p,
-                                          _p, _p, _p, _p]),
-        "csm_deciles_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
-        "csm_pipeline": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _i32,
-                                        _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
-    }
-    for name, (res, args) in sig.items():
+    "csm_shard_summary_state": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p,
+                                               _p]),
+    "csm_signal_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _p,
+                                      _p, _p, _p, _p]),
+    "csm_deciles_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
+    "csm_pipeline": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _i32,
+                                    _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "csm_comm_unique_id": (ctypes.c_int, [_p]),
+    "csm_allgather_init": (ctypes.c_int, [_p, _p, _i32, _i32]),
+    "csm_allgather": (ctypes.c_int, [_p, _p, _p, _i64]),
+    "csm_allgather_free": (ctypes.c_int, [_p]),
+}
+
+
+def _declare(lib):
+    for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     return lib
+
+
+EXPORTS = tuple(SIGNATURES)
 
 
 def load_library():

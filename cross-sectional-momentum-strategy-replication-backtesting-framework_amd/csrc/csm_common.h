@@ -30,6 +30,8 @@ struct csm_ctx {
   int n_cu;               // compute units of the device (decile kernel choice)
   int32_t* dec_flg;       // [dec_flg_n] rows the merged decile pass left to the general kernel
   int32_t dec_flg_n;      // (allocated at create, so a captured pipeline never allocates)
+  void* comm;             // RCCL communicator of csm_allgather_init (collective.hip), or NULL
+  int comm_rank, comm_size;
 };
 
 static inline int set_err(csm_ctx* c, int code, const char* fmt, ...) {
@@ -102,7 +104,7 @@ __device__ __forceinline__ uint32_t csm_fid(double x) {
 template <int NB>
 void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                           int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
+                           int32_t* CNT, int32_t* NV, int64_t* tim);
 
 // fused-pipeline decile launcher on the bucket ids of csm_signal_ids (deciles_pre.hip),
 // NB in {0,2,3,4,5,10,20}.  flg (T_m ints) non-NULL: the merged kernel first, then the general
@@ -110,37 +112,11 @@ void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, co
 template <int NB>
 void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
-                        int32_t* NV, int ablate, int64_t* tim, uint16_t* ids, int32_t* flg,
-                        bool merged_only);
-
-// narrow rows with register-resident bucket ids (deciles_narrow.hip, RI mode): N even,
-// N <= deciles_narrow_reg_max_n(), 16-B aligned M / NR
-#define DEC_NREG_RI 5
-int deciles_narrow_reg_max_n();
-template <int NB>
-void launch_deciles_narrow_reg(int T_m, hipStream_t st, const double* M, const double* NR,
-                               int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
+                        int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg);
 
 // the same on narrow rows (deciles_npre.hip: 2048 buckets = the fixed map's ids >> 2)
 template <int NB>
 void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim,
-                               uint16_t* ids, int32_t* flg, bool merged_only);
-
-// one-wave-per-row decile launcher (deciles_wave.hip), NB in {0,2,3,4,5,10,20}
-template <int NB>
-void launch_deciles_wave(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
-                         int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                         int32_t* CNT, int32_t* NV, int ablate, int64_t* tim);
-
-// wide-row decile launcher with register-resident bucket ids (deciles_reg.hip): rows with
-// N even and N <= deciles_reg_max_n(), 16-B aligned M / NR, 2-B aligned L.  The first
-// DEC_REG_RI x 2048 cells of a row keep their ids in registers; the rest are re-read.
-#define DEC_REG_RI 46   // 2 x 46 id VGPRs per lane (48: a few spills)
-int deciles_reg_max_n();
-template <int NB>
-void launch_deciles_reg(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
-                        int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
-                        int32_t* NV, int ablate, int64_t* tim);
+                               int32_t* CNT, int32_t* NV, int64_t* tim, uint16_t* ids,
+                               int32_t* flg);

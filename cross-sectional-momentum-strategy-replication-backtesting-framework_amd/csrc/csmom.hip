@@ -124,41 +124,6 @@ __global__ __launch_bounds__(256) void k_month_end(const double* __restrict__ P,
   }
 }
 
-// Kernel A' (one-shot month-end): one thread per (two assets, month) issues all MAXD day-row
-// loads of its month at once (rows past the month's end re-load its last row: cache hits that
-// change neither "last non-NaN" nor "any present"), reduces and exits.  The grid sweeps the
-// panel in address order, the access pattern of the fastest read microbenchmark (scripts/mb).
-template <int MAXD>
-__global__ __launch_bounds__(256) void k_month_end_rows(const double* __restrict__ P,
-                                                        const int64_t* __restrict__ month_start,
-                                                        int64_t N, double* __restrict__ PM) {
-  const int m = blockIdx.y;
-  const int64_t a = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
-  if (a >= N) return;
-  const int64_t f0 = month_start[m], nn = month_start[m + 1] - f0;
-  const double* p = P + f0 * N + a;
-  double2 X[MAXD];
-#pragma unroll
-  for (int k = 0; k < MAXD; ++k)
-    X[k] = *reinterpret_cast<const double2*>(p + (int64_t)(k < nn ? k : nn - 1) * N);
-  double pm[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    double last = 0.0;
-    bool pr = false, v = false;
-#pragma unroll
-    for (int k = 0; k < MAXD; ++k) {
-      const double x = c == 0 ? X[k].x : X[k].y;
-      const bool ok = x == x;
-      pr |= !is_absent(x);
-      v |= ok;
-      last = ok ? x : last;
-    }
-    pm[c] = pr ? (v ? last : qnan()) : absent_val();
-  }
-  *reinterpret_cast<double2*>(PM + (int64_t)m * N + a) = make_double2(pm[0], pm[1]);
-}
-
 // =====================================================================================
 // Per-asset scan state and one present-row step (shared by k_momentum and k_signal).
 // The J+skip ring of factors fl(1+ret) lives in LDS, slot-major with a per-lane column
@@ -188,16 +153,7 @@ __device__ __forceinline__ void scan_init(ScanLane& s, double* ring, int RS, int
   s.prev = -1;
 }
 
-// Output stores of the scan: ST = 0 plain, 1 nontemporal (the monthly panels are consumed by
-// the next kernel from HBM anyway), 2 none (profiling ablation only: results are discarded).
-template <int ST>
-__device__ __forceinline__ void st_out(double* p, double v) {
-  if (ST == 0) *p = v;
-  else if (ST == 1) __builtin_nontemporal_store(v, p);
-}
-
 // Consumes month m's price x of asset a; returns mom (NaN when absent / undefined).
-template <int ST = 0>
 __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double* ring, int RS,
                                             int W, int J, int64_t N, int64_t a,
                                             double* __restrict__ R, double* __restrict__ M,
@@ -205,9 +161,9 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
   const double NaN = qnan();
   const int64_t o = (int64_t)m * N + a;
   if (is_absent(x)) {
-    if (R) st_out<ST>(R + o, NaN);
-    st_out<ST>(M + o, NaN);
-    st_out<ST>(NR + o, NaN);
+    if (R) R[o] = NaN;
+    M[o] = NaN;
+    NR[o] = NaN;
     return NaN;
   }
   const bool xv = !isnan_d(x);
@@ -225,17 +181,16 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
   const double mom = acc - 1.0;
   const bool ranked = !isnan_d(mom);
   const double ps_new = xv ? x : s.psff;
-  if (s.prev >= 0) st_out<ST>(NR + (int64_t)s.prev * N + a, ps_new / s.psff - 1.0);
+  if (s.prev >= 0) NR[(int64_t)s.prev * N + a] = ps_new / s.psff - 1.0;
   if (ranked) {
     s.psff = ps_new;
     s.prev = m;
   } else {
-    st_out<ST>(NR + o, NaN);
+    NR[o] = NaN;
     s.prev = -1;
   }
-  if (R) st_out<ST>(R + o, ret);
-  st_out<ST>(M + o, mom);
-  if (ST == 2 && mom == 1234.5678) M[o] = mom;  // keeps the ablated scan's work alive
+  if (R) R[o] = ret;
+  M[o] = mom;
   return mom;
 }
 
@@ -243,23 +198,6 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
 // (and ret_1m) as one 16-B store per row, next_ret as one 16-B store when both assets write
 // the same row (the steady state), so a wave issues half the store instructions.  Same
 // arithmetic in the same order as two scan_step calls: bit-identical outputs.
-// Output stores of the paired scan: plain, or nontemporal (NT) -- the monthly panels are
-// streamed past the caches to the next kernel.
-template <bool NT>
-__device__ __forceinline__ void st_d2(double* p, double a, double b) {
-  if (NT) {
-    __builtin_nontemporal_store(a, p);
-    __builtin_nontemporal_store(b, p + 1);
-  } else {
-    *reinterpret_cast<double2*>(p) = make_double2(a, b);
-  }
-}
-template <bool NT>
-__device__ __forceinline__ void st_d1(double* p, double a) {
-  if (NT) __builtin_nontemporal_store(a, p);
-  else *p = a;
-}
-template <bool NT = false>
 __device__ __forceinline__ void scan_step_pair(ScanLane (&s)[2], const double (&x)[2], int m,
                                                double* ring0, int RS, int W, int J, int64_t N,
                                                int64_t a0, double* __restrict__ R,
@@ -318,63 +256,6 @@ __device__ __forceinline__ void scan_step_pair(ScanLane (&s)[2], const double (&
   } else {
     if (wc[0]) NR[o] = NaN;
     if (wc[1]) NR[o + 1] = NaN;
-  }
-}
-
-// scan_step_pair with the J+skip ring in REGISTERS (a shift register of RW >= J + skip factors
-// per asset, rg[c][0] the newest): no LDS round trips on the product chain, and no branches --
-// an absent month selects the old state back.  The product runs over the same factors in the
-// same order (oldest first) as the LDS ring; it starts from 1.0 and multiplies by 1.0 outside
-// the window (both exact), so the outputs are bit-identical to scan_step_pair's.
-template <int RW, bool NT = false>
-__device__ __forceinline__ void scan_step_pair_rr(ScanLane (&s)[2], const double (&x)[2], int m,
-                                                  double (&rg)[2][RW], int W, int J, int64_t N,
-                                                  int64_t a0, double* __restrict__ R,
-                                                  double* __restrict__ M, double* __restrict__ NR,
-                                                  double (&mom)[2]) {
-  const double NaN = qnan();
-  double ret[2], vp[2];
-  int wp[2];
-  bool wc[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const bool ab = is_absent(x[c]);
-    const bool xv = x[c] == x[c];
-    const double pnew = xv ? x[c] : s[c].pff;
-    const double r = pnew / s[c].pff - 1.0;
-    const double f = 1.0 + r;
-#pragma unroll
-    for (int k = RW - 1; k > 0; --k) rg[c][k] = ab ? rg[c][k] : rg[c][k - 1];
-    rg[c][0] = ab ? rg[c][0] : f;
-    s[c].pff = ab ? s[c].pff : pnew;
-    double acc = 1.0;
-#pragma unroll
-    for (int k = RW - 1; k >= 0; --k)   // wave-uniform window test
-      acc = (k < W && k >= W - J) ? acc * rg[c][k] : acc;
-    mom[c] = ab ? NaN : acc - 1.0;
-    ret[c] = ab ? NaN : r;
-    const bool ranked = mom[c] == mom[c];
-    const double ps_new = xv ? x[c] : s[c].psff;
-    wp[c] = (!ab && s[c].prev >= 0) ? s[c].prev : -1;
-    vp[c] = ps_new / s[c].psff - 1.0;
-    wc[c] = !ranked;
-    s[c].psff = ranked ? ps_new : s[c].psff;
-    s[c].prev = ranked ? m : (ab ? s[c].prev : -1);
-  }
-  const int64_t o = (int64_t)m * N + a0;
-  if (R) st_d2<NT>(R + o, ret[0], ret[1]);
-  st_d2<NT>(M + o, mom[0], mom[1]);
-  if (wp[0] >= 0 && wp[0] == wp[1]) {
-    st_d2<NT>(NR + (int64_t)wp[0] * N + a0, vp[0], vp[1]);
-  } else {
-    if (wp[0] >= 0) st_d1<NT>(NR + (int64_t)wp[0] * N + a0, vp[0]);
-    if (wp[1] >= 0) st_d1<NT>(NR + (int64_t)wp[1] * N + a0 + 1, vp[1]);
-  }
-  if (wc[0] && wc[1]) {
-    st_d2<NT>(NR + o, NaN, NaN);
-  } else {
-    if (wc[0]) st_d1<NT>(NR + o, NaN);
-    if (wc[1]) st_d1<NT>(NR + o + 1, NaN);
   }
 }
 
@@ -760,11 +641,9 @@ template <> struct RowT<2> { typedef double2 T; };
 __device__ __forceinline__ double comp(double v, int) { return v; }
 __device__ __forceinline__ double comp(double2 v, int k) { return k == 0 ? v.x : v.y; }
 
-// TILED: P is the asset-tiled panel [ceil(N/128)][T_d][128] (csm_tile_panel) and the wave's
-// 128 assets (VEC = 2) are one tile, so its whole history is one contiguous T_d KiB stream;
-// otherwise P is row-major [T_d][N] and consecutive day rows of a wave are N * 8 B apart.
-// BW > 1 (row-major only): BW waves cover 64 * VEC * BW adjacent assets and meet at a
-// barrier every NBUF months, so a workgroup's day-row reads stay BW KiB contiguous in time.
+// P is row-major [T_d][N]: consecutive day rows of a wave are N * 8 B apart.
+// BW > 1: BW waves cover 64 * VEC * BW adjacent assets and walk them independently (no
+// barrier), so a CU's loads of a day row are one BW-KiB span.
 // Speculative shards keep PM only for the first and last W + SHARD_PM_EDGE months (what the
 // summary walks and the repair read for a dense asset); other months are re-derived from the
 // daily panel for the rare asset that needs them (shard_pm_at).
@@ -777,17 +656,13 @@ __device__ __forceinline__ bool shard_pm_kept(int m, int T_m, int W) {
 // months of the shard, the pending ranked row (month index, -1 none), its subset-ffilled
 // price, and the first / last present month (-1 none) -- for k_shard_summary_state and
 // k_shard_repair.
-// RR > 0 (VEC 2, paired stores, no carry in / out): the scan ring lives in registers
-// (scan_step_pair_rr, J + skip <= RR), no LDS.  ST 3 is a profiling ablation: no scan, M = the
-// month price (wrong results).
-template <int MAXD, int VEC, int NBUF, bool TILED = false, int ST = 0, int BW = 1,
-          bool SH = false, bool PS = true, bool BSYNC = true, int RR = 0, bool BL = false>
+// BL (VEC 2): day rows by raw buffer loads (see load_month).
+template <int MAXD, int VEC, int NBUF, int BW, bool SH, bool BL>
 __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
     double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS) {
-  static_assert(!TILED || BW == 1, "tiled panels are read one tile per wave");
   typedef typename RowT<VEC>::T VT;
   extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC * BW]
   const int W = J + skip;
@@ -795,23 +670,12 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   const int64_t a0 = ((int64_t)blockIdx.x * 64 * BW + tid) * VEC;
   const bool live = a0 < N;
   const int RS = 64 * VEC * BW;
-  static_assert(RR == 0 || (VEC == 2 && !SH && !TILED), "register rings: paired lanes only");
   ScanLane sl[VEC];
-  double rg[2][RR > 0 ? RR : 1];
   // SH counters live in LDS after the ring ([3][RS] ints: present months, first, last present
   // month): the kernel already holds ~500 registers, and these are touched once per month
   int* shc = reinterpret_cast<int*>(ring_lds + W * RS);
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
-    if constexpr (RR > 0) {
-#pragma unroll
-      for (int q = 0; q < RR; ++q) rg[k][q] = qnan();
-      sl[k].pff = qnan();
-      sl[k].psff = qnan();
-      sl[k].head = 0;
-      sl[k].prev = -1;
-      continue;
-    }
     scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, carry, N, a0 + k, live);
     if (SH) {
       shc[VEC * tid + k] = 0;
@@ -819,15 +683,14 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
       shc[2 * RS + VEC * tid + k] = -1;
     }
   }
-  const double* base = TILED ? P + (int64_t)blockIdx.x * T_d * (64 * VEC) + VEC * tid
-                             : P + (live ? a0 : 0);
-  const int64_t rstride = TILED ? 64 * VEC : N;
+  const double* base = P + (live ? a0 : 0);
+  const int64_t rstride = N;
   // Loads are issued unconditionally (months past the end re-load the last month: cache
   // hits) so every wait is a counted vmcnt; only the processing is guarded.
   // BL: raw buffer loads over a per-month resource that ends at the month's last day row, so
   // the padding loads past it are out of range: counted by vmcnt like any load, but they return
   // 0 without a memory request (process masks them by the wave-uniform row count).
-  static_assert(!BL || (VEC == 2 && !TILED), "buffer loads: row-major paired lanes");
+  static_assert(!BL || VEC == 2, "buffer loads: paired lanes");
   const int voff = (int)((live ? a0 : 0) * 8);
   auto load_month = [&](VT (&buf)[MAXD], int mm) {
     mm = mm < T_m ? mm : T_m - 1;
@@ -877,38 +740,26 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
         else PMo[(int64_t)m * N + a0] = pm[0];
       }
       double mom[VEC];
-      if constexpr (ST == 3 || ST == 4) {   // ablations: no scan (3), no scan and no stores (4)
-#pragma unroll
-        for (int c = 0; c < VEC; ++c) mom[c] = pm[c];
-        if (ST == 3 || pm[0] == 1234.5678) {
-          if (VEC == 2) *reinterpret_cast<double2*>(M + (int64_t)m * N + a0) = make_double2(pm[0], pm[VEC - 1]);
-          else M[(int64_t)m * N + a0] = pm[0];
-        }
-      } else if constexpr (RR > 0) {
-        scan_step_pair_rr<RR>(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
-                              m, rg, W, J, N, a0, R, M, NR, reinterpret_cast<double (&)[2]>(mom));
-      } else if constexpr (VEC == 2 && (ST == 0 || ST == 1) && PS) {   // paired 16-B stores (R / M / NR are 16-B aligned)
-        scan_step_pair<ST == 1>(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
+      if constexpr (VEC == 2) {   // paired 16-B stores (R / M / NR are 16-B aligned)
+        scan_step_pair(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
                        m, ring_lds + VEC * tid, RS, W, J, N, a0, R, M, NR,
                        reinterpret_cast<double (&)[2]>(mom));
       } else {
 #pragma unroll
         for (int c = 0; c < VEC; ++c)
-          mom[c] = scan_step<ST>(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
+          mom[c] = scan_step(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
       }
-      if (IDS && ST != 4) {   // fixed-map bucket ids for the decile pass (csm_signal_ids)
+      if (IDS) {   // fixed-map bucket ids for the decile pass (csm_signal_ids)
         if (VEC == 2)
-        {
-          const uint32_t w = csm_fid(mom[0]) | (csm_fid(mom[VEC - 1]) << 16);
-          if (ST == 1) __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0));
-          else *reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0) = w;
-        }
+          *reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0) =
+              csm_fid(mom[0]) | (csm_fid(mom[VEC - 1]) << 16);
         else
           IDS[(int64_t)m * N + a0] = (uint16_t)csm_fid(mom[0]);
       }
     }
   };
-  VT A[MAXD], B[MAXD], C[MAXD];
+  static_assert(NBUF == 2 || NBUF == 4, "two or four month buffers");
+  VT A[MAXD], B[MAXD];
   if (NBUF == 2) {
     // month m+1 in flight while month m is reduced (half the registers: two waves per SIMD)
     load_month(A, 0);
@@ -918,28 +769,15 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
       load_month(A, m + 2);
       if (m + 1 < T_m) process(B, m + 1);
     }
-  } else if (NBUF == 3) {
-    // months m+1, m+2 in flight while month m is reduced
-    load_month(A, 0);
-    load_month(B, 1);
-    for (int m = 0; m < T_m; m += 3) {
-      load_month(C, m + 2);
-      process(A, m);
-      load_month(A, m + 3);
-      if (m + 1 < T_m) process(B, m + 1);
-      load_month(B, m + 4);
-      if (m + 2 < T_m) process(C, m + 2);
-    }
   } else {
     // months m+1..m+3 in flight (the whole-history-per-wave pattern needs ~3 months in
     // flight to approach the row-stream rate, see scripts/mb)
-    VT D[MAXD];
+    VT C[MAXD], D[MAXD];
     load_month(A, 0);
     load_month(B, 1);
     load_month(C, 2);
     for (int m = 0; m < T_m; m += 4) {
       load_month(D, m + 3);
-      if (BW > 1 && BSYNC) __syncthreads();
       process(A, m);
       load_month(A, m + 4);
       if (m + 1 < T_m) process(B, m + 1);
@@ -953,7 +791,7 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm,
-                  (SH || RR > 0) ? nullptr : carry_out);
+                  SH ? nullptr : carry_out);
       if (SH) {
         const int* q = shc + VEC * tid + k;
         carry_out[a0 + k] = (double)q[0];
@@ -966,269 +804,6 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   }
 }
 
-// =====================================================================================
-// Kernel AB'' (fused, day batches): k_signal for the common case -- 16-B row loads (even N),
-// no carry, every month but the first and the last at least D days long (host-checked; the
-// end of the data closes a short last month) -- streaming the day rows in
-// fixed batches of D instead of one register buffer per month.  k_signal pads every month to
-// MAXD loads (re-loads of the last day: cache hits, but they take issue slots and a share of
-// the 63 loads a wave can have outstanding); here every load is a new day row, NB - 1
-// batches in flight.  A batch holds at most one month end (months are >= D days): the rows
-// before it finish the current month, the rows after it start the next one, both reduced
-// branch-free with per-row uniform selects.  Same per-month arithmetic and stores as
-// k_signal (scan_step_pair): bit-identical outputs.
-// =====================================================================================
-template <int D, int NB>
-__global__ __launch_bounds__(64) void k_signal_db(
-    const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
-    int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
-    double* __restrict__ NR, int64_t T_d, uint16_t* __restrict__ IDS) {
-  static_assert(NB == 4, "four batch buffers (three in flight)");
-  extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][128]
-  const int W = J + skip;
-  const int tid = threadIdx.x;
-  const int64_t a0 = ((int64_t)blockIdx.x * 64 + tid) * 2;
-  const bool live = a0 < N;
-  constexpr int RS = 128;
-  ScanLane sl[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) scan_init(sl[c], ring_lds + 2 * tid + c, RS, W, nullptr, N, a0 + c, live);
-  const double* base = P + (live ? a0 : 0);
-  // the month being reduced: last valid price, any row present, any valid price
-  double last[2] = {0.0, 0.0};
-  bool pp[2] = {false, false}, vv[2] = {false, false};
-  int m = 0;
-  int64_t mend = T_m > 0 ? month_start[1] : 0;   // first day after month m
-  auto load_batch = [&](double2 (&buf)[D], int64_t d0) {
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      const int64_t d = d0 + k < T_d ? d0 + k : T_d - 1;
-      buf[k] = *reinterpret_cast<const double2*>(base + d * N);
-    }
-  };
-  auto finish = [&]() {   // month m is complete: month price, scan, stores
-    double pm[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) pm[c] = pp[c] ? (vv[c] ? last[c] : qnan()) : absent_val();
-    if (live) {
-      const int64_t o = (int64_t)m * N + a0;
-      if (PMo) *reinterpret_cast<double2*>(PMo + o) = make_double2(pm[0], pm[1]);
-      double mom[2];
-      scan_step_pair(sl, pm, m, ring_lds + 2 * tid, RS, W, J, N, a0, R, M, NR, mom);
-      if (IDS) *reinterpret_cast<uint32_t*>(IDS + o) = csm_fid(mom[0]) | (csm_fid(mom[1]) << 16);
-    }
-    ++m;
-    mend = m < T_m ? month_start[m + 1] : INT64_MAX;
-  };
-  auto consume = [&](const double2 (&X)[D], int64_t d0) {
-    // rows [0, kb) belong to month m, rows [kb, D) to month m + 1 (kb == D: no month end here)
-    const int kb = (int)(mend - d0 < D ? mend - d0 : D);
-    double lB[2] = {0.0, 0.0};
-    bool pB[2] = {false, false}, vB[2] = {false, false};
-    // kb is wave-uniform: a scalar branch per row picks the accumulator (no per-row lane masks)
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      if (k < kb) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const double x = c == 0 ? X[k].x : X[k].y;
-          const bool ok = x == x;
-          pp[c] |= !is_absent(x);
-          vv[c] |= ok;
-          last[c] = ok ? x : last[c];
-        }
-      } else if (d0 + k < T_d) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const double x = c == 0 ? X[k].x : X[k].y;
-          const bool ok = x == x;
-          pB[c] |= !is_absent(x);
-          vB[c] |= ok;
-          lB[c] = ok ? x : lB[c];
-        }
-      }
-    }
-    if (kb < D || d0 + D == mend) {   // month m ends in this batch (wave-uniform)
-      finish();
-#pragma unroll
-      for (int c = 0; c < 2; ++c) { last[c] = lB[c]; pp[c] = pB[c]; vv[c] = vB[c]; }
-    }
-  };
-  double2 A[D], B[D], C[D], E[D];
-  load_batch(A, 0);
-  load_batch(B, D);
-  load_batch(C, 2 * D);
-  for (int64_t d0 = 0; d0 < T_d; d0 += 4 * D) {
-    load_batch(E, d0 + 3 * D);
-    consume(A, d0);
-    load_batch(A, d0 + 4 * D);
-    if (d0 + D < T_d) consume(B, d0 + D);
-    load_batch(B, d0 + 5 * D);
-    if (d0 + 2 * D < T_d) consume(C, d0 + 2 * D);
-    load_batch(C, d0 + 6 * D);
-    if (d0 + 3 * D < T_d) consume(E, d0 + 3 * D);
-  }
-  if (m < T_m) finish();   // a short last month that began in the batch where its predecessor ended
-  if (live) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      scan_finish(sl[c], ring_lds + 2 * tid + c, RS, W, N, a0 + c, NR, nullptr, nullptr);
-  }
-}
-
-// =====================================================================================
-// Kernel AB' (fused, multi-wave): the same month-end + scan as k_signal, with the month
-// reductions spread over NW waves.  A workgroup owns 128 assets (two per lane for the 16-B
-// row loads).  Months go round-robin to the waves: in batch b, wave w reduces month
-// b*NW + w for all 128 assets and parks the month prices in LDS; after one barrier every
-// wave scans its 128/NW assets through the batch's NW months in order.  The next batch's
-// day rows (NB = 2: the next two batches') are in flight during the barrier and the scan,
-// so one workgroup keeps NW..2*NW months of loads outstanding and the sequential scan is
-// spread over NW SIMDs instead of one.  Results are bit-identical to k_signal.
-// =====================================================================================
-// Every workgroup must be resident at once (each lives for the whole kernel): 782 x NW waves
-// at C4 on 1024 SIMDs, so NW = 4 asks for <= 128 VGPRs (4 waves per SIMD).
-template <int MAXD, int NW, int NB>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 4 && NB == 1 ? 4 : 2)))
-void k_signal_mw(
-    const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
-    int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
-    double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out) {
-  constexpr int TA = 128;           // assets per workgroup
-  constexpr int SA = TA / NW;       // assets each wave scans
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* pmb = lds;                // [2][NW][TA] month prices, double-buffered by batch parity
-  double* ring = lds + 2 * NW * TA; // [W][TA] scan rings
-  const int W = J + skip;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * TA;
-  // reduction role: lane covers assets t0 + 2*lane, +1
-  const int64_t ar = t0 + 2 * lane;
-  const bool rlive = ar < N;        // N even: both assets live together
-  const double* base = P + (rlive ? ar : 0);
-  // scan role: lane < SA covers asset t0 + w*SA + lane
-  const int ci = w * SA + lane;
-  const int64_t as = t0 + ci;
-  const bool slive = lane < SA && as < N;
-  ScanLane sl;
-  if (lane < SA) scan_init(sl, ring + ci, TA, W, carry, N, as, slive);  // lanes >= SA own no column
-  const int nbatch = (T_m + NW - 1) / NW;
-  auto load_month = [&](double2 (&buf)[MAXD], int mm) {
-    mm = mm < T_m ? mm : T_m - 1;
-    const int64_t f0 = month_start[mm], nn = month_start[mm + 1] - f0;
-#pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-      buf[k] = *reinterpret_cast<const double2*>(base + (f0 + (k < nn ? k : nn - 1)) * N);
-  };
-  auto reduce_park = [&](const double2 (&X)[MAXD], int m, double* dst) {
-    double pm[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      double last = 0.0;
-      bool p = false, v = false;
-#pragma unroll
-      for (int k = 0; k < MAXD; ++k) {
-        const double x = c == 0 ? X[k].x : X[k].y;
-        const bool ok = x == x;
-        p |= !is_absent(x);
-        v |= ok;
-        last = ok ? x : last;
-      }
-      pm[c] = p ? (v ? last : qnan()) : absent_val();
-    }
-    *reinterpret_cast<double2*>(dst + 2 * lane) = make_double2(pm[0], pm[1]);
-    if (PMo && rlive && m < T_m)
-      *reinterpret_cast<double2*>(PMo + (int64_t)m * N + ar) = make_double2(pm[0], pm[1]);
-  };
-  auto scan_batch = [&](int b) {
-    const double* src = pmb + (b & 1) * NW * TA;
-    if (slive) {
-      for (int j = 0; j < NW; ++j) {
-        const int m = b * NW + j;
-        if (m >= T_m) break;
-        scan_step(sl, src[j * TA + ci], m, ring + ci, TA, W, J, N, as, R, M, NR);
-      }
-    }
-  };
-  double2 A[MAXD];
-  if (NB == 1) {
-    load_month(A, w);
-    for (int b = 0; b < nbatch; ++b) {
-      reduce_park(A, b * NW + w, pmb + (b & 1) * NW * TA + w * TA);
-      load_month(A, (b + 1) * NW + w);
-      __syncthreads();
-      scan_batch(b);
-    }
-  } else {
-    double2 B[MAXD];
-    load_month(A, w);
-    load_month(B, NW + w);
-    for (int b = 0; b < nbatch; b += 2) {
-      reduce_park(A, b * NW + w, pmb + w * TA);
-      load_month(A, (b + 2) * NW + w);
-      __syncthreads();
-      scan_batch(b);
-      if (b + 1 < nbatch) {
-        reduce_park(B, (b + 1) * NW + w, pmb + NW * TA + w * TA);
-        load_month(B, (b + 3) * NW + w);
-        __syncthreads();
-        scan_batch(b + 1);
-      }
-    }
-  }
-  if (slive) scan_finish(sl, ring + ci, TA, W, N, as, NR, next_pm, carry_out);
-}
-
-// =====================================================================================
-// Next present month price after a month boundary (the next_pm input of a segment of the
-// fused signal): for each asset, the month price (last valid, NaN if the month has rows but
-// no price) of the first month >= m0 in which it has a daily row; ABSENT if none.  Usually
-// month m0 itself, so one month of daily rows is read.
-// =====================================================================================
-// last_month (nullable): each asset's last month with a daily row (csm_last_present_month,
-// panel metadata computed once at ingestion) -- stops the search at a delisting instead of
-// walking every remaining month.
-__global__ __launch_bounds__(256) void k_next_present(const double* __restrict__ P,
-                                                      const int64_t* __restrict__ month_start,
-                                                      int T_m, int64_t N, int m0,
-                                                      const int32_t* __restrict__ last_month,
-                                                      double* __restrict__ out) {
-  const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (a >= N) return;
-  double res = absent_val();
-  const int mlast = last_month ? last_month[a] : T_m - 1;
-  for (int m = m0; m <= mlast; ++m) {
-    const int64_t d0 = month_start[m], d1 = month_start[m + 1];
-    bool pr = false, v = false;
-    double last = 0.0;
-    for (int64_t d = d0; d < d1; ++d) {
-      const double x = P[d * N + a];
-      pr |= !is_absent(x);
-      const bool ok = x == x;
-      v |= ok;
-      last = ok ? x : last;
-    }
-    if (pr) { res = v ? last : qnan(); break; }
-  }
-  out[a] = res;
-}
-
-// one thread per (asset, month): presence of the month -> atomicMax of the last present month
-__global__ __launch_bounds__(256) void k_last_present_month(const double* __restrict__ P,
-                                                            const int64_t* __restrict__ month_start,
-                                                            int64_t N, int32_t* __restrict__ last) {
-  const int m = blockIdx.y;
-  const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (a >= N) return;
-  const int64_t d0 = month_start[m], d1 = month_start[m + 1];
-  bool pr = false;
-  for (int64_t d = d0; d < d1 && !pr; ++d) pr = !is_absent(P[d * N + a]);
-  if (pr) atomicMax(last + a, m);
-}
-
-// =====================================================================================
-// Kernel C: per-date qcut labels + fused decile means (csrc/deciles.inc, wide-row variant).
 // =====================================================================================
 #define DEC_THREADS 512
 #define HB 8192
@@ -1648,63 +1223,24 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
 }
 
 // =====================================================================================
-// Panel re-blocking [T_d][N] -> [ceil(N/128)][T_d][128] (csm_tile_panel).  Both sides are
-// contiguous 1 KiB (tile, day) rows; assets past N in the last tile are ABSENT.
-// =====================================================================================
-#define CSM_TILE 128
-__global__ __launch_bounds__(256) void k_tile_panel(const double* __restrict__ P, int64_t T_d,
-                                                    int64_t N, double* __restrict__ Pt) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (tile, day)
-  const int lane = threadIdx.x & 63;
-  const int64_t tiles = (N + CSM_TILE - 1) / CSM_TILE;
-  if (row >= tiles * T_d) return;
-  const int64_t tile = row / T_d, d = row - tile * T_d;
-  const int64_t a = tile * CSM_TILE + 2 * lane;
-  double2 v;
-  if (a + 1 < N) {
-    v = *reinterpret_cast<const double2*>(P + d * N + a);
-  } else {
-    v.x = a < N ? P[d * N + a] : absent_val();
-    v.y = absent_val();
-  }
-  *reinterpret_cast<double2*>(Pt + row * CSM_TILE + 2 * lane) = v;
-}
-
-// =====================================================================================
 // C ABI
 // =====================================================================================
-// Process-wide tuning knobs (csm_tune): kernel variants for A/B measurement in one process.
-static int g_tune_signal_vec = 2;      // k_signal assets per lane: 1 or 2
-static int g_tune_signal_nbuf = 4;     // k_signal month buffers: 3 or 4
-static int g_tune_dec_ablate = 0;      // k_deciles pass ablation bitmask (profiling only: wrong results)
-static int g_tune_dec_merge = 1;       // PRE decile pass: merged sweep + general kernel for the rest (1), general only (0), merged only (2: test hook, rows it leaves are not written)
-static int g_tune_signal_mw = 0;       // 0: k_signal; NW*10+NB: k_signal_mw<.., NW, NB>
-static int g_tune_signal_store = 0;    // k_signal output stores: 0 plain, 1 nontemporal, 2 none (ablation)
-static int g_tune_signal_bw = 1;       // k_signal waves per workgroup (1, 2, 4), nbuf 4 only
-static int g_tune_signal_bl = 1;       // k_signal month rows by raw buffer loads (padding out of range): C4 1.695 -> 1.674 ms (profiles/r02/experiments/exp_signal_bl.log)
-static int g_tune_signal_rr = 0;       // k_signal scan ring in registers (J + skip <= 16): 1 on
-static int g_tune_signal_bwf = 0;      // k_signal waves per workgroup with NO barrier (adjacent columns, independent walks); 0 auto
-#define SIGNAL_BWF_MIN_N (180 * 512)
-static int g_tune_month_end_rows = 0;
-static int g_tune_signal_pair = 1;     // k_signal paired 16-B output stores (VEC 2): 1 on, 0 off
-static int g_tune_signal_db = 0;       // k_signal_db day-batch rows (16 | 20 | 21), 0 off
-static int g_tune_signal_maxd23 = 1;   // k_signal month buffers of 23 day rows when months fit: 1.789 -> 1.744 ms at C4 (profiles/r02)
+// Process-wide knobs (csm_tune).  Every one selects between PRODUCT paths that give identical
+// results (the fallbacks odd widths / unaligned buffers / narrow panels take), so tests can
+// drive each path on inputs that would not reach it by default.  The measured variants that
+// lost their A/B (profiles/r0*/experiments) are not in the library.
+static int g_tune_signal_vec = 2;      // k_signal assets per lane: 2 (paired 16-B rows) | 1 (odd N)
+static int g_tune_signal_bwf = 0;      // k_signal blocks: 0 auto | 1 one wave | 4 four barrier-free waves x 2 month buffers (buffer loads)
+#define SIGNAL_BWF_MIN_N (180 * 512)   // auto: 4-wave blocks once the grid still covers >= 180 CUs
 static int64_t* g_dec_timing = nullptr;
-// k_deciles bucket-id scratch path (N % 4 == 0): 1 on, 0 off.  Off by default: it moves
-// fewer bytes but measured slower at C4 (0.44 vs 0.40 ms, profiles/r01/experiments).
-static int g_tune_dec_ids = 0;
-// k_deciles register-resident bucket ids (deciles_reg.hip; V2 rows): 0 off (default), 1 when
-// every date row gets its own CU (T_m <= CUs), 2 always.  Off by default: it streams M once
-// instead of three times, but its ~250 VGPRs allow one 512-thread workgroup per CU (the plain
-// kernel fits two), so fewer loads are in flight per CU.  Measured C4 (461 dates): 0.57 vs
-// 0.33 ms; a 58-date shard: 0.235 vs 0.220 ms (profiles/r01/experiments/dec_reg_phases.log).
-static int g_tune_dec_reg = 0;
-static int g_tune_dec_nreg = 0;   // narrow rows <= 5120 assets: register-resident bucket ids (1 on)
-// csm_momentum_multi: 1 register shift ring when max(J) + skip <= 16, 0 the LDS ring
-static int g_tune_mj_reg = 2;   // 2: two assets per lane (C5 scan 37.7 -> 35.5 ms/step), 1: one
-// rows with at most this many assets take the narrow-row decile kernel (deciles_narrow.hip)
-static int64_t g_tune_dec_wave_max = 0;       // rows with at most this many assets: deciles_wave.hip
-static int64_t g_tune_dec_narrow_max = 16384;  // csm_tune_ptr("dec_timing"): [T_m][DEC_NPH] device buffer  // >0: csm_month_end uses k_month_end_rows (value = max month days)
+// PRE decile pass (csm_deciles_ids): 1 the merged sweep, then the general kernel for the rows it
+// leaves | 0 the general kernel only
+static int g_tune_dec_merge = 1;
+// csm_momentum_multi: 2 register shift ring, two assets per lane (even N, aligned) | 1 one asset
+// per lane | 0 the shared-memory ring (max(J) + skip > 16 always takes it)
+static int g_tune_mj_reg = 2;
+// rows with at most this many assets take the narrow-row decile kernels
+static int64_t g_tune_dec_narrow_max = 16384;
 
 extern "C" {
 
@@ -1714,32 +1250,14 @@ int csm_tune_portfolio(const char* key, int value);  // portfolio.hip
 
 int csm_tune(const char* key, int value) {
   if (!key) return CSM_E_INVAL;
-  if (!strcmp(key, "cohort_lds") || !strcmp(key, "cohort_seg") || !strcmp(key, "turn_list") ||
-      !strcmp(key, "sort_wave") || !strcmp(key, "turn_want") ||
-      !strcmp(key, "overlap_rows") || !strcmp(key, "seg_stage2") ||
-      !strcmp(key, "turn_gen_grid") || !strcmp(key, "turn_prep"))
+  if (!strcmp(key, "cohort_lds") || !strcmp(key, "cohort_seg") || !strcmp(key, "turn_want") ||
+      !strcmp(key, "overlap_rows") || !strcmp(key, "turn_gen_grid"))
     return csm_tune_portfolio(key, value);
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
-  if (!strcmp(key, "signal_nbuf") && (value == 2 || value == 3 || value == 4)) { g_tune_signal_nbuf = value; return CSM_OK; }
-  if (!strcmp(key, "dec_ablate") && value >= 0) { g_tune_dec_ablate = value; return CSM_OK; }
-  if (!strcmp(key, "dec_merge") && value >= 0 && value <= 2) { g_tune_dec_merge = value; return CSM_OK; }
-  if (!strcmp(key, "dec_ids") && (value == 0 || value == 1)) { g_tune_dec_ids = value; return CSM_OK; }
+  if (!strcmp(key, "signal_bwf") && (value == 0 || value == 1 || value == 4)) { g_tune_signal_bwf = value; return CSM_OK; }
+  if (!strcmp(key, "dec_merge") && (value == 0 || value == 1)) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
-  if (!strcmp(key, "dec_reg") && value >= 0 && value <= 2) { g_tune_dec_reg = value; return CSM_OK; }
-  if (!strcmp(key, "dec_nreg") && (value == 0 || value == 1)) { g_tune_dec_nreg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
-  if (!strcmp(key, "dec_wave_max") && value >= 0) { g_tune_dec_wave_max = value; return CSM_OK; }
-  if (!strcmp(key, "month_end_rows") && value >= 0 && value <= 32) { g_tune_month_end_rows = value; return CSM_OK; }
-  if (!strcmp(key, "signal_bw") && (value == 1 || value == 2 || value == 4)) { g_tune_signal_bw = value; return CSM_OK; }
-  if (!strcmp(key, "signal_bwf") && value >= 0 && value <= 4) { g_tune_signal_bwf = value; return CSM_OK; }
-  if (!strcmp(key, "signal_rr") && (value == 0 || value == 1)) { g_tune_signal_rr = value; return CSM_OK; }
-  if (!strcmp(key, "signal_bl") && (value == 0 || value == 1)) { g_tune_signal_bl = value; return CSM_OK; }
-  if (!strcmp(key, "signal_store") && value >= 0 && value <= 4) { g_tune_signal_store = value; return CSM_OK; }
-  if (!strcmp(key, "signal_pair") && (value == 0 || value == 1)) { g_tune_signal_pair = value; return CSM_OK; }
-  if (!strcmp(key, "signal_maxd23") && (value == 0 || value == 1)) { g_tune_signal_maxd23 = value; return CSM_OK; }
-  if (!strcmp(key, "signal_db") && (value == 0 || value == 16 || value == 20 || value == 21)) { g_tune_signal_db = value; return CSM_OK; }
-  if (!strcmp(key, "signal_mw") && (value == 0 || value == 21 || value == 22 || value == 41 ||
-                                    value == 42)) { g_tune_signal_mw = value; return CSM_OK; }
   return CSM_E_INVAL;
 }
 
@@ -1771,6 +1289,7 @@ int csm_create(int device, csm_ctx** out) {
 }
 
 int csm_destroy(csm_ctx* ctx) {
+  if (ctx) (void)csm_allgather_free(ctx);
   if (ctx && (ctx->scratch || ctx->dec_flg)) {
     (void)hipSetDevice(ctx->device);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
@@ -1806,15 +1325,6 @@ int csm_month_end(csm_ctx* ctx, const double* P, const double* V, int64_t T_d, i
     return set_err(ctx, CSM_E_INVAL, "csm_month_end: V and VOL must both be given or both NULL");
   if (T_m == 0) return CSM_OK;
   const bool v2 = (N % 2 == 0) && aligned16(P) && aligned16(PM) && (!V || aligned16(V));
-  if (v2 && !V && g_tune_month_end_rows > 0 && T_d > 0) {
-    // one-shot variant: every month must fit MAXD rows (host-checked bound)
-    const int maxd = g_tune_month_end_rows;
-    dim3 g2((unsigned)((N / 2 + 255) / 256), (unsigned)T_m);
-    if (maxd <= 24) hipLaunchKernelGGL((k_month_end_rows<24>), g2, dim3(256), 0, ctx->stream, P, month_start, N, PM);
-    else hipLaunchKernelGGL((k_month_end_rows<32>), g2, dim3(256), 0, ctx->stream, P, month_start, N, PM);
-    LAUNCH_CHECK(ctx, "k_month_end_rows");
-    return CSM_OK;
-  }
   const int vec = v2 ? 2 : 1;
   dim3 grid((unsigned)((N + 256LL * vec - 1) / (256LL * vec)), (unsigned)T_m);
   if (v2) {
@@ -1912,15 +1422,14 @@ int csm_momentum_multi_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t 
   return momentum_multi(ctx, PM, T_m, N, Js, nJ, skip, M, NR, IDS);
 }
 
-static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double* P, int64_t T_d,
+static int signal_launch(csm_ctx* ctx, const char* who, const double* P, int64_t T_d,
                          int64_t N, const int64_t* month_start, int32_t T_m,
                          int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
                          double* M, double* NR, const double* carry, const double* next_pm,
-                         double* carry_out, bool sh = false, uint16_t* ids = nullptr,
-                         int32_t min_month_days = 0) {
+                         double* carry_out, bool sh = false, uint16_t* ids = nullptr) {
   int r = prep(ctx);
   if (r) return r;
-  if (sh && (tiled || !PM || carry || next_pm || !carry_out || T_m < 1))
+  if (sh && (!PM || carry || next_pm || !carry_out || T_m < 1))
     return set_err(ctx, CSM_E_INVAL, "%s: a speculative shard pass needs PM and state, no carry / "
                    "next_pm, and at least one month", who);
   if (!P || !month_start || !M || !NR || N <= 0 || T_d < 0 || T_m < 0 || J < 1 || skip < 0 ||
@@ -1930,157 +1439,35 @@ static int signal_launch(csm_ctx* ctx, const char* who, bool tiled, const double
   if (max_month_days > 32)
     return set_err(ctx, CSM_E_INVAL, "%s: months longer than 32 days are not supported "
                    "(use csm_month_end + csm_momentum)", who);
-  if (tiled && (N % 2 != 0 || !aligned16(P) || !aligned16(M) || !aligned16(NR) ||
-                (PM && !aligned16(PM)) || (R && !aligned16(R))))
-    return set_err(ctx, CSM_E_INVAL, "%s: the tiled panel needs even N and 16-B aligned buffers", who);
   if (T_m == 0) return CSM_OK;
   const int W = J + skip;
   const bool can2 = (N % 2 == 0) && aligned16(P) && (!PM || aligned16(PM)) && aligned16(M) &&
                     aligned16(NR) && (!R || aligned16(R));
-  if (!tiled && can2 && g_tune_signal_mw != 0 && !sh && !ids) {
-    const int nw = g_tune_signal_mw / 10, nb = g_tune_signal_mw % 10;
-    const void* fm = nullptr;
-#define SMW(MD, NW_, NB_) (const void*)k_signal_mw<MD, NW_, NB_>
-    if (max_month_days <= 24)
-      fm = nw == 2 ? (nb == 1 ? SMW(24, 2, 1) : SMW(24, 2, 2)) : (nb == 1 ? SMW(24, 4, 1) : SMW(24, 4, 2));
-    else
-      fm = nw == 2 ? (nb == 1 ? SMW(32, 2, 1) : SMW(32, 2, 2)) : (nb == 1 ? SMW(32, 4, 1) : SMW(32, 4, 2));
-#undef SMW
-    const size_t ldsm = (size_t)(2 * nw + W) * 128 * sizeof(double);
-    if (ldsm > 65536)
-      HIP_CHECK(ctx, hipFuncSetAttribute(fm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsm));
-    int T_m_ = T_m, J_ = J, skip_ = skip;
-    int64_t N_ = N;
-    void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
-                    (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out};
-    HIP_CHECK(ctx, hipLaunchKernel(fm, dim3((unsigned)((N + 127) / 128)), dim3(64 * nw), args, ldsm,
-                                   ctx->stream));
-    LAUNCH_CHECK(ctx, who);
-    return CSM_OK;
-  }
-  const int vec = tiled ? 2 : ((g_tune_signal_vec == 1 || !can2) ? 1 : 2);
-  const int nbuf = (g_tune_signal_nbuf == 3) ? 3 : (g_tune_signal_nbuf == 2) ? 2 : 4;
-  const int db = g_tune_signal_db;
-  if (db > 0 && !tiled && !sh && vec == 2 && nbuf == 4 && !carry && !next_pm && !carry_out &&
-      g_tune_signal_bw == 1 && g_tune_signal_store == 0 && g_tune_signal_pair &&
-      min_month_days >= db) {   // day batches (every month >= db days)
-    const void* fd = db >= 21 ? (const void*)k_signal_db<21, 4>
-                   : db >= 20 ? (const void*)k_signal_db<20, 4> : (const void*)k_signal_db<16, 4>;
-    const size_t ldsd = (size_t)W * 128 * sizeof(double);
-    if (ldsd > 65536)
-      HIP_CHECK(ctx, hipFuncSetAttribute(fd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd));
-    int T_m_ = T_m, J_ = J, skip_ = skip;
-    int64_t N_ = N, T_d_ = T_d;
-    void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
-                    (void*)&M, (void*)&NR, &T_d_, (void*)&ids};
-    HIP_CHECK(ctx, hipLaunchKernel(fd, dim3((unsigned)((N / 2 + 63) / 64)), dim3(64), args, ldsd,
-                                   ctx->stream));
-    LAUNCH_CHECK(ctx, who);
-    return CSM_OK;
-  }
-  // Barrier-free multi-wave workgroups: the BWF waves of a block walk adjacent 1-KiB column
-  // slices of the same day rows independently, so a CU's loads of a day row are one 4-KiB span.
-  // Auto (signal_bwf 0): 4 waves x 2 month buffers once the grid still covers >= 180 CUs
-  // (C4 1.75-1.85 -> 1.63-1.78 ms interleaved on three boxes, profiles/r02/experiments).
-  int bwf = g_tune_signal_bwf;
-  int nbf = nbuf;
-  if (bwf == 0) {
-    const bool big = N >= (int64_t)SIGNAL_BWF_MIN_N && g_tune_signal_nbuf == 4;
-    bwf = big ? 4 : 1;
-    nbf = big ? 2 : nbuf;
-  }
-  // profiling ablation (signal_store 3, 4-wave blocks x 2 buffers): no scan, wrong results
-  const bool noscan = g_tune_signal_store >= 3 && !sh && !tiled && vec == 2 && max_month_days <= 23 &&
-                      g_tune_signal_pair && g_tune_signal_bw == 1;
-  const bool bwf_ok = !sh && !tiled && vec == 2 && max_month_days <= 23 && g_tune_signal_maxd23 &&
-                      g_tune_signal_pair && g_tune_signal_bw == 1 &&
-                      (g_tune_signal_store == 0 || (g_tune_signal_store == 1 && bwf == 4 && nbf == 2)) &&
-                      ((nbf == 4 && (bwf == 2 || bwf == 4)) ||
-                       (nbf == 3 && bwf >= 2 && bwf <= 4) ||
-                       (nbf == 2 && bwf >= 1 && bwf <= 4));
-  const bool rr = bwf_ok && g_tune_signal_rr && W <= 16 && !carry && !carry_out &&
-                  ((bwf == 4 && nbf >= 2) || (bwf == 1 && nbf == 2));
-  // raw buffer loads (padding rows out of range): rows of at most 2 GiB / 32
-  const bool bl = bwf_ok && g_tune_signal_bl && N * 8 * 32 < ((int64_t)1 << 31) &&
-                  bwf == 4 && (nbf == 2 || nbf == 3);
-  // speculative shards: the same 4-wave x 2-buffer blocks with buffer loads when they apply
-  const bool sh4 = sh && vec == 2 && max_month_days <= 23 && g_tune_signal_maxd23 && bwf == 4 &&
-                   nbf == 2 && g_tune_signal_bl && N * 8 * 32 < ((int64_t)1 << 31) &&
-                   g_tune_signal_store == 0 && g_tune_signal_pair && g_tune_signal_bw == 1;
-  const int bw = noscan ? 4 : sh4 ? 4 : bwf_ok ? bwf
-                     : (!sh && !tiled && vec == 2 && nbuf == 4 && max_month_days <= 24) ? g_tune_signal_bw : 1;
-  const size_t lds = rr ? 0 : (size_t)W * 64 * vec * bw * sizeof(double) +
+  const int vec = (g_tune_signal_vec == 1 || !can2) ? 1 : 2;
+  // Barrier-free 4-wave blocks (adjacent 1-KiB column slices walked independently, 2 month
+  // buffers, raw buffer loads with the padding rows out of range): the wide-panel default
+  // (C4 1.75-1.85 -> 1.63-1.78 ms, then buffer loads 1.695 -> 1.674, profiles/r02/experiments).
+  // Rows of at most 2 GiB / 32 (buffer offsets), months of at most 23 days.
+  const bool fits4 = vec == 2 && max_month_days <= 23 && N * 8 * 32 < ((int64_t)1 << 31);
+  const bool wide4 = fits4 && (g_tune_signal_bwf == 4 ||
+                               (g_tune_signal_bwf == 0 && N >= (int64_t)SIGNAL_BWF_MIN_N));
+  const int bw = wide4 ? 4 : 1;
+  const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double) +
                      (sh ? (size_t)3 * 64 * vec * bw * sizeof(int) : 0);
   const unsigned blocks = (unsigned)((N / vec + 64 * bw - 1) / (64 * bw));
   const void* fn = nullptr;
-#define SIG(MD, V, NB) (const void*)k_signal<MD, V, NB, false>
-#define SIGT(MD, NB) (const void*)k_signal<MD, 2, NB, true>
-  if (sh4)
-    fn = (const void*)k_signal<23, 2, 2, false, 0, 4, true, true, false, 0, true>;
-  else if (sh)
-    fn = max_month_days <= 24
-             ? (vec == 2 ? (const void*)k_signal<24, 2, 4, false, 0, 1, true>
-                         : (const void*)k_signal<24, 1, 4, false, 0, 1, true>)
-             : (vec == 2 ? (const void*)k_signal<32, 2, 4, false, 0, 1, true>
-                         : (const void*)k_signal<32, 1, 4, false, 0, 1, true>);
-  else if (tiled)
-    fn = max_month_days <= 24 ? (nbuf == 3 ? SIGT(24, 3) : SIGT(24, 4))
-                              : (nbuf == 3 ? SIGT(32, 3) : SIGT(32, 4));
-  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_bw == 2)
-    fn = (const void*)k_signal<24, 2, 4, false, 0, 2>;
-  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_bw == 4)
-    fn = (const void*)k_signal<24, 2, 4, false, 0, 4>;
-  else if (bwf_ok && g_tune_signal_store == 1)   // 4 waves x 2 buffers, nontemporal stores
-    fn = bl ? (const void*)k_signal<23, 2, 2, false, 1, 4, false, true, false, 0, true>
-            : (const void*)k_signal<23, 2, 2, false, 1, 4, false, true, false>;
-  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 1)
-    fn = (const void*)k_signal<24, 2, 4, false, 1>;
-  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_store == 2)
-    fn = (const void*)k_signal<24, 2, 4, false, 2>;
-  else if (bl && nbf == 2 && bwf == 4)
-    fn = rr ? (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false, 16, true>
-            : (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false, 0, true>;
-  else if (bl && nbf == 3 && bwf == 4)
-    fn = (const void*)k_signal<23, 2, 3, false, 0, 4, false, true, false, 0, true>;
-  else if (rr && nbf == 2 && bwf == 4)
-    fn = (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false, 16>;
-  else if (rr && nbf == 3 && bwf == 4)
-    fn = (const void*)k_signal<23, 2, 3, false, 0, 4, false, true, false, 16>;
-  else if (rr && nbf == 4 && bwf == 4)
-    fn = (const void*)k_signal<23, 2, 4, false, 0, 4, false, true, false, 16>;
-  else if (rr && nbf == 2 && bwf == 1)
-    fn = (const void*)k_signal<23, 2, 2, false, 0, 1, false, true, false, 16>;
-  else if (noscan)
-    fn = g_tune_signal_store == 4 ? (const void*)k_signal<23, 2, 2, false, 4, 4, false, true, false>
-                                  : (const void*)k_signal<23, 2, 2, false, 3, 4, false, true, false>;
-  else if (bwf_ok && nbf == 4 && bwf == 2)
-    fn = (const void*)k_signal<23, 2, 4, false, 0, 2, false, true, false>;
-  else if (bwf_ok && nbf == 4 && bwf == 4)
-    fn = (const void*)k_signal<23, 2, 4, false, 0, 4, false, true, false>;
-  else if (bwf_ok && nbf == 3 && bwf == 2)
-    fn = (const void*)k_signal<23, 2, 3, false, 0, 2, false, true, false>;
-  else if (bwf_ok && nbf == 2 && bwf == 1)
-    fn = (const void*)k_signal<23, 2, 2, false, 0, 1, false, true, false>;
-  else if (bwf_ok && nbf == 2 && bwf == 4)
-    fn = (const void*)k_signal<23, 2, 2, false, 0, 4, false, true, false>;
-  else if (bwf_ok && nbf == 2 && bwf == 2)
-    fn = (const void*)k_signal<23, 2, 2, false, 0, 2, false, true, false>;
-  else if (bwf_ok && nbf == 2 && bwf == 3)
-    fn = (const void*)k_signal<23, 2, 2, false, 0, 3, false, true, false>;
-  else if (bwf_ok && nbf == 3 && bwf == 3)
-    fn = (const void*)k_signal<23, 2, 3, false, 0, 3, false, true, false>;
-  else if (bwf_ok && nbf == 3 && bwf == 4)
-    fn = (const void*)k_signal<23, 2, 3, false, 0, 4, false, true, false>;
-  else if (vec == 2 && nbuf == 4 && max_month_days <= 23 && g_tune_signal_maxd23 && g_tune_signal_pair)
-    fn = (const void*)k_signal<23, 2, 4, false, 0, 1, false, true>;
-  else if (vec == 2 && nbuf == 4 && max_month_days <= 24 && g_tune_signal_pair == 0)
-    fn = (const void*)k_signal<24, 2, 4, false, 0, 1, false, false>;
-  else if (max_month_days <= 24)
-    fn = vec == 2 ? (nbuf == 3 ? SIG(24, 2, 3) : SIG(24, 2, 4)) : (nbuf == 3 ? SIG(24, 1, 3) : SIG(24, 1, 4));
+  // one-wave blocks, four month buffers: 23 / 24 / 32 day rows (the longest month)
+#define SIG1(V, SH_)                                                                            \
+  (max_month_days <= 23 && V == 2 ? (const void*)k_signal<23, V, 4, 1, SH_, false>              \
+   : max_month_days <= 24         ? (const void*)k_signal<24, V, 4, 1, SH_, false>              \
+                                  : (const void*)k_signal<32, V, 4, 1, SH_, false>)
+  if (wide4)
+    fn = sh ? (const void*)k_signal<23, 2, 2, 4, true, true> : (const void*)k_signal<23, 2, 2, 4, false, true>;
+  else if (vec == 2)
+    fn = sh ? SIG1(2, true) : SIG1(2, false);
   else
-    fn = vec == 2 ? (nbuf == 3 ? SIG(32, 2, 3) : SIG(32, 2, 4)) : (nbuf == 3 ? SIG(32, 1, 3) : SIG(32, 1, 4));
-#undef SIG
-#undef SIGT
+    fn = sh ? SIG1(1, true) : SIG1(1, false);
+#undef SIG1
   if (lds > 65536)
     HIP_CHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   {
@@ -2099,7 +1486,7 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
                int32_t T_m, int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
                double* M, double* NR, const double* carry, const double* next_pm,
                double* carry_out) {
-  return signal_launch(ctx, "csm_signal", false, P, T_d, N, month_start, T_m, max_month_days, J,
+  return signal_launch(ctx, "csm_signal", P, T_d, N, month_start, T_m, max_month_days, J,
                        skip, PM, R, M, NR, carry, next_pm, carry_out);
 }
 
@@ -2110,14 +1497,15 @@ int csm_signal_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
   if (!ids || (N % 4) != 0 || ((uintptr_t)ids & 7u) != 0)
     return set_err(ctx, CSM_E_INVAL, "csm_signal_ids: ids must be non-NULL and 8-B aligned, N %% 4 == 0 "
                    "(N=%lld)", (long long)N);
-  return signal_launch(ctx, "csm_signal_ids", false, P, T_d, N, month_start, T_m, max_month_days, J,
-                       skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids, min_month_days);
+  (void)min_month_days;   // kept in the ABI (host hint for fixed day batches; no kernel uses it)
+  return signal_launch(ctx, "csm_signal_ids", P, T_d, N, month_start, T_m, max_month_days, J,
+                       skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids);
 }
 
 int csm_signal_shard(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                      const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
                      int32_t skip, double* PM, double* R, double* M, double* NR, double* state) {
-  return signal_launch(ctx, "csm_signal_shard", false, P, T_d, N, month_start, T_m,
+  return signal_launch(ctx, "csm_signal_shard", P, T_d, N, month_start, T_m,
                        max_month_days, J, skip, PM, R, M, NR, nullptr, nullptr, state, true);
 }
 
@@ -2127,64 +1515,8 @@ int csm_signal_shard_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                          double* state, uint16_t* ids) {
   if (!ids || (N % 4) != 0 || ((uintptr_t)ids & 7u) != 0)
     return set_err(ctx, CSM_E_INVAL, "csm_signal_shard_ids: needs ids, N %% 4 == 0, 8-B aligned ids");
-  return signal_launch(ctx, "csm_signal_shard_ids", false, P, T_d, N, month_start, T_m,
+  return signal_launch(ctx, "csm_signal_shard_ids", P, T_d, N, month_start, T_m,
                        max_month_days, J, skip, PM, R, M, NR, nullptr, nullptr, state, true, ids);
-}
-
-int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
-                     const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
-                     int32_t skip, double* PM, double* R, double* M, double* NR,
-                     const double* carry, const double* next_pm, double* carry_out) {
-  return signal_launch(ctx, "csm_signal_tiled", true, Pt, T_d, N, month_start, T_m,
-                       max_month_days, J, skip, PM, R, M, NR, carry, next_pm, carry_out);
-}
-
-int csm_last_present_month(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
-                           const int64_t* month_start, int32_t T_m, int32_t* last_month) {
-  int r = prep(ctx);
-  if (r) return r;
-  if (!P || !month_start || !last_month || N <= 0 || T_d < 0 || T_m < 0 || T_m > 65535)
-    return set_err(ctx, CSM_E_INVAL, "csm_last_present_month: bad arguments");
-  HIP_CHECK(ctx, hipMemsetAsync(last_month, 0xFF, (size_t)N * sizeof(int32_t), ctx->stream));  // -1
-  if (T_m == 0) return CSM_OK;
-  hipLaunchKernelGGL(k_last_present_month, dim3((unsigned)((N + 255) / 256), (unsigned)T_m),
-                     dim3(256), 0, ctx->stream, P, month_start, N, last_month);
-  LAUNCH_CHECK(ctx, "k_last_present_month");
-  return CSM_OK;
-}
-
-int csm_next_present(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
-                     const int64_t* month_start, int32_t T_m, int32_t m0,
-                     const int32_t* last_month, double* next_pm) {
-  int r = prep(ctx);
-  if (r) return r;
-  if (!P || !month_start || !next_pm || N <= 0 || T_d < 0 || T_m < 0 || m0 < 0 || m0 > T_m)
-    return set_err(ctx, CSM_E_INVAL, "csm_next_present: bad arguments (N=%lld T_m=%d m0=%d)",
-                   (long long)N, T_m, m0);
-  hipLaunchKernelGGL(k_next_present, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream,
-                     P, month_start, T_m, N, m0, last_month, next_pm);
-  LAUNCH_CHECK(ctx, "k_next_present");
-  return CSM_OK;
-}
-
-int64_t csm_tiled_size(int64_t T_d, int64_t N) {
-  if (T_d < 0 || N <= 0) return 0;
-  return ((N + CSM_TILE - 1) / CSM_TILE) * T_d * CSM_TILE;
-}
-
-int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double* Pt) {
-  int r = prep(ctx);
-  if (r) return r;
-  if (!P || !Pt || N <= 0 || T_d < 0 || (N % 2) != 0 || !aligned16(P) || !aligned16(Pt))
-    return set_err(ctx, CSM_E_INVAL, "csm_tile_panel: bad arguments (N=%lld T_d=%lld; N even, "
-                   "16-B aligned buffers)", (long long)N, (long long)T_d);
-  if (T_d == 0) return CSM_OK;
-  const int64_t tiles = (N + CSM_TILE - 1) / CSM_TILE;
-  const int64_t rows = tiles * T_d;  // one 64-lane wave moves one 1 KiB (tile, day) row
-  const unsigned blocks = (unsigned)((rows + 3) / 4);
-  hipLaunchKernelGGL(k_tile_panel, dim3(blocks), dim3(256), 0, ctx->stream, P, T_d, N, Pt);
-  LAUNCH_CHECK(ctx, "k_tile_panel");
-  return CSM_OK;
 }
 
 }  // extern "C"
@@ -2192,39 +1524,24 @@ int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double
 template <int NB>
 static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                           int32_t* CNT, int32_t* NV, uint16_t* ids, int n_cu, bool pre = false,
+                           int32_t* CNT, int32_t* NV, uint16_t* ids, bool pre = false,
                            int32_t* flg = nullptr) {
-  const int ab = g_tune_dec_ablate;
   int64_t* tm = g_dec_timing;
   if (pre) {   // ids written by csm_signal_ids / csm_momentum_multi_ids (fixed map): M is read only for a few cells
-    if (N <= g_tune_dec_narrow_max)   // sweep rows: 1024 buckets (the fixed map's ids >> 3)
-      launch_deciles_pre_narrow<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids,
-                                    g_tune_dec_merge ? flg : nullptr, g_tune_dec_merge == 2);
+    if (N <= g_tune_dec_narrow_max)   // sweep rows: 2048 buckets (the fixed map's ids >> 2)
+      launch_deciles_pre_narrow<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm, ids,
+                                    g_tune_dec_merge ? flg : nullptr);
     else
-      launch_deciles_pre<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids,
-                             g_tune_dec_merge ? flg : nullptr, g_tune_dec_merge == 2);
+      launch_deciles_pre<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm, ids,
+                             g_tune_dec_merge ? flg : nullptr);
     return;
   }
-  if (N <= g_tune_dec_wave_max && !ids) {     // the narrowest rows: one wave per row
-    launch_deciles_wave<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
+  if (N <= g_tune_dec_narrow_max) {   // rows of a few thousand assets (C2/C3/C5)
+    launch_deciles_narrow<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm);
     return;
   }
-  if (N <= g_tune_dec_narrow_max && !ids && v2 && g_tune_dec_nreg && N <= deciles_narrow_reg_max_n()) {
-    launch_deciles_narrow_reg<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
-    return;
-  }
-  if (N <= g_tune_dec_narrow_max && !ids) {   // rows of a few thousand assets (C2/C3/C5)
-    launch_deciles_narrow<NB>(v2, T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
-    return;
-  }
-  const bool reg_rows = g_tune_dec_reg == 2 || (g_tune_dec_reg == 1 && T_m <= n_cu);
-  if (!ids && v2 && reg_rows && N <= deciles_reg_max_n()) {   // ids in registers: one HBM read of M per row
-    launch_deciles_reg<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm);
-    return;
-  }
-  if (ids) hipLaunchKernelGGL((k_deciles<NB, true, true>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
-  else if (v2) hipLaunchKernelGGL((k_deciles<NB, true, false>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
-  else hipLaunchKernelGGL((k_deciles<NB, false, false>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ab, tm, ids);
+  if (v2) hipLaunchKernelGGL((k_deciles<NB, true>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm, ids);
+  else hipLaunchKernelGGL((k_deciles<NB, false>), dim3(T_m), dim3(dec_wide::kThreads), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm, ids);
 }
 
 extern "C" {
@@ -2244,27 +1561,16 @@ int csm_deciles(csm_ctx* ctx, const double* M, const double* NR, int32_t T_m, in
   for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
   const bool v2 = (N % 2 == 0) && aligned16(M) && (!NR || aligned16(NR)) && (((uintptr_t)L & 1u) == 0);
   uint16_t* ids = nullptr;
-  if (g_tune_dec_ids && N % 4 == 0 && v2 && (((uintptr_t)L & 3u) == 0)) {
-    const size_t need = (size_t)T_m * (size_t)N * sizeof(uint16_t);
-    if (ctx->scratch_bytes < need) {
-      if (ctx->scratch) HIP_CHECK(ctx, hipFree(ctx->scratch));
-      ctx->scratch = nullptr;
-      ctx->scratch_bytes = 0;
-      HIP_CHECK(ctx, hipMalloc(&ctx->scratch, need));
-      ctx->scratch_bytes = need;
-    }
-    ids = (uint16_t*)ctx->scratch;
-  }
   if (!NR) {
-    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, ctx->n_cu);
+    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids);
   } else {
     switch (n_bins) {
-      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
-      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
-      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
-      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
-      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
-      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu); break;
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids); break;
       default:
         return set_err(ctx, CSM_E_INVAL, "csm_deciles: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", n_bins);
     }
@@ -2301,15 +1607,15 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
     flg = ctx->dec_flg;
   }
   if (!NR) {
-    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, ctx->n_cu, pre, flg);
+    launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, pre, flg);
   } else {
     switch (n_bins) {
-      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
-      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
-      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
-      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
-      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
-      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, ctx->n_cu, pre, flg); break;
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
       default:
         return set_err(ctx, CSM_E_INVAL, "%s: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", who, n_bins);
     }
@@ -2371,8 +1677,9 @@ int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const in
     }
     ids = (uint16_t*)ctx->scratch;
   }
-  r = signal_launch(ctx, "csm_pipeline", false, P, T_d, N, month_start, T_m, max_month_days, J,
-                    skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids, min_month_days);
+  (void)min_month_days;
+  r = signal_launch(ctx, "csm_pipeline", P, T_d, N, month_start, T_m, max_month_days, J,
+                    skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids);
   if (r) return r;
   QTab q;
   for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;

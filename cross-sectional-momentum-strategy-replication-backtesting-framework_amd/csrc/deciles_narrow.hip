@@ -9,7 +9,6 @@
 #define HB 1024
 #define CAP 1024     // candidates of the target buckets (refinement splits beyond)
 #define DEC_MINB 6   // 6 workgroups per CU (8: register spills, slower)
-#define DEC_MINB_RI 4   // register-id rows: 4 (6 spills)
 namespace dec_narrow {
 #include "deciles.inc"
 }  // namespace dec_narrow
@@ -17,36 +16,20 @@ namespace dec_narrow {
 template <int NB>
 void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                           int32_t* CNT, int32_t* NV, int ablate, int64_t* tim) {
+                           int32_t* CNT, int32_t* NV, int64_t* tim) {
   uint16_t* ids = nullptr;
   if (v2)
     hipLaunchKernelGGL((dec_narrow::k_deciles<NB, true, false>), dim3(T_m), dim3(DEC_THREADS), 0,
-                       st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim, ids);
+                       st, M, NR, N, nbins, q, L, EW, CNT, NV, tim, ids);
   else
     hipLaunchKernelGGL((dec_narrow::k_deciles<NB, false, false>), dim3(T_m), dim3(DEC_THREADS), 0,
-                       st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim, ids);
+                       st, M, NR, N, nbins, q, L, EW, CNT, NV, tim, ids);
 }
-
-// rows of <= DEC_NREG_RI * 1024 assets (C5's 5k-asset bootstrap rows) with register-resident
-// bucket ids (RI mode): M is streamed once per row instead of up to three times; bit-identical
-// to the plain narrow kernel (lanes own the same cells)
-template <int NB>
-void launch_deciles_narrow_reg(int T_m, hipStream_t st, const double* M, const double* NR,
-                               int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim) {
-  hipLaunchKernelGGL((dec_narrow::k_deciles<NB, true, false, DEC_NREG_RI>), dim3(T_m),
-                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
-                     (uint16_t*)nullptr);
-}
-int deciles_narrow_reg_max_n() { return DEC_NREG_RI * 4 * DEC_THREADS; }
 
 #define INST(NB)                                                                              \
-  template void launch_deciles_narrow_reg<NB>(int, hipStream_t, const double*, const double*,  \
-                                              int64_t, int, const QTab&, int8_t*, double*,       \
-                                              int32_t*, int32_t*, int, int64_t*);                \
   template void launch_deciles_narrow<NB>(bool, int, hipStream_t, const double*, const double*,  \
                                           int64_t, int, const QTab&, int8_t*, double*,           \
-                                          int32_t*, int32_t*, int, int64_t*);
+                                          int32_t*, int32_t*, int64_t*);
 INST(0)
 INST(2)
 INST(3)

@@ -20,23 +20,22 @@ namespace dec_npre {
 template <int NB>
 void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                               int32_t* CNT, int32_t* NV, int ablate, int64_t* tim,
-                               uint16_t* ids, int32_t* flg, bool merged_only) {
+                               int32_t* CNT, int32_t* NV, int64_t* tim,
+                               uint16_t* ids, int32_t* flg) {
   if (flg)
-    hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, 0, true, true>), dim3(T_m),
-                       dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
+    hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, true>), dim3(T_m),
+                       dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
                        ids, flg);
-  if (flg && merged_only) return;
-  hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, 0, true, false>), dim3(T_m),
-                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
+  hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, false>), dim3(T_m),
+                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
                      ids, flg);
 }
 
 #define INST(NB)                                                                              \
   template void launch_deciles_pre_narrow<NB>(int, hipStream_t, const double*, const double*,  \
                                               int64_t, int, const QTab&, int8_t*, double*,       \
-                                              int32_t*, int32_t*, int, int64_t*, uint16_t*,       \
-                                              int32_t*, bool);
+                                              int32_t*, int32_t*, int64_t*, uint16_t*,       \
+                                              int32_t*);
 INST(0)
 INST(2)
 INST(3)

@@ -15,23 +15,21 @@ namespace dec_pre {
 template <int NB>
 void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
-                        int32_t* NV, int ablate, int64_t* tim, uint16_t* ids, int32_t* flg,
-                        bool merged_only) {
+                        int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg) {
   if (flg)   // merged pass: one sweep of ids + next_ret per row (deciles.inc, MG)
-    hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, 0, true, true>), dim3(T_m),
-                       dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
+    hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, true>), dim3(T_m),
+                       dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
                        ids, flg);
-  if (flg && merged_only) return;   // test hook (csm_tune "dec_merge" 2)
   // the general kernel: every row (flg NULL) or only the rows the merged pass left
-  hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, 0, true, false>), dim3(T_m),
-                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, ablate, tim,
+  hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, false>), dim3(T_m),
+                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
                      ids, flg);
 }
 
 #define INST(NB)                                                                              \
   template void launch_deciles_pre<NB>(int, hipStream_t, const double*, const double*, int64_t, \
                                        int, const QTab&, int8_t*, double*, int32_t*, int32_t*,  \
-                                       int, int64_t*, uint16_t*, int32_t*, bool);
+                                       int64_t*, uint16_t*, int32_t*);
 INST(0)
 INST(2)
 INST(3)

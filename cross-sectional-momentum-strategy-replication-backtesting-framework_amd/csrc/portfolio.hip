@@ -1090,11 +1090,7 @@ __global__ __launch_bounds__(PF_THREADS, BM ? TO_MINB_BM : 1) void k_turnover(
     turnover_body<VW, IMP, false>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH, Ct,
                                   half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp, gen_list,
                                   gen_count, TPv, TPm);
-  } else if (!gen_list) {   // full grid: the steady rows' workgroups exit after the prologue
-    turnover_body<VW, IMP, true, BM>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf,
-                                     CH, Ct, half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp,
-                                     gen_list, gen_count);
-  } else {
+  } else {   // the general rows the steady launch put on the work list
     const int n = *(volatile int32_t*)gen_count;   // written by the previous launch
     for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
       turnover_body<VW, IMP, true, BM>(gen_list[i], L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH,
@@ -1312,17 +1308,8 @@ __global__ __launch_bounds__(256) void k_bootstrap_panel(const double* __restric
 static int g_tune_cohort_lds = 1;
 // 1: label-sorted segment gathers (k_label_sort + k_cohort_seg) where N <= SEG_MAXN
 static int g_tune_cohort_seg = 1;
-// turnover's general rows: 0 full second grid, 1 work list (C5 112.0 -> 108.9, C3 1.438 ->
-// 1.405 ms/step same box), 2 work list above 8192 workgroups
-static int g_tune_turn_list = 1;
-// legs-only equal-weight label sort: 1 one wave per row (k_label_sort_legs_ew), 0 a workgroup per row
-static int g_tune_sort_wave = 1;
-// 1: k_cohort_seg stages its return row with 16-B loads, a whole row in flight; 0: 8-B loop
-static int g_tune_seg_stage2 = 1;
 // workgroups of the persistent general-row turnover launch (walking the work list)
 static int64_t g_tune_turn_gen_grid = 8192;   // C5 portfolio: 512 49.1, 2048 40.1, 8192 39.5 ms
-// 1: k_turn_prep computes the steady equal-weight rows' factors once per row; 0: in-workgroup
-static int g_tune_turn_prep = 1;
 // 1: k_overlap_rows (one thread per (t, b, decile) serving every K of the set) for single-chunk
 // cohort plans, 0: k_overlap always
 static int g_tune_overlap_rows = 1;
@@ -1395,9 +1382,9 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                            pl.C, PERM, OFF, WSRT, FWp);
         hipLaunchKernelGGL((k_cohort_seg<NB, true, true>), g2, dim3(PF_THREADS), lds, st, NR,
                            (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
-                           N, K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
+                           N, K, pl.C, Cs, xcd, 1, SWRp, SWp);
       } else {
-        if ((N & 3) == 0 && g_tune_sort_wave)   // one wave per row (C5's equal-weight legs)
+        if ((N & 3) == 0)   // one wave per row (C5's equal-weight legs)
           hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
                              dim3(PF_THREADS), 0, st, L, N, pl.C, (int64_t)T_m * B, PERM, OFF, FWp);
         else
@@ -1405,20 +1392,20 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                              pl.C, PERM, OFF, WSRT, FWp);
         hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR,
                            (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
-                           N, K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
+                           N, K, pl.C, Cs, xcd, 1, SWRp, SWp);
       }
     } else if (W) {
       hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
       hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR,
                          (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
+                         K, pl.C, Cs, xcd, 1, SWRp, SWp);
     } else {
       hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
       hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR,
                          (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, Cs, xcd, g_tune_seg_stage2, SWRp, SWp);
+                         K, pl.C, Cs, xcd, 1, SWRp, SWp);
     }
     return;
   }
@@ -1494,28 +1481,12 @@ int csm_tune_portfolio(const char* key, int value) {
     g_tune_turn_want = value;
     return CSM_OK;
   }
-  if (key && !strcmp(key, "sort_wave") && (value == 0 || value == 1)) {
-    g_tune_sort_wave = value;
-    return CSM_OK;
-  }
-  if (key && !strcmp(key, "turn_prep") && (value == 0 || value == 1)) {
-    g_tune_turn_prep = value;
-    return CSM_OK;
-  }
   if (key && !strcmp(key, "turn_gen_grid") && value >= 1) {
     g_tune_turn_gen_grid = value;
     return CSM_OK;
   }
-  if (key && !strcmp(key, "seg_stage2") && (value == 0 || value == 1)) {
-    g_tune_seg_stage2 = value;
-    return CSM_OK;
-  }
   if (key && !strcmp(key, "overlap_rows") && (value == 0 || value == 1)) {
     g_tune_overlap_rows = value;
-    return CSM_OK;
-  }
-  if (key && !strcmp(key, "turn_list") && value >= 0 && value <= 2) {
-    g_tune_turn_list = value;
     return CSM_OK;
   }
   return CSM_E_INVAL;
@@ -1598,16 +1569,14 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
     if (costs) {
       const bool imp = ADV && aum > 0.0;
       const int64_t nblk = lay.p.Ct * lay.rows;
-      // general rows: a work list for big grids (turn_list 1, or 2 = auto above 8192
-      // workgroups), else a second full grid whose steady workgroups exit early
-      const bool use_list = g_tune_turn_list == 1 || (g_tune_turn_list == 2 && nblk > 8192);
-      int32_t* gen_count = use_list ? (int32_t*)((char*)workspace + lay.gen_b) : nullptr;
-      int32_t* gen_list = use_list ? gen_count + 1 : nullptr;
-      if (use_list) HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
-      const unsigned gen_grid = use_list ? (unsigned)std::min<int64_t>(nblk, g_tune_turn_gen_grid)
-                                         : (unsigned)nblk;
+      // general rows: the steady launch appends them to a work list that a persistent launch
+      // walks (C5 112.0 -> 108.9, C3 1.438 -> 1.405 ms/step against a second full grid)
+      int32_t* gen_count = (int32_t*)((char*)workspace + lay.gen_b);
+      int32_t* gen_list = gen_count + 1;
+      HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
+      const unsigned gen_grid = (unsigned)std::min<int64_t>(nblk, g_tune_turn_gen_grid);
       // steady equal-weight rows take their factors from k_turn_prep (no per-workgroup prologue)
-      const bool prep = g_tune_turn_prep && !W && !imp && (N & 3) == 0;
+      const bool prep = !W && !imp && (N & 3) == 0;
       double* TPv = prep ? (double*)((char*)workspace + lay.tp_b) : nullptr;
       uint32_t* TPm = prep ? (uint32_t*)((char*)workspace + lay.tpm_b) : nullptr;
       if (prep)

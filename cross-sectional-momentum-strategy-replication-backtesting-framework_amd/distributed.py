@@ -48,6 +48,42 @@ def all_gather_stack(x: torch.Tensor, group=None) -> torch.Tensor:
     return out.to(x.device)
 
 
+class CsmCollective:
+    """The date-shard all-gathers through libcsmom.so's own RCCL communicator (csm_comm_unique_id
+    / csm_allgather_init / csm_allgather, include/csmom.h) -- the collectives a non-Python host
+    makes.  The 128-byte unique id travels over an existing process group (any backend); the
+    gathers run on the engine's current HIP stream.  Drop-in for all_gather_stack in
+    DateShardPipeline(collective=...)."""
+
+    def __init__(self, engine, group=None):
+        import ctypes
+        self.eng = engine
+        self.G = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        uid = (ctypes.c_ubyte * 128)()
+        if self.rank == 0:
+            st = engine.lib.csm_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p))
+            if st != 0:
+                raise RuntimeError(f"csm_comm_unique_id failed ({st})")
+        if self.G > 1:
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group else 0,
+                                       group=group)
+            uid = (ctypes.c_ubyte * 128).from_buffer_copy(box[0])
+        engine._call("csm_allgather_init", ctypes.cast(uid, ctypes.c_void_p), self.rank, self.G)
+
+    def all_gather_stack(self, x: torch.Tensor) -> torch.Tensor:
+        import ctypes
+        x = x.contiguous()
+        out = torch.empty((self.G,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        self.eng._call("csm_allgather", ctypes.c_void_p(x.data_ptr()),
+                       ctypes.c_void_p(out.data_ptr()), x.numel() * x.element_size())
+        return out
+
+    def close(self):
+        self.eng._call("csm_allgather_free")
+
+
 @dataclass
 class ShardResult:
     M: torch.Tensor      # [T_m_local][N] mom_J of this rank's months
@@ -76,8 +112,11 @@ class DateShardPipeline:
     """
 
     def __init__(self, stages, months_per_rank, J=12, skip=1, n_bins=10, group=None,
-                 fused=False):
+                 fused=False, collective=None):
         self.st = stages
+        # collective: None = torch.distributed (all_gather_stack), or a CsmCollective
+        self.gather = (collective.all_gather_stack if collective is not None
+                       else (lambda x: all_gather_stack(x, group)))
         self.months = list(months_per_rank)
         self.J, self.skip, self.n_bins = J, skip, n_bins
         self.group = group
@@ -110,7 +149,7 @@ class DateShardPipeline:
             PM, _, M, NR, state = st.signal_shard(P_local, month_start_local, max_month_days,
                                                   J, s, **({} if ids is None else {"ids": ids}))
             summary = st.shard_summary(PM, J, s, state=state)
-            summaries = all_gather_stack(summary, self.group)          # collective 1
+            summaries = self.gather(summary)                           # collective 1
             carry, next_pm = st.fold_carry(summaries, self.rank, J, s)
             st.shard_repair(PM, carry, next_pm, state, M, NR, J, s,
                             **({} if ids is None else {"ids": ids}))
@@ -119,7 +158,7 @@ class DateShardPipeline:
         self._check_months(PM.shape[0])
         summary = st.shard_summary(PM, J, s)
         if self.G > 1:
-            summaries = all_gather_stack(summary, self.group)          # collective 1
+            summaries = self.gather(summary)                           # collective 1
             carry, next_pm = st.fold_carry(summaries, self.rank, J, s)
         else:
             carry, next_pm = None, None
@@ -140,7 +179,7 @@ class DateShardPipeline:
             pad_cnt[:T_m] = CNT
             # one collective for both: counts ride as exact float64
             packed = torch.cat([pad_ew, pad_cnt.to(EW.dtype)], dim=1)
-            allp = all_gather_stack(packed, self.group)                 # collective 2
+            allp = self.gather(packed)                                  # collective 2
             ews = [allp[g, :self.months[g], :nb] for g in range(self.G)]
             cns = [allp[g, :self.months[g], nb:] for g in range(self.G)]
             EW = torch.cat(ews, 0).contiguous()

@@ -336,119 +336,6 @@ class Engine:
                    _ptr(R), _ptr(M), _ptr(NR), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV), _ptr(LS))
         return PipelineOut(PM=PM, M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS, R=R, NV=NV)
 
-    def tile_panel(self, P, out=None):
-        """Re-block a row-major [T_d][N] panel into the asset-tiled layout
-        [ceil(N/128)][T_d][128] (csm_tile_panel); returns the flat tiled tensor."""
-        T_d, N = P.shape
-        _need(P, "P", torch.float64, (T_d, N), self.device)
-        n = int(self.lib.csm_tiled_size(T_d, N))
-        Pt = self.empty((n,)) if out is None else out
-        _need(Pt, "Pt", torch.float64, (n,), self.device)
-        self._call("csm_tile_panel", _ptr(P), T_d, N, _ptr(Pt))
-        return Pt
-
-    def signal_tiled(self, Pt, T_d, N, month_start, max_month_days, J=12, skip=1,
-                     with_pm=False, with_ret=False, carry=None, next_pm=None, carry_out=None,
-                     out=None):
-        """csm_signal_tiled: the fused month-end + scan over the tiled panel."""
-        T_m = month_start.numel() - 1
-        _need(Pt, "Pt", torch.float64, (int(self.lib.csm_tiled_size(T_d, N)),), self.device)
-        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
-        W = J + skip
-        for t, nm, shp in ((carry, "carry", (W + 2, N)), (next_pm, "next_pm", (N,)),
-                           (carry_out, "carry_out", (W + 2, N))):
-            if t is not None:
-                _need(t, nm, torch.float64, shp, self.device)
-        if out is None:
-            PM = self.empty((T_m, N)) if with_pm else None
-            R = self.empty((T_m, N)) if with_ret else None
-            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
-        else:
-            PM, R, M, NR = out
-        self._call("csm_signal_tiled", _ptr(Pt), T_d, N, _ptr(month_start), T_m,
-                   int(max_month_days), int(J), int(skip), _ptr(PM), _ptr(R), _ptr(M), _ptr(NR),
-                   _ptr(carry), _ptr(next_pm), _ptr(carry_out))
-        return PM, R, M, NR
-
-    def last_present_month(self, P, month_start):
-        """csm_last_present_month: panel metadata ([N] int32, -1 = never present)."""
-        T_d, N = P.shape
-        T_m = month_start.numel() - 1
-        out = self.empty((N,), torch.int32)
-        self._call("csm_last_present_month", _ptr(P), T_d, N, _ptr(month_start), T_m, _ptr(out))
-        return out
-
-    def next_present(self, P, month_start, m0, last_month=None, out=None):
-        """csm_next_present: month price of each asset's first present month >= m0."""
-        T_d, N = P.shape
-        T_m = month_start.numel() - 1
-        out = self.empty((N,)) if out is None else out
-        self._call("csm_next_present", _ptr(P), T_d, N, _ptr(month_start), T_m, int(m0),
-                   _ptr(last_month), _ptr(out))
-        return out
-
-    def segmented_plan(self, P, month_start_host, J=12, skip=1, segments=4, month_start=None):
-        """Buffers for run_segmented: month ranges, per-segment device offsets, carries, and
-        the panel's last-present-month metadata (one pass over P, done here, at plan time)."""
-        ms = np.asarray(month_start_host, dtype=np.int64)
-        T_m = len(ms) - 1
-        N = P.shape[1]
-        S = max(1, min(int(segments), T_m))
-        base, rem = divmod(T_m, S)
-        bounds, m0 = [], 0
-        for g in range(S):
-            m1 = m0 + base + (1 if g < rem else 0)
-            bounds.append((m0, m1))
-            m0 = m1
-        seg_ms = [torch.from_numpy(ms[a:b + 1] - ms[a]).to(self.device) for a, b in bounds]
-        W = J + skip
-        carries = [self.empty((W + 2, N)), self.empty((W + 2, N))]
-        npms = [self.empty((N,)) for _ in bounds]
-        if getattr(self, "_aux_stream", None) is None:
-            self._aux_stream = torch.cuda.Stream(self.device)
-        msd = (torch.from_numpy(ms).to(self.device) if month_start is None else month_start)
-        last = self.last_present_month(P, msd) if S > 1 else None
-        return dict(bounds=bounds, seg_ms=seg_ms, carries=carries, npms=npms, ms_host=ms,
-                    aux=self._aux_stream, max_days=int(np.diff(ms).max()) if T_m else 1,
-                    last_month=last)
-
-    def run_segmented(self, P, month_start, plan, J=12, skip=1, n_bins=10, out=None):
-        """The fused pass split into month segments: segment g's signal (csm_signal with the
-        carry of segment g-1 and the next_pm of its boundary) runs on the current stream while
-        the per-date ranking of segment g-1 runs on a side stream.  Bit-identical to
-        signal + deciles + long_short over the whole panel."""
-        T_d, N = P.shape
-        T_m = month_start.numel() - 1
-        if out is None:
-            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
-            L = self.empty((T_m, N), torch.int8)
-            EW, CNT = self.empty((T_m, n_bins)), self.empty((T_m, n_bins), torch.int32)
-            LS = self.empty((T_m,))
-        else:
-            M, NR, L, EW, CNT, LS = out
-        main = torch.cuda.current_stream(self.device)
-        aux = plan["aux"]
-        ms = plan["ms_host"]
-        bounds = plan["bounds"]
-        aux.wait_stream(main)
-        for g, (m0, m1) in enumerate(bounds):
-            d0, d1 = int(ms[m0]), int(ms[m1])
-            npm = (self.next_present(P, month_start, m1, plan["last_month"], out=plan["npms"][g])
-                   if m1 < T_m else None)
-            cin = plan["carries"][g % 2] if g > 0 else None
-            cout = plan["carries"][(g + 1) % 2] if g + 1 < len(bounds) else None
-            self.signal(P[d0:d1], plan["seg_ms"][g], plan["max_days"], J, skip, carry=cin,
-                        next_pm=npm, carry_out=cout, out=(None, None, M[m0:m1], NR[m0:m1]))
-            ev = torch.cuda.Event()
-            ev.record(main)
-            aux.wait_event(ev)
-            with torch.cuda.stream(aux):
-                self.deciles(M[m0:m1], NR[m0:m1], n_bins,
-                             out=(L[m0:m1], EW[m0:m1], CNT[m0:m1], None))
-        main.wait_stream(aux)
-        self.long_short(EW, CNT, LS)
-        return M, NR, L, EW, CNT, LS
-
     def deciles(self, M, NR=None, n_bins=10, out=None, with_nv=False):
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)

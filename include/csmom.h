@@ -27,46 +27,32 @@
 extern "C" {
 #endif
 
-#define CSM_ABI_VERSION 2
+#define CSM_ABI_VERSION 3
 #define CSM_ABSENT_BITS 0x7FF4000000000001ULL
 
 #define CSM_OK 0
 #define CSM_E_INVAL (-1)   /* bad argument (null pointer, size, unsupported parameter) */
 #define CSM_E_HIP (-2)     /* HIP runtime / launch failure */
+#define CSM_E_RCCL (-3)    /* RCCL missing or a collective failed */
+#define CSM_UNIQUE_ID_BYTES 128
 
 typedef struct csm_ctx csm_ctx;
 
 int csm_abi_version(void);
 
-/* Process-wide tuning knobs for A/B measurement: "signal_vec" (1|2 assets per lane in the
- * fused kernel), "signal_nbuf" (2|3|4 month buffers; 2 only with "signal_bwf"), "dec_ablate" (profiling-only bitmask
- * that SKIPS decile passes and so produces wrong results), "dec_ids" (0|1 bucket-id scratch
- * path), "dec_merge" (1: csm_deciles_ids' merged label sweep, the
- * general kernel for the rows it leaves | 0: the general kernel only | 2: test hook, the merged
- * kernel only -- rows it leaves are not written), "dec_reg" (0 off | 1 when T_m <= CUs | 2 always: register-resident bucket ids,
- * bit-identical), "dec_narrow_max" (widest row for the narrow-row decile kernel),
- * "mj_reg" (csm_momentum_multi: 2 register shift ring with two assets per lane (16-B rows;
- * even N, aligned buffers), 1 register shift ring when max(J) + skip <= 16, the default;
- * 0 the shared-memory ring), "month_end_rows" (0 off | max month days: one-shot month-end
- * kernel), "signal_bw" (1|2|4 waves per fused-kernel workgroup), "signal_bwf" (0 auto:
- * 4 waves x 2 month buffers when N >= 92160, else 1 | 1..4 waves per fused-kernel workgroup with
- * no barrier, walking adjacent 1-KiB column slices independently; with signal_nbuf 2 | 3 | 4), "signal_store" (0 plain |
- * 1 nontemporal | 2 none | 3 no scan | 4 no scan, no stores: profiling ablations, wrong results), "signal_rr" (0 | 1:
- * fused-kernel scan ring in registers when J + skip <= 16, no carry; bit-identical), "signal_bl" (0 | 1, the default: fused-kernel day
- * rows by raw buffer loads, padding rows out of range; bit-identical), "signal_mw" (0 | 21 | 22 | 41 | 42 multi-wave
- * fused kernel), "cohort_lds" / "cohort_seg" (portfolio cohort-sum kernel choice),
- * "turn_list" (turnover's general rows: 0 a full second grid, 1 a work list, the default,
- * 2 the work list above 8192 workgroups), "sort_wave" (legs-only equal-weight label sort: 1 one
- * wave per formation row, the default | 0 a workgroup per row), "turn_want" (turnover
- * workgroups wanted per launch, default 4096: rows split into chunks to reach it; set before
- * sizing the portfolio workspace), "overlap_rows" (cohort -> PR combine: 1 one thread per
- * (month, panel, decile) serving every K of the set when the cohort plan has one chunk, the
- * default | 0 one per (K, month, panel, decile)), "seg_stage2" (segment cohort sums: 1 the
- * return row staged with 16-B loads, the default | 0 an 8-B loop), "turn_gen_grid" (workgroups
- * of the persistent general-row turnover launch, default 8192), "turn_prep" (steady equal-weight
- * turnover rows: 1 factors from a once-per-row k_turn_prep, the default | 0 each workgroup's
- * own prologue).  Returns
- * CSM_E_INVAL for an unknown key or value. */
+/* Process-wide knobs that select between PRODUCT paths with identical results (so tests can
+ * drive the fallbacks on inputs that would not reach them): "signal_vec" (2 paired 16-B rows |
+ * 1 one asset per lane, the odd-N path), "signal_bwf" (0 auto | 1 one-wave blocks | 4 the wide
+ * panels' four barrier-free waves with buffer loads), "dec_merge" (1 the merged decile sweep on
+ * ids, the general kernel for the rows it leaves | 0 the general kernel only), "mj_reg"
+ * (csm_momentum_multi: 2 register ring, two assets per lane | 1 one asset | 0 the LDS ring),
+ * "dec_narrow_max" (widest row for the narrow-row decile kernels), "cohort_seg" / "cohort_lds"
+ * (portfolio cohort-sum kernel: label-sorted segments (rows <= 7168) | per-wave LDS sums |
+ * register sums), "turn_want" (turnover workgroups per launch, default 4096; set before sizing
+ * the portfolio workspace), "turn_gen_grid" (workgroups of the general-row turnover launch,
+ * default 8192), "overlap_rows" (1 one thread per (month, panel, decile) for single-chunk
+ * plans | 0 one per (K, month, panel, decile)).  Returns CSM_E_INVAL for an unknown key or
+ * value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
  * wall-clock ticks (100 MHz) at its phase boundaries (NULL switches it off). */
@@ -158,48 +144,13 @@ int csm_signal(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int6
 /*
  * csm_signal (no carry) that also writes ids[T_m][N] (uint16, 8-B aligned, N % 4 == 0): each
  * mom_J's bucket under the fixed monotone map of csm_deciles_ids (0xFFFF = NaN), so the decile
- * pass reads 2 B per cell instead of 8.  min_month_days (HOST value: the shortest month in
- * days, the first and the last month excepted; 0 = unknown) lets the kernel stream fixed day
- * batches when every interior month is long enough.
+ * pass reads 2 B per cell instead of 8.  min_month_days (HOST value: the shortest interior
+ * month in days; 0 = unknown) is accepted for ABI stability and not used by this build.
  */
 int csm_signal_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                    const int64_t* month_start, int32_t T_m, int32_t max_month_days,
                    int32_t min_month_days, int32_t J, int32_t skip, double* PM, double* R,
                    double* M, double* NR, uint16_t* ids);
-
-/*
- * next_pm[N] for a month boundary m0: the month price of each asset's first present month
- * >= m0 (ABSENT if none).  With csm_signal's carry_out / carry this splits the fused pass into
- * month segments that chain bit for bit (so per-date ranking of early segments can overlap
- * the signal of later ones).
- */
-int csm_next_present(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
-                     const int64_t* month_start, int32_t T_m, int32_t m0,
-                     const int32_t* last_month, double* next_pm);
-/* Panel metadata for csm_next_present (nullable there): each asset's last month with a
- * daily row, -1 if none (one pass over the panel, computed once when it is loaded). */
-int csm_last_present_month(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
-                           const int64_t* month_start, int32_t T_m, int32_t* last_month);
-
-/*
- * Asset-tiled daily panel (the engine's preferred HBM layout for the signal pass):
- * Pt[ceil(N/128)][T_d][128] float64, assets past N ABSENT.  A 128-asset tile's whole history
- * is one contiguous stream, so the per-asset time walk of csm_signal_tiled reads sequential
- * KiB rows instead of rows N * 8 B apart.  csm_tiled_size returns the element count of Pt.
- * csm_tile_panel re-blocks a row-major [T_d][N] panel (even N, 16-B aligned) into Pt; the
- * host pivot (panel.py) can also write Pt directly.
- */
-int64_t csm_tiled_size(int64_t T_d, int64_t N);
-int csm_tile_panel(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, double* Pt);
-
-/*
- * csm_signal over the tiled panel Pt (same outputs, row-major [T_m][N]; same carry
- * contract).  N even; 16-B aligned buffers.
- */
-int csm_signal_tiled(csm_ctx* ctx, const double* Pt, int64_t T_d, int64_t N,
-                     const int64_t* month_start, int32_t T_m, int32_t max_month_days, int32_t J,
-                     int32_t skip, double* PM, double* R, double* M, double* NR,
-                     const double* carry, const double* next_pm, double* carry_out);
 
 /*
  * Per-date qcut labels, fused with the equal-weight decile means.  Replaces
@@ -412,6 +363,22 @@ int csm_turnover_features(csm_ctx* ctx, const double* PM, const double* VOL, con
 int csm_double_sort_labels(csm_ctx* ctx, const double* M, const double* X, const int8_t* Lm,
                            const int8_t* Lv, int32_t T_m, int64_t N, int32_t n_vol, double* Xm,
                            int8_t* Lc);
+
+/*
+ * The date-shard collectives over RCCL (xGMI on one node), for hosts that shard
+ * run_demo.py:31-67 without torch.distributed: csm_comm_unique_id fills CSM_UNIQUE_ID_BYTES
+ * (host memory) on ONE rank; the bytes reach the other ranks out of band; every rank calls
+ * csm_allgather_init with them (one communicator per context, on the context's device); then
+ * csm_allgather gathers `bytes` from every rank into recv (device, nranks * bytes, rank order)
+ * on the context's stream -- collective 1 (the [S][N] shard summaries for csm_fold_carry) and
+ * collective 2 (the per-date decile means / counts for csm_long_short).  csm_allgather_free
+ * (also done by csm_destroy) releases the communicator.  RCCL is loaded at first use;
+ * CSM_E_RCCL when it is missing or a call fails.
+ */
+int csm_comm_unique_id(void* unique_id);
+int csm_allgather_init(csm_ctx* ctx, const void* unique_id, int32_t rank, int32_t nranks);
+int csm_allgather(csm_ctx* ctx, const void* send, void* recv, int64_t bytes);
+int csm_allgather_free(csm_ctx* ctx);
 
 #ifdef __cplusplus
 }

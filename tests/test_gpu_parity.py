@@ -219,8 +219,8 @@ def test_fused_signal_large_panel_vs_oracle(engine):
 
 
 def test_fused_odd_n_and_variants(engine):
-    """Odd N runs the fused kernel with one asset per lane; every (assets-per-lane, buffer
-    depth) variant gives the same bits."""
+    """Odd N runs the fused kernel with one asset per lane; both assets-per-lane paths give the
+    same bits on an even panel."""
     z = load_golden("edge")
     P = z["P"][:, :-1]
     ms_h = z["month_start"].astype(np.int64)
@@ -235,91 +235,43 @@ def test_fused_odd_n_and_variants(engine):
     lib = engine.lib
     try:
         for vec in (1, 2):
-            for nbuf in (3, 4):
-                assert lib.csm_tune(b"signal_vec", vec) == 0 and lib.csm_tune(b"signal_nbuf", nbuf) == 0
-                got = engine.signal(P2, ms2, maxd, 12, 1, with_pm=True)
-                for a, b in zip(got, base):
-                    if a is not None:
-                        assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (vec, nbuf)
+            assert lib.csm_tune(b"signal_vec", vec) == 0
+            got = engine.signal(P2, ms2, maxd, 12, 1, with_pm=True)
+            for a, b in zip(got, base):
+                if a is not None:
+                    assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), vec
     finally:
         lib.csm_tune(b"signal_vec", 2)
-        lib.csm_tune(b"signal_nbuf", 4)
     assert lib.csm_tune(b"nope", 1) != 0
 
 
 @pytest.mark.parametrize("name", ["edge", "c1"])
-def test_signal_kernel_variants_bit_identical(engine, name):
-    """Every k_signal variant -- asset-tiled panel, multi-wave month reductions (k_signal_mw),
-    multi-wave workgroups, nontemporal stores -- and the one-shot month-end kernel produce the
-    same bits as the default fused kernel."""
+def test_signal_block_shapes_bit_identical(engine, name):
+    """The fused kernel's two block shapes -- one wave per block with four month buffers, and
+    the wide panels' four barrier-free waves with two buffers and raw buffer loads (padding rows
+    out of range; partial last block) -- give the same bits, for J = 12 / skip 1 and J = 3 /
+    skip 0, and equal the unfused month-end."""
     z = load_golden(name)
     P = z["P"]
     if P.shape[1] % 2:
         P = P[:, :-1]
     ms_h = z["month_start"].astype(np.int64)
     maxd = int(np.diff(ms_h).max())
-    T_d, N = P.shape
     Pd, ms = _up(P), _up(ms_h)
     lib = engine.lib
-    base = engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True)
-
-    def check(got, tag):
-        for a, b in zip(got, base):
-            if a is not None:
-                assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), tag
-    Pt = engine.tile_panel(Pd)
-    check(engine.signal_tiled(Pt, T_d, N, ms, maxd, 12, 1, with_pm=True, with_ret=True), "tiled")
-    # the tiled panel itself: tile t, day d, slot k holds asset 128 t + k (ABSENT past N)
-    pt = Pt.cpu().numpy().reshape(-1, T_d, 128)
-    for t in range(pt.shape[0]):
-        w = min(128, N - 128 * t)
-        assert bits_equal(pt[t, :, :w], P[:, 128 * t:128 * t + w])
-        assert O.is_absent(pt[t, :, w:]).all()
     try:
-        for knob, vals in ((b"signal_mw", (21, 22, 41, 42)), (b"signal_bw", (2, 4)),
-                           (b"signal_store", (1,))):
-            for v in vals:
-                assert lib.csm_tune(knob, v) == 0
-                check(engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True),
-                      f"{knob}={v}")
-                lib.csm_tune(knob, 0 if knob != b"signal_bw" else 1)
-        # barrier-free multi-wave blocks (adjacent column slices, partial last block)
-        for bwf, nbuf in ((4, 2), (3, 2), (2, 2), (1, 2), (4, 3), (2, 3), (4, 4), (2, 4)):
-            assert lib.csm_tune(b"signal_nbuf", nbuf) == 0
-            assert lib.csm_tune(b"signal_bwf", bwf) == 0
-            check(engine.signal(Pd, ms, maxd, 12, 1, with_pm=True, with_ret=True),
-                  f"signal_bwf={bwf} nbuf={nbuf}")
-        # raw buffer loads (padding rows out of range), register scan rings, nontemporal
-        # stores, alone and combined, on the barrier-free blocks
-        for bl, rr, st, bwf, nbuf in ((1, 0, 0, 4, 2), (1, 0, 0, 4, 3), (0, 1, 0, 4, 2),
-                                      (0, 1, 0, 4, 3), (0, 1, 0, 4, 4), (0, 1, 0, 1, 2),
-                                      (1, 1, 0, 4, 2), (0, 0, 1, 4, 2), (1, 0, 1, 4, 2)):
-            for knob, v in ((b"signal_bl", bl), (b"signal_rr", rr), (b"signal_store", st),
-                            (b"signal_nbuf", nbuf), (b"signal_bwf", bwf)):
-                assert lib.csm_tune(knob, v) == 0
-            for J, skip in ((12, 1), (3, 0)):
-                got = engine.signal(Pd, ms, maxd, J, skip, with_pm=True, with_ret=True)
-                ref = base if (J, skip) == (12, 1) else None
-                if ref is None:
-                    for knob, v in ((b"signal_bl", 0), (b"signal_rr", 0), (b"signal_store", 0)):
-                        lib.csm_tune(knob, v)   # the clamped-load LDS-ring kernel
-                    ref = engine.signal(Pd, ms, maxd, J, skip, with_pm=True, with_ret=True)
-                for a, b in zip(got, ref):
-                    if a is not None:
-                        assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), \
-                            f"bl={bl} rr={rr} store={st} bwf={bwf} nbuf={nbuf} J={J} skip={skip}"
-        for knob, v in ((b"signal_bl", 1), (b"signal_rr", 0), (b"signal_store", 0)):
-            lib.csm_tune(knob, v)
-        lib.csm_tune(b"signal_bwf", 0)
-        lib.csm_tune(b"signal_nbuf", 4)
-        assert lib.csm_tune(b"month_end_rows", maxd) == 0
-        PM, _ = engine.month_end(Pd, ms)
-        assert bits_equal(PM.cpu().numpy(), base[0].cpu().numpy())
+        for J, skip in ((12, 1), (3, 0)):
+            assert lib.csm_tune(b"signal_bwf", 1) == 0
+            base = engine.signal(Pd, ms, maxd, J, skip, with_pm=True, with_ret=True)
+            assert lib.csm_tune(b"signal_bwf", 4) == 0
+            got = engine.signal(Pd, ms, maxd, J, skip, with_pm=True, with_ret=True)
+            for a, b in zip(got, base):
+                if a is not None:
+                    assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (J, skip)
     finally:
-        for knob, v in ((b"signal_mw", 0), (b"signal_bw", 1), (b"signal_store", 0),
-                        (b"month_end_rows", 0), (b"signal_bwf", 0), (b"signal_nbuf", 4),
-                        (b"signal_bl", 1), (b"signal_rr", 0)):
-            lib.csm_tune(knob, v)
+        lib.csm_tune(b"signal_bwf", 0)
+    PM, _ = engine.month_end(Pd, ms)
+    assert bits_equal(PM.cpu().numpy(), base[0].cpu().numpy())
 
 
 def test_fused_rejects_long_months(engine):
@@ -328,43 +280,6 @@ def test_fused_rejects_long_months(engine):
     ms2 = torch.tensor([0, 40], dtype=torch.int64, device="cuda:0")
     with pytest.raises(csmom.CsmError):
         engine.signal(P2, ms2, 40)       # month longer than 32 days
-
-
-@pytest.mark.parametrize("name", ["edge", "c1"])
-def test_deciles_bucket_id_path_equals_direct(engine, name):
-    """The bucket-id scratch path (N % 4 == 0) and the direct path give the same labels and
-    counts, and decile means equal to rounding."""
-    z = load_golden(name)
-    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
-    _, M, NR = engine.momentum(PM, 12, 1)
-    lib = engine.lib
-    a = engine.deciles(M, NR, 10, with_nv=True)
-    try:
-        assert lib.csm_tune(b"dec_ids", 1) == 0
-        b = engine.deciles(M, NR, 10, with_nv=True)
-    finally:
-        lib.csm_tune(b"dec_ids", 0)
-    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
-    ea, eb = a[1].cpu().numpy(), b[1].cpu().numpy()
-    assert np.array_equal(np.isnan(ea), np.isnan(eb)) and max_rel(ea, eb) <= 1e-13
-
-
-@pytest.mark.parametrize("segments", [1, 2, 3, 7])
-def test_segmented_overlapped_pass_bit_identical(engine, segments):
-    """run_segmented (signal segments chained by carry + next_pm, ranking of segment g-1 on
-    a side stream) equals the one-shot fused pass bit for bit."""
-    z = load_golden("edge")
-    ms_h = z["month_start"].astype(np.int64)
-    P, ms = _up(z["P"]), _up(ms_h)
-    maxd = int(np.diff(ms_h).max())
-    ref = engine.run(P, ms, 12, 1, 10, max_month_days=maxd, fused=True)
-    plan = engine.segmented_plan(P, ms_h, 12, 1, segments)
-    M, NR, L, EW, CNT, LS = engine.run_segmented(P, ms, plan, 12, 1, 10)
-    torch.cuda.synchronize()
-    for a, b in ((M, ref.M), (NR, ref.NR), (EW, ref.EW), (LS, ref.LS)):
-        assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
-    assert torch.equal(L, ref.L) and torch.equal(CNT, ref.CNT)
-    assert np.array_equal(L.cpu().numpy(), z["J12s1_L"])
 
 
 @pytest.mark.parametrize("name", ["edge", "c1", "small", "real_data"])
@@ -386,49 +301,6 @@ def test_narrow_and_wide_decile_kernels_agree(engine, name):
     assert np.array_equal(np.isnan(ea), np.isnan(eb)) and max_rel(ea, eb) <= 1e-13
 
 
-@pytest.mark.parametrize("n", [100_000, 94_208, 40_002, 117_760])
-@pytest.mark.parametrize("case", [c for c in STRESS if c != "odd_n"])
-def test_register_id_decile_kernel_stress(engine, case, n):
-    """The register-resident bucket-id kernel (dec_reg=2; deciles_reg.hip: the first 94208
-    cells of an even row keep their ids in registers, the rest up to 117760 are re-read):
-    labels equal the oracle's qcut on the stress pathologies, with and without a tail."""
-    x = _stress_row(case, n)
-    lib = engine.lib
-    try:
-        assert lib.csm_tune(b"dec_reg", 2) == 0
-        L, _, _, _ = engine.deciles(_up(x[None, :]), None, 10)
-    finally:
-        lib.csm_tune(b"dec_reg", 0)
-    assert np.array_equal(L.cpu().numpy()[0], _oracle_labels(x))
-
-
-@pytest.mark.parametrize("n", [100_000, 65_536, 20_002, 117_760])
-@pytest.mark.parametrize("n_bins", [10, 3, 20])
-def test_register_id_kernel_equals_plain_wide_kernel(engine, n, n_bins):
-    """The register-id kernel and the plain wide kernel (three row sweeps) give bit-identical
-    labels, counts and decile means (lanes own the same cells and add them in the same order),
-    on multi-date panels with NaN cells."""
-    rng = np.random.default_rng(n + n_bins)
-    T = 5
-    M = rng.standard_normal((T, n)) * 0.3
-    M[rng.random((T, n)) < 0.03] = np.nan
-    M[1, : n // 3] = np.round(M[1, : n // 3], 2)        # ties
-    NR = rng.standard_normal((T, n)) * 0.05
-    NR[rng.random((T, n)) < 0.02] = np.nan
-    Md, NRd = _up(M), _up(NR)
-    lib = engine.lib
-    b = engine.deciles(Md, NRd, n_bins, with_nv=True)
-    try:
-        assert lib.csm_tune(b"dec_reg", 2) == 0
-        a = engine.deciles(Md, NRd, n_bins, with_nv=True)
-    finally:
-        lib.csm_tune(b"dec_reg", 0)
-    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
-    assert bits_equal(a[1].cpu().numpy(), b[1].cpu().numpy())
-    ref = np.stack([_oracle_labels(M[t], n_bins) for t in range(T)])
-    assert np.array_equal(a[0].cpu().numpy(), ref)
-
-
 @pytest.mark.parametrize("name", ["edge", "c1", "longwin"])
 @pytest.mark.parametrize("Js,skip", [((3, 6, 9, 12), 1), ((12,), 1), ((1, 2), 0),
                                      ((24, 48, 12, 5, 7), 2), ((16,), 0), ((14, 2), 2)])
@@ -442,7 +314,7 @@ def test_momentum_multi_equals_per_J_scans(engine, name, Js, skip):
         try:
             outs = engine.momentum_multi(PM, Js, skip)
         finally:
-            engine.lib.csm_tune(b"mj_reg", 1)
+            engine.lib.csm_tune(b"mj_reg", 2)
         assert len(outs) == len(Js)
         for J, (M, NR) in zip(Js, outs):
             _, M1, NR1 = engine.momentum(PM, J, skip, chunked=False)
@@ -474,30 +346,3 @@ def test_sweep_batch_multi_J_scan_equals_per_J(engine):
 
     b, _ = SweepRunner(PerJ(engine), cfg).run_batch(PMb, B)
     assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
-
-
-@pytest.mark.parametrize("name", ["edge", "c1", "small", "real_data"])
-def test_wave_decile_kernel_equals_narrow(engine, name):
-    """One wave per row (deciles_wave.hip): labels, counts and ranked rows equal the narrow-row
-    kernel's bit for bit (the range sample differs; the order statistics are exact either
-    way), decile means to rounding; and the stress rows at narrow width against the oracle."""
-    z = load_golden(name)
-    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
-    _, M, NR = engine.momentum(PM, 12, 1)
-    lib = engine.lib
-    a = engine.deciles(M, NR, 10, with_nv=True)
-    try:
-        assert lib.csm_tune(b"dec_wave_max", 16384) == 0
-        b = engine.deciles(M, NR, 10, with_nv=True)
-        for case in [c for c in STRESS if c != "odd_n"][: (3 if name != "edge" else len(STRESS))]:
-            xs = _stress_row(case)[:12_000]
-            Ls, _, _, _ = engine.deciles(_up(xs[None, :]), None, 10)
-            assert np.array_equal(Ls.cpu().numpy()[0], _oracle_labels(xs)), case
-        xo = _stress_row("odd_n")[:9_999]
-        Lo, _, _, _ = engine.deciles(_up(xo[None, :]), None, 10)
-        assert np.array_equal(Lo.cpu().numpy()[0], _oracle_labels(xo))
-    finally:
-        lib.csm_tune(b"dec_wave_max", 0)
-    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
-    ea, eb = a[1].cpu().numpy(), b[1].cpu().numpy()
-    assert np.array_equal(np.isnan(ea), np.isnan(eb)) and max_rel(ea, eb) <= 1e-12

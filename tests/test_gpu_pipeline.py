@@ -197,35 +197,6 @@ def test_pipeline_narrow_rows_fall_back(engine):
         assert max_rel(out.LS.cpu().numpy(), ref["LS"]) <= REL
 
 
-@pytest.mark.parametrize("db", [16, 20, 21])
-def test_day_batch_signal_kernel_bit_identical(engine, db):
-    """k_signal_db (fixed day batches; interior months >= db days, the first and last month
-    partial: 7, 15 and 1 days here) equals k_signal bit for bit -- month prices, ret_1m, mom_J,
-    next_ret, ids."""
-    lib = engine.lib
-    for T in (1_333, 1_341, 1_347):
-        pan = _panel(N=8_000, T=T, seed=db)
-        ms_h = pan["month_start"]
-        d = np.diff(ms_h)
-        maxd, mind = int(d.max()), int(d[1:-1].min())
-        assert mind >= 20 and (d[0] < 20 or d[-1] < 20)
-        P, ms = _up(pan["P"]), _up(ms_h)
-        ref = engine.signal_ids(P, ms, maxd, 12, 1, with_pm=True, with_ret=True)
-        try:
-            assert lib.csm_tune(b"signal_db", db) == 0
-            got = engine.signal_ids(P, ms, maxd, 12, 1, with_pm=True, with_ret=True,
-                                    min_month_days=mind)
-        finally:
-            lib.csm_tune(b"signal_db", 0)
-        for a, b in zip(got, ref):
-            if a.dtype == torch.float64:
-                assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (T, db)
-            else:
-                assert torch.equal(a, b), (T, db)
-        r = O.pipeline(pan["P"], ms_h, 12, 1, 10)
-        assert bits_equal(got[2].cpu().numpy(), r["M"]) and bits_equal(got[3].cpu().numpy(), r["NR"])
-
-
 MERGE_CASES = STRESS + ["lognormal_mild", "wave_cluster"]
 
 
@@ -262,26 +233,6 @@ def test_deciles_ids_merged_equals_general(engine, tune_merge, case):
     assert max_rel(a, rEW) <= REL
 
 
-def test_deciles_ids_merged_pass_takes_and_leaves_rows(engine, tune_merge):
-    """Test hook dec_merge = 2 (merged kernel only): it labels a momentum-like row and an
-    empty row (every label NaN) itself and leaves a row whose uncertain cells overflow one
-    wave's list (its uncertain cells keep the sentinel) and a row of ties across edges
-    (untouched)."""
-    x = np.stack([_stress_row("lognormal_mild"), _stress_row("wave_cluster"),
-                  _stress_row("ties"), _stress_row("empty")])
-    M, IDS = _up(x), _ids_dev(x)
-    L = torch.full(x.shape, 100, dtype=torch.int8, device="cuda:0")
-    assert tune_merge(2) == 0
-    engine.deciles_ids(M, None, IDS, 10, out=(L, None, None, None))
-    torch.cuda.synchronize()
-    Lh = L.cpu().numpy()
-    assert np.array_equal(Lh[0], _oracle_labels(x[0]))
-    assert (Lh[1] == 100).any()   # certain cells were written before the overflow showed
-    assert (Lh[2] == 100).all()
-    assert (Lh[3] == -1).all()    # no ranked cell: the merged kernel finishes the row
-
-
-
 # ---- sweeps: csm_momentum_multi_ids -> csm_deciles_ids on narrow rows (1024 buckets = ids >> 3)
 
 def _month_panel(N, T_m, seed):
@@ -297,7 +248,7 @@ def _month_panel(N, T_m, seed):
     return pm
 
 
-MJ_REG_DEFAULT = 1
+MJ_REG_DEFAULT = 2
 
 
 def test_momentum_multi_ids_bit_identical(engine):
@@ -366,31 +317,3 @@ def test_sweep_batch_ids_equal_streaming(engine):
     a, _ = SweepRunner(engine, SweepConfig()).run_batch(PMb, B)
     b, _ = SweepRunner(engine, SweepConfig(decile_ids=False)).run_batch(PMb, B)
     assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
-
-
-@pytest.mark.parametrize("width", [1_000, 4_000, 5_000, 5_120])
-def test_narrow_register_ids_bit_identical(engine, width):
-    """dec_nreg (rows <= 5120 assets keep their bucket ids in registers, M streamed once): labels,
-    counts, ranked rows and decile means equal the plain narrow kernel's bit for bit, and the
-    labels the oracle's qcut, on every stress case."""
-    lib = engine.lib
-    rng = np.random.default_rng(width + 1)
-    x = np.stack([_stress_row(c, n=width) for c in MERGE_CASES + ["lognormal_mild"] * 3])
-    nr = rng.normal(0.01, 0.1, x.shape)
-    nr[rng.random(x.shape) < 0.03] = np.nan
-    M, NR = _up(x), _up(nr)
-    base = engine.deciles(M, NR, 10, with_nv=True)
-    try:
-        assert lib.csm_tune(b"dec_nreg", 1) == 0
-        got = engine.deciles(M, NR, 10, with_nv=True)
-        lab_only = engine.deciles(M, None, 10)[0]
-    finally:
-        lib.csm_tune(b"dec_nreg", 0)
-    for a, b in zip(got, base):
-        if a.dtype == torch.float64:
-            assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
-        else:
-            assert torch.equal(a, b)
-    assert torch.equal(lab_only, got[0])
-    refL = np.stack([_oracle_labels(x[r]) for r in range(x.shape[0])])
-    assert np.array_equal(got[0].cpu().numpy(), refL)

@@ -393,53 +393,6 @@ def test_legs_only_falls_back_when_a_leg_column_is_missing(engine):
     assert int(flag.item()) == 0
 
 
-@pytest.mark.parametrize("vw", [False, True])
-def test_turnover_general_rows_list_equals_full_grid(engine, vw):
-    """Turnover's general rows (first months, empty cohorts) through the work list or through a
-    second full grid: identical bits (each row is computed by one workgroup either way)."""
-    L, NR, _, PM = _labels(engine, "c1")
-    W = _up(np.abs(PM.cpu().numpy()) * 1e6) if vw else None
-    rng = np.random.default_rng(3)
-    ADV = _up(rng.uniform(1e5, 1e8, L.shape))
-    lib = engine.lib
-    got = {}
-    try:
-        for mode in (0, 1):
-            assert lib.csm_tune(b"turn_list", mode) == 0
-            got[mode] = engine.portfolio_multi(L, NR, 10, Ks=(3, 6, 12), W=W, aum=5e6, ADV=ADV)
-    finally:
-        lib.csm_tune(b"turn_list", 1)
-    for K in (3, 6, 12):
-        for f in ("TURN", "COST", "NET", "LS"):
-            assert bits_equal(getattr(got[0][K], f).cpu().numpy(), getattr(got[1][K], f).cpu().numpy()), (K, f)
-
-
-@pytest.mark.parametrize("B,n_bins", [(1, 10), (6, 10), (4, 3), (3, 2)])
-def test_legs_label_sort_one_wave_per_row_bit_identical(engine, B, n_bins):
-    """The one-wave-per-row legs label sort (equal weights) against the workgroup-per-row one:
-    identical portfolio outputs bit for bit (same segments, sentinels, offsets, leg totals)."""
-    L, NR, _, PM = _labels(engine, "c1")
-    if n_bins != 10:
-        _, M, NR = engine.momentum(PM, 12, 1)
-        L, _, _, _ = engine.deciles(M, None, n_bins)
-    T_m, N = L.shape
-    if B > 1:
-        rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 3 * i, axis=1) for i in range(B)],
-                                     axis=1).reshape(T_m, B * N))
-        L, NR = rep(L), rep(NR)
-    lib = engine.lib
-    got = {}
-    try:
-        for mode in (1, 0):
-            assert lib.csm_tune(b"sort_wave", mode) == 0
-            got[mode] = engine.portfolio_multi(L, NR, n_bins, Ks=(3, 12), B=B, legs_only=True)
-    finally:
-        lib.csm_tune(b"sort_wave", 1)
-    for K in (3, 12):
-        for f in ("PR", "LS", "TURN", "COST", "NET"):
-            assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
-
-
 @pytest.mark.parametrize("B,legs,vw,Ks", [(1, False, False, (3, 6, 12)), (1, True, False, (12, 3)),
                                           (16, True, False, (3, 6, 9, 12)),
                                           (16, False, True, (1, 9, 9)), (4, False, True, (12, 2, 5))])
@@ -448,7 +401,7 @@ def test_overlap_rows_bit_identical(engine, B, legs, vw, Ks):
     against k_overlap (one thread per (K, t, b, decile)): PR / LS / TURN / COST / NET bit for
     bit on single-chunk plans (B = 16), repeated and unsorted K sets, legs-only and full
     accounting, equal and value weights; chunked plans (B = 1, 4: C > 1) keep k_overlap in
-    both modes.  Also the 16-B row staging of k_cohort_seg (seg_stage2) against the 8-B loop."""
+    both modes."""
     L, NR, _, _ = _labels(engine, "c1")
     T_m, N = L.shape
     if B > 1:
@@ -464,38 +417,9 @@ def test_overlap_rows_bit_identical(engine, B, legs, vw, Ks):
     try:
         for mode in (1, 0):
             assert lib.csm_tune(b"overlap_rows", mode) == 0
-            assert lib.csm_tune(b"seg_stage2", mode) == 0
             got[mode] = engine.portfolio_multi(L, NR, 10, Ks=Ks, B=B, W=W, legs_only=legs)
     finally:
         lib.csm_tune(b"overlap_rows", 1)
-        lib.csm_tune(b"seg_stage2", 1)
     for K in set(Ks):
         for f in ("PR", "LS", "TURN", "COST", "NET"):
             assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
-
-
-@pytest.mark.parametrize("B,legs,Ks", [(1, False, (3, 6, 12)), (16, True, (3, 6, 9, 12)),
-                                       (6, True, (12, 1)), (16, False, (2, 2, 7))])
-def test_turn_prep_bit_identical(engine, B, legs, Ks):
-    """Steady equal-weight turnover rows with k_turn_prep's once-per-row factors (turn_prep 1)
-    against each workgroup's own prologue (0): TURN / COST / NET / LS bit for bit, including
-    the first months (general rows, routed by the prepared full-leg masks)."""
-    L, NR, _, _ = _labels(engine, "c1")
-    T_m, N = L.shape
-    assert N % 4 == 0
-    if B > 1:
-        rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 7 * i, axis=1) for i in range(B)],
-                                     axis=1).reshape(T_m, B * N))
-        L, NR = rep(L), rep(NR)
-    lib = engine.lib
-    got = {}
-    try:
-        for mode in (1, 0):
-            assert lib.csm_tune(b"turn_prep", mode) == 0
-            got[mode] = engine.portfolio_multi(L, NR, 10, Ks=Ks, B=B, legs_only=legs)
-    finally:
-        lib.csm_tune(b"turn_prep", 1)
-    for K in set(Ks):
-        for f in ("TURN", "COST", "NET", "LS"):
-            assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
-        assert np.isfinite(got[1][K].TURN.cpu().numpy()[-1]).all()

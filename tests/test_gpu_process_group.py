@@ -163,3 +163,23 @@ def test_sweep_shards_two_processes_equal_one_process(engine):
         assert np.array_equal(tab[..., 0], one[..., 0])
         m = ~np.isnan(one)
         assert np.allclose(tab[m], one[m], rtol=1e-12, atol=1e-15)
+
+
+def test_csm_allgather_single_rank(engine):
+    """The C-ABI collective (csm_comm_unique_id / csm_allgather_init / csm_allgather over RCCL)
+    on a one-rank communicator: the gather returns the rank's buffer, on the engine's stream;
+    the date-shard pass driven through it equals the torch.distributed one (G = 1: no gather
+    runs, the construction and the call sequence are exercised).  Two ranks need two GPUs
+    (RCCL rejects two ranks on one device): bench.py --collective csm on the driver's node."""
+    from csmom.distributed import CsmCollective
+    coll = CsmCollective(engine)
+    try:
+        x = torch.arange(1000, dtype=torch.float64, device=engine.device) * 0.5
+        y = coll.all_gather_stack(x)
+        torch.cuda.synchronize()
+        assert tuple(y.shape) == (1, 1000) and torch.equal(y[0], x)
+        ids = torch.randint(0, 1 << 15, (7, 33), dtype=torch.int16, device=engine.device)
+        assert torch.equal(coll.all_gather_stack(ids)[0], ids)
+    finally:
+        coll.close()
+    assert engine.lib.csm_allgather(engine.ctx, None, None, 8) != 0   # freed: no communicator

@@ -95,11 +95,10 @@ def test_fused_shards_four_wave_blocks(engine, G, J, skip):
     out = engine.run(P, _up(ms), J, skip, 10, with_ret=True)
     lib = engine.lib
     try:
-        assert lib.csm_tune(b"signal_bwf", 4) == 0 and lib.csm_tune(b"signal_nbuf", 2) == 0
+        assert lib.csm_tune(b"signal_bwf", 4) == 0
         M, NR, L, EW, CNT, LS = virtual_shards(engine, P, ms, G, J, skip, 10, fused=True)
     finally:
         lib.csm_tune(b"signal_bwf", 0)
-        lib.csm_tune(b"signal_nbuf", 4)
     assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
     assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
     assert torch.equal(L, out.L)

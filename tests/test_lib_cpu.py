@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     raw = ctypes.CDLL(str(csmom.lib_path()))
     for s in header_symbols():
         assert hasattr(raw, s), s
-    assert lib.csm_abi_version() == 2
+    assert lib.csm_abi_version() == 3
 
 
 def test_null_context_is_inval():
@@ -66,26 +66,37 @@ def test_engine_requires_gpu():
 
 def test_tune_keys_documented_in_header_are_accepted():
     """csm_tune only sets process-wide knobs (no GPU call): every key include/csmom.h lists
-    takes its documented values and restores its default; unknown keys / values are rejected."""
+    takes its documented values and restores its default; unknown keys / values are rejected,
+    including the profiling ablations and the measured-and-dropped variants of earlier rounds
+    (none of them is in the library any more)."""
     import csmom
     lib = csmom.load_library()
-    cases = {b"signal_vec": ([1, 2], 2), b"signal_nbuf": ([2, 3, 4], 4), b"dec_ablate": ([0, 1], 0),
-             b"signal_bwf": ([0, 1, 2, 3, 4], 0),
-             b"dec_ids": ([0, 1], 0), b"dec_reg": ([0, 1, 2], 0),
-             b"dec_narrow_max": ([0, 16384], 16384), b"mj_reg": ([0, 1, 2], 2),
-             b"signal_store": ([0, 1, 2, 3, 4], 0), b"signal_rr": ([0, 1], 0),
-             b"signal_bl": ([0, 1], 1), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
-             b"turn_list": ([0, 1, 2], 1), b"sort_wave": ([0, 1], 1),
+    cases = {b"signal_vec": ([1, 2], 2), b"signal_bwf": ([0, 1, 4], 0),
+             b"dec_merge": ([0, 1], 1), b"dec_narrow_max": ([0, 16384], 16384),
+             b"mj_reg": ([0, 1, 2], 2), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
-             b"seg_stage2": ([0, 1], 1), b"turn_gen_grid": ([1, 2048], 8192),
-             b"turn_prep": ([0, 1], 1)}
+             b"turn_gen_grid": ([1, 2048], 8192)}
     for key, (vals, default) in cases.items():
         for v in vals:
             assert lib.csm_tune(key, v) == 0, (key, v)
         assert lib.csm_tune(key, default) == 0
-    assert lib.csm_tune(b"dec_reg", 3) != 0
-    assert lib.csm_tune(b"signal_vec", 3) != 0
-    assert lib.csm_tune(b"overlap_rows", 2) != 0
-    assert lib.csm_tune(b"turn_want", 0) != 0
-    assert lib.csm_tune(b"no_such_knob", 1) != 0
+    for key, v in ((b"signal_vec", 3), (b"signal_bwf", 2), (b"dec_merge", 2), (b"overlap_rows", 2),
+                   (b"turn_want", 0), (b"no_such_knob", 1)):
+        assert lib.csm_tune(key, v) != 0, (key, v)
+    # result-corrupting profiling knobs and negative-result variants are gone
+    for key in (b"dec_ablate", b"signal_store", b"signal_rr", b"signal_db", b"signal_mw",
+                b"dec_reg", b"dec_nreg", b"dec_wave_max", b"dec_ids", b"month_end_rows",
+                b"signal_nbuf", b"signal_bw", b"signal_bl", b"turn_list", b"sort_wave",
+                b"seg_stage2", b"turn_prep"):
+        assert lib.csm_tune(key, 0) != 0 and lib.csm_tune(key, 1) != 0, key
     assert lib.csm_tune(None, 1) != 0
+
+
+def test_collective_entry_points_without_gpu():
+    """The C-ABI all-gather validates its arguments before touching RCCL or the GPU."""
+    import csmom
+    lib = csmom.load_library()
+    assert lib.csm_allgather_init(None, None, 0, 1) == -1
+    assert lib.csm_allgather(None, None, None, 8) == -1
+    assert lib.csm_allgather_free(None) == -1
+    assert lib.csm_comm_unique_id(None) == -1
