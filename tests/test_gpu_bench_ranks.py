@@ -77,13 +77,16 @@ def _spawn_bench(argv, timeout=200):
 
 def test_bench_c4_two_ranks_gloo(engine, tmp_path):
     from csmom.synth import make_device_panel, shard_calendar
-    N, DAYS, SEED = 20_000, 1_400, 4
+    # wide enough for the fused shard pass with bucket ids (N >= 32768, N % 4 == 0): each rank
+    # ranks its months exactly as the one-GPU csm_pipeline does, so the means are bit-identical
+    N, DAYS, SEED = 40_000, 1_100, 4
     dump = tmp_path / "c4.npz"
     line = _spawn_bench(["--gpus", "2", "--backend", "gloo", "--assets", str(N), "--days",
                          str(DAYS), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
                          "--seed", str(SEED), "--dump", str(dump)])
     assert line["n_gpus"] == 2 and line["decile_match_pct"] == 100.0
     assert "all 2 ranks" in line["decile_check"]
+    assert line["engine_path"].startswith("speculative fused")
     # the same global panel on one GPU: both shards, concatenated along the days
     total = DAYS * WORLD
     parts = []
