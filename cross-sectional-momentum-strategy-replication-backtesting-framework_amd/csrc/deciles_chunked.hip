@@ -32,7 +32,7 @@
 #define DC_FIN_THREADS 256
 #define DC_CAP 2048         // candidates per row (cells of the interior ranges)
 #define DC_LW 256           // list entries per wave and chunk
-#define DC_REC 128          // ints per row record
+#define DC_REC 192          // ints per row record
 
 // row record (int32 offsets)
 #define R_N 0
@@ -42,7 +42,9 @@
 #define R_PRE (R_RHI + MAXQ)
 #define R_CNT (R_PRE + MAXQ)
 #define R_OFF (R_CNT + MAXQ)
-static_assert(R_OFF + MAXQ <= DC_REC, "row record");
+#define R_RP (R_OFF + MAXQ)   // residual ranks (inside the range) of edge k's two order statistics
+#define R_RQ (R_RP + MAXQ)
+static_assert(R_RQ + MAXQ <= DC_REC, "row record");
 
 namespace {
 
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(DC_HIST_THREADS, 2) void k_dec_hist(const uint16_t*
   int32_t* rec = REC + (int64_t)t * DC_REC;
   const int k = lane;
   bool ok = true;
-  int rl = 0, rh = 0, pre = 0, cn = 0;
+  int rl = 0, rh = 0, pre = 0, cn = 0, rp = 0, rq = 0;
   if (n > 0 && k <= NB) {
     if (k == 0) {
       rl = rh = bucket_of_rank(hist, 0);
@@ -146,6 +148,8 @@ __global__ __launch_bounds__(DC_HIST_THREADS, 2) void k_dec_hist(const uint16_t*
           rh = bucket_of_rank(hist, ph);
           pre = (int)hist[rl];
           cn = (int)((rh + 1 < DC_HB ? (int64_t)hist[rh + 1] : n) - pre);
+          rp = (int)(pi - pre);
+          rq = (int)(ph - pre);
         }
       }
     }
@@ -168,6 +172,8 @@ __global__ __launch_bounds__(DC_HIST_THREADS, 2) void k_dec_hist(const uint16_t*
     rec[R_PRE + k] = pre;
     rec[R_CNT + k] = cn;
     rec[R_OFF + k] = inc - own;
+    rec[R_RP + k] = rp;
+    rec[R_RQ + k] = rq;
   }
   if (lane == 0) {
     rec[R_N] = (int32_t)n;
@@ -177,7 +183,9 @@ __global__ __launch_bounds__(DC_HIST_THREADS, 2) void k_dec_hist(const uint16_t*
 }
 
 // ----------------------------------------------------------------------------- k_dec_sweep
-// Chunk (blockIdx.x) of date t (blockIdx.y): DC_SWEEP_THREADS x 4 cells per step, ITER steps.
+// Chunk (blockIdx.x) of date t (blockIdx.y): ITER groups of 4 cells per lane, all loads issued
+// before any is used.  The bucket -> label table of the row is rebuilt in LDS from the record's
+// ranges (8 KB; one barrier), so a cell's label is one LDS byte read.
 template <int NB, int ITER>
 __global__ __launch_bounds__(DC_SWEEP_THREADS) void k_dec_sweep(
     const uint16_t* __restrict__ IDS, const double* __restrict__ NR, int64_t N,
@@ -185,102 +193,103 @@ __global__ __launch_bounds__(DC_SWEEP_THREADS) void k_dec_sweep(
     double* __restrict__ PART, int32_t* __restrict__ LCNT, uint32_t* __restrict__ LIST) {
   constexpr int NW = DC_SWEEP_THREADS / 64;
   constexpr int64_t CH = (int64_t)ITER * 4 * DC_SWEEP_THREADS;
+  __shared__ __attribute__((aligned(16))) int8_t tab[DC_HB];
+  // per-lane label sums in LDS, one private column per lane: a cell adds with one ds_add_f64 /
+  // ds_add_u32 (no return, no contention, the lane's cells in program order -- so the same
+  // rounding as sequential adds, deterministic) instead of NB compare / select / fma per cell
+  // in registers, which made the sweep VALU-bound
+  __shared__ double acc[NB][DC_SWEEP_THREADS];
+  __shared__ uint32_t acn[NB][DC_SWEEP_THREADS];
+  __shared__ double wh[NW][NB], wlo[NW][NB];
+  __shared__ int wc[NW][NB];
   const int c = blockIdx.x, t = blockIdx.y, C = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (FLG[t]) return;   // the general kernel ranks this row
   const int32_t* rec = REC + (int64_t)t * DC_REC;
-  int rlo[NB + 1], rhi[NB + 1];
-#pragma unroll
-  for (int k = 0; k <= NB; ++k) { rlo[k] = rec[R_RLO + k]; rhi[k] = rec[R_RHI + k]; }
+  const int64_t i0 = (int64_t)c * CH + 4 * tid;
   const int64_t i_end = min(N, (int64_t)(c + 1) * CH);
   const uint16_t* irow = IDS + (int64_t)t * N;
   const double* nrow = NR + (int64_t)t * N;
   int8_t* lrow = L + (int64_t)t * N;
+  // every load of the chunk in flight first
+  uint2 pk[ITER];
+  double2 ra[ITER], rb[ITER];
+#pragma unroll
+  for (int u = 0; u < ITER; ++u) {
+    const int64_t i = i0 + (int64_t)u * 4 * DC_SWEEP_THREADS;
+    pk[u] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    ra[u] = rb[u] = make_double2(0.0, 0.0);
+    if (i < i_end) {
+      pk[u] = *reinterpret_cast<const uint2*>(irow + i);
+      ra[u] = *reinterpret_cast<const double2*>(nrow + i);
+      rb[u] = *reinterpret_cast<const double2*>(nrow + i + 2);
+    }
+  }
+  // bucket -> label table meanwhile: the ranges are sorted and disjoint; inside edge 0's /
+  // edge NB's range the label is 0 / NB - 1, inside an interior range -3 (uncertain), between
+  // ranges j - 1 and j: j - 1.  Each thread owns 32 consecutive buckets.
+  {
+    constexpr int PT = DC_HB / DC_SWEEP_THREADS;
+    const int b0 = tid * PT;
+    int j = 0;   // ranges wholly below the current bucket
+    while (j <= NB && rec[R_RHI + j] < b0) ++j;
+    uint32_t w = 0;
+#pragma unroll 4
+    for (int o = 0; o < PT; ++o) {
+      const int b2 = b0 + o;
+      while (j <= NB && rec[R_RHI + j] < b2) ++j;
+      int lab = j - 1;
+      if (j <= NB && rec[R_RLO + j] <= b2) lab = j == 0 ? 0 : (j == NB ? NB - 1 : -3);
+      w |= (uint32_t)(uint8_t)(int8_t)lab << (8 * (o & 3));
+      if ((o & 3) == 3) { reinterpret_cast<uint32_t*>(tab + b0)[o >> 2] = w; w = 0; }
+    }
+  }
+  __syncthreads();
   const int64_t wl = ((int64_t)t * C + c) * NW + wid;   // this wave's list
   uint32_t* list = LIST + wl * DC_LW;
   const uint64_t lt = (1ull << lane) - 1ull;
-  int lc = 0;            // wave-uniform list length
-  bool ovf = false;      // wave-uniform
-  double hs[NB];
-  int cn[NB];
+  int lc = 0;   // wave-uniform list length
 #pragma unroll
-  for (int d = 0; d < NB; ++d) { hs[d] = 0.0; cn[d] = 0; }
-  constexpr int U = 4;   // 4-cell groups of ids + next_ret in flight per lane
-  for (int it = 0; it < ITER; it += U) {
-    uint2 pk[U];
-    double2 ra[U], rb[U];
+  for (int d = 0; d < NB; ++d) { acc[d][tid] = 0.0; acn[d][tid] = 0u; }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = (int64_t)c * CH + (int64_t)(it + u) * 4 * DC_SWEEP_THREADS + 4 * tid;
-      pk[u] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-      ra[u] = rb[u] = make_double2(0.0, 0.0);
-      if (i < i_end) {
-        pk[u] = *reinterpret_cast<const uint2*>(irow + i);
-        ra[u] = *reinterpret_cast<const double2*>(nrow + i);
-        rb[u] = *reinterpret_cast<const double2*>(nrow + i + 2);
+  for (int u = 0; u < ITER; ++u) {
+    const int64_t i = i0 + (int64_t)u * 4 * DC_SWEEP_THREADS;
+    const uint32_t id[4] = {pk[u].x & 0xFFFFu, pk[u].x >> 16, pk[u].y & 0xFFFFu, pk[u].y >> 16};
+    const double rs[4] = {ra[u].x, ra[u].y, rb[u].x, rb[u].y};
+    int lab[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lab[q] = id[q] == CSM_FB_NAN ? -1 : (int)tab[id[q]];
+    const uint32_t w = (uint32_t)(uint8_t)lab[0] | ((uint32_t)(uint8_t)lab[1] << 8) |
+                       ((uint32_t)(uint8_t)lab[2] << 16) | ((uint32_t)(uint8_t)lab[3] << 24);
+    if (i < i_end) *reinterpret_cast<uint32_t*>(lrow + i) = w;   // uncertain bytes: finish
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (lab[q] >= 0 && rs[q] == rs[q]) {
+        atomicAdd(&acc[lab[q]][tid], rs[q]);
+        atomicAdd(&acn[lab[q]][tid], 1u);
       }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = (int64_t)c * CH + (int64_t)(it + u) * 4 * DC_SWEEP_THREADS + 4 * tid;
-      const uint32_t id[4] = {pk[u].x & 0xFFFFu, pk[u].x >> 16, pk[u].y & 0xFFFFu, pk[u].y >> 16};
-      const double rs[4] = {ra[u].x, ra[u].y, rb[u].x, rb[u].y};
-      uint32_t w = 0;
-      uint32_t um = 0;   // uncertain cells of the group
+    // uncertain cells into the wave's list, (group, cell, lane) order: deterministic
+    const bool any = lab[0] == -3 || lab[1] == -3 || lab[2] == -3 || lab[3] == -3;
+    if (__ballot(any)) {   // wave-uniform, rare
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int b = (int)id[q];
-        int j = 0, i2 = 0;   // ranges wholly below b / ranges starting at or below b
-#pragma unroll
-        for (int k = 0; k <= NB; ++k) { j += rhi[k] < b ? 1 : 0; i2 += rlo[k] <= b ? 1 : 0; }
-        // inside range j (i2 == j + 1): edge 0's / edge NB's range hold labels 0 / NB - 1, an
-        // interior range is uncertain; between ranges j - 1 and j: label j - 1
-        int lab = (i2 == j + 1) ? (j == 0 ? 0 : (j == NB ? NB - 1 : -3)) : j - 1;
-        lab = id[q] == CSM_FB_NAN ? -1 : lab;
-        um |= (lab == -3 ? 1u : 0u) << q;
-        w |= (uint32_t)(uint8_t)(int8_t)lab << (8 * q);
-        const bool ok = lab >= 0 && rs[q] == rs[q];
-        const double r = ok ? rs[q] : 0.0;
-#pragma unroll
-        for (int d = 0; d < NB; ++d) {
-          const bool h = ok && lab == d;
-          hs[d] = fma(h ? 1.0 : 0.0, r, hs[d]);   // == hs[d] + (h ? r : 0.0)
-          cn[d] += h ? 1 : 0;
-        }
-      }
-      if (i < i_end) *reinterpret_cast<uint32_t*>(lrow + i) = w;   // uncertain bytes: finish
-      // the group's uncertain cells into the wave's list (wave prefix over lanes; list order =
-      // (step, lane, cell): deterministic)
-      const int nh = __popc(um);
-      int inc = nh;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += v;
-      }
-      const int tot = __shfl(inc, 63, 64);
-      if (tot) {
-        if (lc + tot > DC_LW) ovf = true;
-        if (!ovf) {
-          int pos = lc + inc - nh;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if ((um >> q) & 1u) list[pos++] = (uint32_t)(i + q);
-        }
-        lc += tot;
+        const bool un = lab[q] == -3;
+        const uint64_t mk = __ballot(un);
+        const int pos = lc + __popcll(mk & lt);
+        if (un && pos < DC_LW) list[pos] = (uint32_t)(i + q);
+        lc += __popcll(mk);
       }
     }
   }
-  (void)lt;
+  const bool ovf = lc > DC_LW;
   if (lane == 0) LCNT[wl] = ovf ? 0 : lc;
   if (ovf && lane == 0) FLG[t] = 1;   // (idempotent) the general kernel re-ranks the row
   // per-label partial sums of the chunk: wave trees (two-sum), waves in order
-  __shared__ double wh[NW][NB > 0 ? NB : 1], wlo[NW][NB > 0 ? NB : 1];
-  __shared__ int wc[NW][NB > 0 ? NB : 1];
 #pragma unroll
   for (int d = 0; d < NB; ++d) {
-    double h = hs[d], l = 0.0;
-    int cc = cn[d];
+    double h = acc[d][tid], l = 0.0;
+    int cc = (int)acn[d][tid];
     for (int o = 32; o > 0; o >>= 1) {
       const double h2 = __shfl_down(h, o, 64), l2 = __shfl_down(l, o, 64);
       const int c2 = __shfl_down(cc, o, 64);
@@ -319,13 +328,13 @@ __global__ __launch_bounds__(DC_FIN_THREADS) void k_dec_finish(
   constexpr int NWS = DC_SWEEP_THREADS / 64;   // lists per chunk
   constexpr int NWF = DC_FIN_THREADS / 64;
   __shared__ uint32_t ent[DC_CAP];
-  __shared__ double xv[DC_CAP], cand[DC_CAP];
+  __shared__ double xv[DC_CAP], rv[DC_CAP], cand[DC_CAP];
+  __shared__ uint8_t ck[DC_CAP];
   __shared__ int lofs[65];
-  __shared__ int fill[MAXQ];
+  __shared__ int fill[MAXQ], roff[MAXQ], rcnt[MAXQ], rrp[MAXQ], rrq[MAXQ];
   __shared__ double aval[MAXQ], bval[MAXQ], bins[MAXQ];
   __shared__ double wh[NWF][NB], wlo[NWF][NB];
   __shared__ int wc[NWF][NB];
-  __shared__ int nent_s;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (FLG[t]) return;   // the general kernel ranks this row
   const int32_t* rec = REC + (int64_t)t * DC_REC;
@@ -334,6 +343,13 @@ __global__ __launch_bounds__(DC_FIN_THREADS) void k_dec_finish(
   const double* row = M + (int64_t)t * N;
   const double* nrow = NR + (int64_t)t * N;
   int8_t* lrow = L + (int64_t)t * N;
+  if (tid <= NB) {
+    fill[tid] = 0;
+    roff[tid] = rec[R_OFF + tid];
+    rcnt[tid] = rec[R_CNT + tid];
+    rrp[tid] = rec[R_RP + tid];
+    rrq[tid] = rec[R_RQ + tid];
+  }
   // the row's lists, (chunk, wave) order, compacted into ent[]
   const int nl = C * NWS;
   for (int l0 = 0; l0 < nl; l0 += 64) {   // block-uniform trip count
@@ -347,8 +363,8 @@ __global__ __launch_bounds__(DC_FIN_THREADS) void k_dec_finish(
         if (lane >= o) inc += v;
       }
       const int base = l0 == 0 ? 0 : lofs[64];
-      lofs[lane] = base + inc - cl;
       __builtin_amdgcn_wave_barrier();
+      lofs[lane] = base + inc - cl;
       if (lane == 63) lofs[64] = base + inc;
     }
     __syncthreads();
@@ -361,33 +377,31 @@ __global__ __launch_bounds__(DC_FIN_THREADS) void k_dec_finish(
     }
     __syncthreads();
   }
-  if (tid == 0) nent_s = min(lofs[64], DC_CAP);
-  if (tid <= NB) fill[tid] = 0;
-  __syncthreads();
-  const int ne = nent_s;   // == the row's candidate total (<= DC_CAP, checked by k_dec_hist)
-  int rlo[NB + 1], rhi[NB + 1];
+  const int ne = min(lofs[64], DC_CAP);   // == the row's candidate total (checked by k_dec_hist)
+  int rhi[NB + 1];
 #pragma unroll
-  for (int k = 0; k <= NB; ++k) { rlo[k] = rec[R_RLO + k]; rhi[k] = rec[R_RHI + k]; }
-  // mom_J of the listed cells (all loads in flight), into their range's candidate slots
+  for (int k = 0; k <= NB; ++k) rhi[k] = rec[R_RHI + k];
+  // mom_J and next_ret of the listed cells (all loads in flight), the values into their
+  // range's candidate slots
   for (int p = tid; p < ne; p += DC_FIN_THREADS) {
-    const double x = row[ent[p]];
+    const uint32_t idx = ent[p];
+    const double x = row[idx];
+    rv[p] = nrow[idx];
     xv[p] = x;
     const int b = csm_fbucket(x);
     int j = 0;
 #pragma unroll
     for (int k = 0; k <= NB; ++k) j += rhi[k] < b ? 1 : 0;   // x lies in interior range j
-    const int pos = atomicAdd(&fill[j], 1);
-    cand[rec[R_OFF + j] + pos] = x;
+    const int q = roff[j] + atomicAdd(&fill[j], 1);
+    cand[q] = x;
+    ck[q] = (uint8_t)j;
   }
   __syncthreads();
   // order statistics inside each range by counting selection (ties broken by slot position):
   // the member whose rank equals the target's residual rank
   for (int p = tid; p < ne; p += DC_FIN_THREADS) {
-    // range of slot p: the last range whose offset is <= p (cnt > 0)
-    int k = 1;
-#pragma unroll
-    for (int kk = 2; kk < NB; ++kk) k = (rec[R_OFF + kk] <= p && rec[R_CNT + kk] > 0) ? kk : k;
-    const int off = rec[R_OFF + k], cntk = rec[R_CNT + k];
+    const int k = ck[p];
+    const int off = roff[k], cntk = rcnt[k];
     const int i = p - off;
     const double x = cand[p];
     int rank = 0;
@@ -395,13 +409,8 @@ __global__ __launch_bounds__(DC_FIN_THREADS) void k_dec_finish(
       const double y = cand[off + j];
       rank += (y < x || (y == x && j < i)) ? 1 : 0;
     }
-    const double v = (double)(n - 1) * qt.q[k];
-    const double pf = floor(v);
-    const int64_t pi = (int64_t)pf;
-    const int64_t ph = (v - pf != 0.0) ? pi + 1 : pi;
-    const int64_t pre = rec[R_PRE + k];
-    if (rank == (int)(pi - pre)) aval[k] = x;
-    if (rank == (int)(ph - pre)) bval[k] = x;
+    if (rank == rrp[k]) aval[k] = x;
+    if (rank == rrq[k]) bval[k] = x;
   }
   __syncthreads();
   // interior edges (NumPy _lerp); edge 0 / n_bins (min / max) never decide a listed cell's label
@@ -426,13 +435,12 @@ __global__ __launch_bounds__(DC_FIN_THREADS) void k_dec_finish(
   // labels of the listed cells (searchsorted-left over the edges: every listed cell is above
   // edge 0 and below edge n_bins), next_ret summed in list order
   for (int p = tid; p < ne; p += DC_FIN_THREADS) {
-    const uint32_t idx = ent[p];
     const double x = xv[p];
     int lab = 0;
 #pragma unroll
     for (int k = 1; k < NB; ++k) lab += eb[k - 1] < x ? 1 : 0;
-    lrow[idx] = (int8_t)lab;
-    const double r = nrow[idx];
+    lrow[ent[p]] = (int8_t)lab;
+    const double r = rv[p];
     const bool ok = r == r;
 #pragma unroll
     for (int d = 0; d < NB; ++d) {

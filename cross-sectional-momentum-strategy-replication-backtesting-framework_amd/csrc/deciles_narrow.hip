@@ -1,6 +1,6 @@
 // deciles_narrow.hip -- the per-date qcut kernel for rows of a few thousand assets (C2 / C3
 // and the C5 bootstrap batches: 30k rows of 5k assets per launch).  Same algorithm and results
-// as the wide-row kernel (csrc/deciles.inc); 256 threads, 1024 buckets and 2048 candidates
+// as the wide-row kernel (csrc/deciles.inc); 256 threads, 1024 buckets and 1024 candidates
 // use a quarter of its LDS, so four times as many rows are in flight per CU -- the per-row
 // serial phases (range, targets, selection, edges) dominate at this width.
 #include "csm_common.h"

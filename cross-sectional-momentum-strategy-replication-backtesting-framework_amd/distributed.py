@@ -139,7 +139,7 @@ class DateShardPipeline:
             T_m = month_start_local.numel() - 1
             self._check_months(T_m)
             if self.G == 1:
-                if _shard_ids(st, P_local, month_start_local) is not None:   # = csm_pipeline
+                if _wants_ids(st, P_local):                                   # = csm_pipeline
                     _, _, M, NR, ids = st.signal_ids(P_local, month_start_local, max_month_days,
                                                      J, s)
                     return self._rank_and_gather(M, NR, ids)
@@ -188,13 +188,18 @@ class DateShardPipeline:
         return ShardResult(M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS)
 
 
+def _wants_ids(stages, P):
+    """Whether the fused shard pass ranks from bucket ids: the engine, on the rows csm_pipeline
+    ranks from ids too (N % 4 == 0, wider than the narrow-row decile kernels), so a sharded run's
+    decile means are the one-GPU pipeline's bit for bit."""
+    from .engine import DEC_NARROW_MAX
+    N = P.shape[1]
+    return bool(getattr(stages, "shard_ids", False)) and N % 4 == 0 and N > DEC_NARROW_MAX
+
+
 def _shard_ids(stages, P, month_start):
-    """An id buffer for the fused shard pass when the stages rank from bucket ids: the engine,
-    on the rows csm_pipeline ranks from ids too (N % 4 == 0, wider than the 16,384-asset
-    narrow-row kernels), so a sharded run's decile means are the one-GPU pipeline's bit for bit.
-    None: rank from mom_J."""
-    T_d, N = P.shape
-    if not getattr(stages, "shard_ids", False) or N % 4 or N <= 16384:
+    """An id buffer for the fused shard pass when _wants_ids; None: rank from mom_J."""
+    if not _wants_ids(stages, P):
         return None
     return torch.empty((month_start.numel() - 1, N), dtype=torch.int16, device=P.device)
 

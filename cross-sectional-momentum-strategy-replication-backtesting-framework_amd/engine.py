@@ -21,6 +21,8 @@ from ._lib import ABSENT_BITS, check, load_library
 
 QTABLE_CACHE: dict[int, np.ndarray] = {}
 FUSED_MIN_N = 32768  # below this the fused kernel has too few waves to fill 256 CUs
+DEC_NARROW_MAX = 16384   # widest row of the narrow-row decile kernels (libcsmom's default)
+LEGS_MAX_N = 7168        # widest row of the legs-only portfolio accounting (SEG_MAXN)
 
 
 def quantile_table(n_bins: int) -> np.ndarray:
@@ -79,6 +81,7 @@ class PortfolioOut:
     TURN: torch.Tensor | None = None  # [T_m][B] long-short turnover
     COST: torch.Tensor | None = None  # [T_m][B] transaction cost
     NET: torch.Tensor | None = None   # [T_m][B] LS - COST
+    legs_only: bool = False           # PR holds deciles 0 and n_bins - 1 only (NaN elsewhere)
 
 
 @dataclass
@@ -277,7 +280,9 @@ class Engine:
 
     def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False):
         """csm_deciles_ids: deciles() from the ids of signal_ids / momentum_multi(with_ids=True)
-        (same labels / counts).  Rows of <= 16384 assets take the narrow kernel (1024 buckets);
+        (same labels / counts).  Rows of <= 16384 assets take the narrow kernel (2048 buckets:
+        the fixed map's ids >> 2); wider rows with next_ret the chunked pass (histogram /
+        load-balanced sweep / finish);
         needs N % 4 == 0."""
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)
@@ -413,7 +418,7 @@ class Engine:
                 _need(t, nm, torch.float64, (T_m, BN), self.device)
         Ks = [int(k) for k in Ks]
         Kmax = max(Ks)
-        legs_only = bool(legs_only) and N <= 7168
+        legs_only = bool(legs_only) and N <= LEGS_MAX_N   # wider rows: every decile
         nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, N, int(n_bins), Kmax))
         if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
             workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
@@ -440,9 +445,10 @@ class Engine:
             self._call("csm_portfolio_from_cohorts_multi", *args)
         pick = lambda x, q: None if x is None else x[q]
         res = {K: PortfolioOut(PR=PR[q], LS=LS[q], TURN=pick(TURN, q), COST=pick(COST, q),
-                               NET=pick(NET, q)) for q, K in enumerate(Ks)}
+                               NET=pick(NET, q), legs_only=legs_only) for q, K in enumerate(Ks)}
         if return_stacked:
-            return res, PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET)
+            return res, PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET,
+                                     legs_only=legs_only)
         return res
 
     def summary(self, LS, TURN=None, COST=None, NET=None, freq=12.0):

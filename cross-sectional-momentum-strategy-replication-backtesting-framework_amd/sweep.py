@@ -33,10 +33,13 @@ SUMMARY_FIELDS = ("months", "mean", "sharpe", "turnover", "cost", "net_mean", "n
 
 
 def _free_bytes(t: torch.Tensor) -> int:
-    """Free memory of t's device (host tensors: unbounded)."""
+    """Memory available to new tensors on t's device: free device memory plus what torch's
+    caching allocator holds reserved but unused (a previous batch's freed panels), so the
+    multi-J choice does not flip between batches.  Host tensors: unbounded."""
     if t.is_cuda:
         free, _ = torch.cuda.mem_get_info(t.device)
-        return int(free)
+        cached = torch.cuda.memory_reserved(t.device) - torch.cuda.memory_allocated(t.device)
+        return int(free + max(cached, 0))
     return 1 << 62
 
 
@@ -95,9 +98,11 @@ class SweepConfig:
     # rows from them (csm_momentum_multi_ids -> csm_deciles_ids): 2-B ids per cell instead of
     # up to three passes over mom_J; same labels
     decile_ids: bool = True
-    # accounting of the two legs only (deciles 0 and n_bins - 1): the summary table (LS, TURN,
-    # COST, NET) is bit for bit the full path's; the per-strategy series' PR holds the legs
-    # (NaN elsewhere).  False: every decile's overlapped return
+    # accounting of the two legs only (deciles 0 and n_bins - 1) on rows of <= 7168 assets: the
+    # summary table (LS, TURN, COST, NET) is bit for bit the full path's; the per-strategy
+    # series' PR then holds the legs (NaN elsewhere; PortfolioOut.legs_only says which form a
+    # series has -- wider rows always get every decile).  False: every decile's overlapped
+    # return
     legs_only: bool = True
     extra: dict = field(default_factory=dict)
 
