@@ -87,6 +87,9 @@ def parse(argv=None):
     ap.add_argument("--per-j-scan", action="store_true",
                     help="C5: one scan per J instead of every J of a wide batch from one scan "
                          "(csm_momentum_multi, the default)")
+    ap.add_argument("--no-boot-scan", action="store_true",
+                    help="C5: csm_bootstrap -> multi-J scan on materialised panels instead of "
+                         "csm_boot_scan (the panel generated in registers, one shared next_ret)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group: nccl (= RCCL over xGMI, one GPU per rank) or gloo "
                          "(device tensors staged through host memory; the 1-GPU rehearsal of the "
@@ -543,6 +546,16 @@ class TimedStages:
         return self._wrap("bootstrap(k_bootstrap_*)", 16.0 * T_m * B * N, self.eng.bootstrap,
                           R, B, **k)
 
+    def boot_scan(self, R, B, Js, skip=1, **k):
+        T_m, N = R.shape   # algorithmic: R once, mom_J (+ ids) per J and one next_ret written
+        per = (8.0 + (2.0 if k.get("with_ids", True) else 0.0)) * len(Js) + 8.0
+        return self._wrap("bootscan(k_bootstrap_index+k_boot_scan)", 8.0 * T_m * N + per * T_m * B * N,
+                          self.eng.boot_scan, R, B, Js, skip, **k)
+
+    @property
+    def device(self):
+        return self.eng.device
+
     def stage_report(self, steps):
         agg = {}
         for name, e0, e1, nb in self.rec:
@@ -597,7 +610,7 @@ def sweep_main(args):
     ts = TimedStages(eng)
     scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
                              multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids,
-                             legs_only=not args.full_deciles)
+                             legs_only=not args.full_deciles, boot_scan=not args.no_boot_scan)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":

@@ -78,6 +78,8 @@ SIGNATURES = {
     "csm_summary": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _f64, _p]),
     "csm_bootstrap": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64,
                                      _f64, _p, _p]),
+    "csm_boot_scan": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64, _f64,
+                                     _p, _i32, _i32, _p, _p, _p, _p, _p]),
     "csm_momentum_chunked": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _i32, _p, _p, _p,
                                             _p, _p]),
     "csm_momentum_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),

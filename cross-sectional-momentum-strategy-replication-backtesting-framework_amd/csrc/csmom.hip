@@ -1242,8 +1242,9 @@ static int g_tune_mj_reg = 2;
 // rows with at most this many assets take the narrow-row decile kernels
 static int64_t g_tune_dec_narrow_max = 16384;
 // wide rows on ids with decile means: 1 the chunked pass (deciles_chunked.hip: histogram /
-// load-balanced sweep / finish) | 0 the merged per-row pass (deciles.inc)
-static int g_tune_dec_chunked = 1;
+// load-balanced sweep / finish) | 0 the merged per-row pass (deciles.inc).  C4, same box,
+// interleaved: chunked 0.254 / 0.256 ms, merged 0.198 / 0.199 ms (profiles/r03/experiments/ab1_*)
+static int g_tune_dec_chunked = 0;
 
 extern "C" {
 

@@ -1303,6 +1303,12 @@ __global__ __launch_bounds__(256) void k_bootstrap_panel(const double* __restric
   }
 }
 
+void launch_bootstrap_index(hipStream_t st, int T_m, int B, int64_t b0, uint64_t seed,
+                            double p_new, int32_t* src) {
+  hipLaunchKernelGGL(k_bootstrap_index, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, T_m,
+                     B, b0, seed, p_new, src);
+}
+
 // ------------------------------------------------------------------------------- C ABI
 // 1: cohort sums through per-wave LDS atomics (k_cohort_lds) where they fit; 0: registers
 static int g_tune_cohort_lds = 1;

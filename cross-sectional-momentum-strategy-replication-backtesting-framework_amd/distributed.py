@@ -201,7 +201,7 @@ def _shard_ids(stages, P, month_start):
     """An id buffer for the fused shard pass when _wants_ids; None: rank from mom_J."""
     if not _wants_ids(stages, P):
         return None
-    return torch.empty((month_start.numel() - 1, N), dtype=torch.int16, device=P.device)
+    return torch.empty((month_start.numel() - 1, P.shape[1]), dtype=torch.int16, device=P.device)
 
 
 def virtual_shards(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, fused=False):

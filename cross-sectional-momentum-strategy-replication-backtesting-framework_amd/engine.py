@@ -511,6 +511,29 @@ class Engine:
                    float(mean_block), float(p0), _ptr(src), _ptr(PMb))
         return src, PMb
 
+    def boot_scan(self, R, B, Js, skip=1, b0=0, seed=5000, mean_block=6.0, p0=100.0,
+                  with_ids=True):
+        """csm_boot_scan: bootstrap(R, B, ...) and momentum_multi(with_ids) in one pass, the panel
+        never written -> (src [B][T_m], [(M, IDS)] per J (IDS None without ids), NR [T_m][B*N]
+        next_ret shared by every J, bad [1] int32).  M / IDS equal momentum_multi's on
+        bootstrap's panel bit for bit; NR equals each J's next_ret on every row J ranks unless
+        bad is set (include/csmom.h)."""
+        T_m, N = R.shape
+        _need(R, "R", torch.float64, (T_m, N), self.device)
+        Js = [int(J) for J in Js]
+        nJ = len(Js)
+        BN = B * N
+        src = self.empty((B, T_m), torch.int32)
+        Ms = [self.empty((T_m, BN)) for _ in Js]
+        IDS = [self.empty((T_m, BN), torch.int16) for _ in Js] if with_ids else None
+        NR = self.empty((T_m, BN))
+        bad = torch.empty(1, dtype=torch.int32, device=self.device)
+        arr = lambda ts: (ctypes.c_void_p * nJ)(*[t.data_ptr() for t in ts])
+        self._call("csm_boot_scan", _ptr(R), T_m, N, int(B), int(b0), ctypes.c_uint64(int(seed)),
+                   float(mean_block), float(p0), (ctypes.c_int32 * nJ)(*Js), nJ, int(skip),
+                   _ptr(src), arr(Ms), arr(IDS) if with_ids else None, _ptr(NR), _ptr(bad))
+        return src, list(zip(Ms, IDS if with_ids else [None] * nJ)), NR, bad
+
     def shard_summary(self, PM, J, skip, out=None, state=None):
         """csm_shard_summary (one pass over PM), or csm_shard_summary_state (short walks,
         the same record) when `state` from signal_shard is given."""

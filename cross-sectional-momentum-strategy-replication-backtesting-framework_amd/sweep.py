@@ -43,6 +43,14 @@ def _free_bytes(t: torch.Tensor) -> int:
     return 1 << 62
 
 
+def _free_bytes_dev(stages) -> int:
+    """_free_bytes of the stages' device (the Engine's), unbounded for host stages."""
+    dev = getattr(stages, "device", None)
+    if dev is None or getattr(dev, "type", "cpu") != "cuda":
+        return 1 << 62
+    return _free_bytes(torch.empty(0, device=dev))
+
+
 def strategy_grid(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12)):
     return [(int(J), int(K)) for J in Js for K in Ks]
 
@@ -104,6 +112,10 @@ class SweepConfig:
     # series has -- wider rows always get every decile).  False: every decile's overlapped
     # return
     legs_only: bool = True
+    # bootstrap sweeps (run_bootstrap): csm_boot_scan -- the panel generated in registers and
+    # scanned for every J at once, one next_ret panel for every J -- instead of csm_bootstrap ->
+    # multi-J scan (same labels and summary table, bit for bit)
+    boot_scan: bool = True
     extra: dict = field(default_factory=dict)
 
     @property
@@ -136,12 +148,14 @@ class SweepRunner:
         return out
 
     def _run_batch(self, PMb, B, W, ADV, SIG, flag):
+        return self._account(self._ranked(PMb, B), B, W, ADV, SIG, flag)
+
+    def _ranked(self, PMb, B):
+        """(J, L, NR) per J of the grid from the month prices of a batch: one J's ranking
+        panels live at a time."""
         c, st = self.cfg, self.st
         T_m, BN = PMb.shape
         N = BN // B
-        rows, series, summ = [], {}, {}
-        kw = dict(W=W, B=B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum, ADV=ADV,
-                  SIG=SIG, with_costs=c.costs)
         # multi_j_scan (wide batches): every J from one scan of PMb (csm_momentum_multi, the
         # register shift ring: C5 scan stage 30.6 -> 28.9 ms/step; bit-identical per J)
         # The multi-J scan keeps every J's M and NR live at once (2 * len(Js) [T_m][B*N] f64
@@ -170,7 +184,17 @@ class SweepRunner:
             else:
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS
-            L = L.reshape(T_m, BN)
+            yield J, L.reshape(T_m, BN), NR
+            del L, NR
+
+    def _account(self, ranked, B, W, ADV, SIG, flag):
+        """Portfolio accounting of every (J, K) from the (J, L, NR) of `ranked` -> summary
+        [B][S][F] and the per-strategy series {(J, K): PortfolioOut}."""
+        c, st = self.cfg, self.st
+        rows, series, summ = [], {}, {}
+        kw = dict(W=W, B=B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum, ADV=ADV,
+                  SIG=SIG, with_costs=c.costs)
+        for J, L, NR in ranked:
             if hasattr(st, "summary"):   # device path: one cohort pass for every K of this J,
                 if flag is not None:
                     kw2 = dict(kw, legs_only=True, need_full=flag)
@@ -195,6 +219,46 @@ class SweepRunner:
                 rows.append(summarize(out.LS, out.TURN, out.COST, out.NET))
         return torch.stack(rows, dim=1), series                  # [B][S][F]
 
+    def _boot_ok(self, T_m, N, B):
+        c = self.cfg
+        ids = c.decile_ids and hasattr(self.st, "deciles_ids") and N % 4 == 0
+        need = (8 + (2 if ids else 0)) * len(c.Js) * T_m * B * N + 8 * T_m * B * N
+        return (c.boot_scan and hasattr(self.st, "boot_scan") and N % 2 == 0
+                and 1 <= len(c.Js) <= 4 and max(c.Js) + c.skip <= 16
+                and need <= _free_bytes_dev(self.st) // 2)
+
+    def run_boot_batch(self, R_base, B, b0, seed=5000, mean_block=6.0):
+        """Bootstrap panels b0 .. b0+B-1 through csm_boot_scan (the panel generated in registers,
+        every J from one scan, one shared next_ret), then the decile pass and the accounting:
+        the summary table equals run_batch on csm_bootstrap's panel bit for bit.  A batch whose
+        generated prices leave the shared next_ret's domain (a price not finite and non-zero) is
+        rerun that way."""
+        c, st = self.cfg, self.st
+        T_m, N = R_base.shape
+        ids = c.decile_ids and hasattr(st, "deciles_ids") and N % 4 == 0
+        _, outs, NR, bad = st.boot_scan(R_base, B, c.Js, c.skip, b0=b0, seed=seed,
+                                        mean_block=mean_block, with_ids=ids)
+        legs = c.legs_only and hasattr(st, "summary")
+        flag = torch.zeros(1, dtype=torch.int32, device=NR.device) if legs else None
+        labels = []
+        for q, J in enumerate(c.Js):
+            (M, IDS), outs[q] = outs[q], None
+            if IDS is not None:
+                L, _, _, _ = st.deciles_ids(M.reshape(T_m * B, N), None, IDS.reshape(T_m * B, N),
+                                            c.n_bins)
+            else:
+                L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
+            del M, IDS
+            labels.append((J, L.reshape(T_m, B * N), NR))
+        out = self._account(labels, B, None, None, None, flag)
+        state = int((bad * 2 + (flag if legs else 0)).item())   # one sync for both flags
+        if state & 2:   # (never on finite returns) the materialised path
+            _, PMb = st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
+            return self.run_batch(PMb, B)
+        if state & 1:   # a panel lacks a leg's column: every decile (rare)
+            out = self._account(labels, B, None, None, None, None)
+        return out
+
     def run_bootstrap(self, R_base: torch.Tensor, n_panels: int, seed: int = 5000,
                       mean_block: float = 6.0, batch: int = 64):
         """C5: n_panels stationary-bootstrap panels of the base month returns, this rank's
@@ -206,8 +270,11 @@ class SweepRunner:
         mine = []
         for b0 in range(p0, p1, batch):
             B = min(batch, p1 - b0)
-            _, PMb = self.st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
-            summ, _ = self.run_batch(PMb, B)
+            if self._boot_ok(T_m, N, B):
+                summ, _ = self.run_boot_batch(R_base, B, b0, seed, mean_block)
+            else:
+                _, PMb = self.st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
+                summ, _ = self.run_batch(PMb, B)
             mine.append(summ)
         local = (torch.cat(mine, 0) if mine else
                  torch.empty((0, S, F), dtype=R_base.dtype, device=R_base.device))

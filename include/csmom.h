@@ -342,6 +342,22 @@ int csm_bootstrap(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t
                   uint64_t seed, double mean_block, double p0, int32_t* src, double* PMb);
 
 /*
+ * csm_bootstrap fused into csm_momentum_multi_ids for the bootstrap sweep (C5): the resampled
+ * prices are generated in registers from R (csm_bootstrap's arithmetic, never written), scanned
+ * for every J of Js in one pass, and written as M[nJ] (+ IDS[nJ], nullable) equal bit for bit to
+ * csm_momentum_multi_ids on csm_bootstrap's panel, plus ONE next_ret panel NR [T_m][B][N] shared
+ * by every J: equal to each J's next_ret on every row that J ranks (all the portfolio reads).
+ *   src [B][T_m] out (as csm_bootstrap);  M[q] / IDS[q] / NR [T_m][B][N] out;
+ *   bad: device int32, set to 1 when a generated price is not finite and non-zero (the shared
+ *   next_ret is then not exact: rerun the batch on the csm_bootstrap path).
+ * N even, 1 <= nJ <= 4, J + skip <= 16, 16-B aligned R / M / NR, 4-B aligned ids.
+ */
+int csm_boot_scan(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t B, int64_t b0,
+                  uint64_t seed, double mean_block, double p0, const int32_t* Js, int32_t nJ,
+                  int32_t skip, int32_t* src, double* const* M, uint16_t* const* IDS, double* NR,
+                  int32_t* bad);
+
+/*
  * Share-turnover features, replacing src/features.py:60-107 (compute_monthly_turnover) on the
  * dense monthly layout (rule T1): per present row adv = VOL / 21, shares = so[a] when not NaN
  * else trunc(mcap[a] / PM) when mcap != 0 and PM > 0 (NaN when that is not finite),

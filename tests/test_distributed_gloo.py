@@ -117,3 +117,22 @@ def test_date_shards_gloo(world, J, skip, fused):
         assert bits_equal(r[4], ref["EW"])
         assert np.array_equal(r[5], ref["CNT"])
         assert bits_equal(r[6], ref["LS"])
+
+
+def test_shard_id_buffer_shape():
+    """The fused shard pass's id buffer: [T_m][N] int16 exactly where csm_pipeline ranks from
+    ids (N % 4 == 0, rows wider than the narrow kernels), None elsewhere (host tensors suffice:
+    the helper only allocates)."""
+    from csmom.distributed import _shard_ids, _wants_ids
+    from csmom.engine import DEC_NARROW_MAX
+
+    class S:
+        shard_ids = True
+
+    ms = torch.arange(0, 13 * 21, 21, dtype=torch.int64)    # 12 months
+    wide = torch.zeros((1, DEC_NARROW_MAX + 4), dtype=torch.float64)
+    ids = _shard_ids(S(), wide, ms)
+    assert ids.shape == (12, DEC_NARROW_MAX + 4) and ids.dtype == torch.int16
+    assert _shard_ids(S(), torch.zeros((1, DEC_NARROW_MAX), dtype=torch.float64), ms) is None
+    assert _shard_ids(S(), torch.zeros((1, DEC_NARROW_MAX + 2), dtype=torch.float64), ms) is None
+    assert not _wants_ids(OracleStages(), wide)

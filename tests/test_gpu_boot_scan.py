@@ -1,0 +1,100 @@
+"""GPU: csm_boot_scan (csm_bootstrap fused into the multi-J scan for the bootstrap sweep, C5)
+against the materialised path it replaces -- csm_bootstrap -> csm_momentum_multi_ids -- and the
+oracle.  Bar: source months, mom_J and bucket ids of every J bit for bit; the shared next_ret
+equals each J's next_ret wherever that is defined and on every cell J labels; SweepRunner's
+summary table bit for bit with SweepConfig.boot_scan on and off (rules E1-E6,
+oracle/portfolio_oracle.py; the scan: src/features.py:44-52, run_demo.py:48)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits_equal
+from oracle import csmom_oracle as O
+from oracle import portfolio_oracle as PO
+
+pytestmark = pytest.mark.gpu
+
+
+def _base_returns(engine, N, T_d=2600, seed=11):
+    from csmom.synth import bday_calendar, make_device_panel
+    days, ms_h, _ = bday_calendar("2000-01-03", T_d)
+    pan = make_device_panel(N, days, ms_h, seed=seed, device="cuda:0")
+    PM, _ = engine.month_end(pan.P, pan.month_start)
+    R, _, _ = engine.momentum(PM, 12, 1, with_ret=True)
+    return R.contiguous()
+
+
+@pytest.mark.parametrize("N,B,b0,Js,skip,ids", [
+    (500, 6, 0, (3, 6, 9, 12), 1, True),      # the default grid: compile-time windows
+    (5000, 3, 999, (3, 6, 9, 12), 1, True),
+    (2000, 5, 37, (3, 12), 1, True),          # generic predicated windows
+    (800, 3, 1, (2, 7, 15), 1, False),
+    (640, 2, 3, (4,), 0, True),
+    (1202, 2, 8, (12, 3, 6, 9), 1, False),    # N % 4 != 0: no ids
+    (12, 3, 0, (3, 6, 9, 12), 1, True),
+])
+def test_boot_scan_equals_materialised(engine, N, B, b0, Js, skip, ids):
+    R = _base_returns(engine, N)
+    T_m = R.shape[0]
+    src, outs, NR, bad = engine.boot_scan(R, B, Js, skip, b0=b0, seed=5000, mean_block=6.0,
+                                          with_ids=ids)
+    assert int(bad.item()) == 0
+    ref_src = PO.bootstrap_indices(T_m, B, 5000, 6.0, b0=b0)
+    assert np.array_equal(src.cpu().numpy().astype(np.int64), ref_src)
+    _, PMb = engine.bootstrap(R, B, b0=b0, seed=5000, mean_block=6.0)
+    ref = engine.momentum_multi(PMb, Js, skip, with_ids=ids)
+    nr = NR.cpu().numpy()
+    for J, (M, IDS), r in zip(Js, outs, ref):
+        assert bits_equal(M.cpu().numpy(), r[0].cpu().numpy()), J
+        if ids:
+            assert torch.equal(IDS, r[2]), J
+        nrj = r[1].cpu().numpy()
+        ok = ~np.isnan(nrj)   # wherever J's next_ret is defined
+        assert bits_equal(nr[ok], nrj[ok]), J
+        on = ~np.isnan(M.cpu().numpy())   # every ranked cell
+        assert bits_equal(nr[on], nrj[on]), J
+    if N == 500:   # and the oracle's scan of the oracle's panel
+        pm = PO.bootstrap_panel(R.cpu().numpy(), ref_src).reshape(T_m, B * N)
+        for J, (M, _) in zip(Js, outs):
+            _, Mr, _, _ = O.momentum_scan(pm, J, skip)
+            assert bits_equal(M.cpu().numpy(), Mr), J
+
+
+def test_boot_scan_bad_prices_flagged(engine):
+    """A return of exactly -1 makes a price 0: outside the shared next_ret's domain, so the
+    kernel raises `bad`; SweepRunner then reruns the batch on the materialised path (the same
+    table as boot_scan off)."""
+    import csmom
+    R = _base_returns(engine, 400)
+    R[40, 7] = -1.0
+    _, _, _, bad = engine.boot_scan(R, 300, (3, 12), 1, b0=0, seed=5000, mean_block=6.0)
+    assert int(bad.item()) == 1   # some of 300 panels draw month 40
+    on = csmom.SweepConfig(Js=(3, 12), Ks=(3, 12), skip=1)
+    off = csmom.SweepConfig(Js=(3, 12), Ks=(3, 12), skip=1, boot_scan=False)
+    a = csmom.SweepRunner(engine, on).run_bootstrap(R, 300, batch=300).cpu().numpy()
+    b = csmom.SweepRunner(engine, off).run_bootstrap(R, 300, batch=300).cpu().numpy()
+    assert bits_equal(a, b)
+
+
+@pytest.mark.parametrize("legs,ids", [(True, True), (False, True), (True, False)])
+def test_sweep_runner_boot_scan_bit_identical(engine, legs, ids):
+    import csmom
+    R = _base_returns(engine, 1500, seed=12)
+    kw = dict(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, legs_only=legs, decile_ids=ids)
+    a = csmom.SweepRunner(engine, csmom.SweepConfig(**kw)).run_bootstrap(
+        R, 20, seed=5000, mean_block=6.0, batch=8).cpu().numpy()
+    b = csmom.SweepRunner(engine, csmom.SweepConfig(boot_scan=False, **kw)).run_bootstrap(
+        R, 20, seed=5000, mean_block=6.0, batch=8).cpu().numpy()
+    assert bits_equal(a, b)
+
+
+def test_boot_scan_rejects_bad_args(engine):
+    import csmom
+    R = _base_returns(engine, 500, T_d=700)
+    with pytest.raises(csmom.CsmError):
+        engine.boot_scan(R, 2, (3, 6, 9, 12, 3), 1)   # more than 4 J
+    with pytest.raises(csmom.CsmError):
+        engine.boot_scan(R, 2, (16,), 1)              # J + skip > 16
+    R2 = _base_returns(engine, 501, T_d=700)
+    with pytest.raises(csmom.CsmError):
+        engine.boot_scan(R2, 2, (3,), 1, with_ids=False)   # odd N

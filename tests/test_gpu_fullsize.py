@@ -155,7 +155,7 @@ def c5(engine):
     summ = csmom.SweepRunner(engine, cfg).run_bootstrap(R0, 100, seed=5000, mean_block=6.0,
                                                          batch=100)
     torch.cuda.synchronize()
-    return cfg, R0.cpu().numpy(), summ.cpu().numpy()
+    return cfg, R0, summ.cpu().numpy()
 
 
 def _oracle_panel_summary(cfg, R_h, b):
@@ -180,17 +180,28 @@ def _summary_rows(LS, TURN, COST, NET, freq=12.0):
 
 
 def test_c5_shape_and_finite(c5):
-    cfg, R_h, summ = c5
+    cfg, R0, summ = c5
     assert summ.shape == (100, 16, 7)
     assert np.isfinite(summ[..., :3]).all()
 
 
 @pytest.mark.parametrize("b", [0, 57, 99])
 def test_c5_sampled_panels_vs_oracle(c5, b):
-    cfg, R_h, summ = c5
-    ref = _oracle_panel_summary(cfg, R_h, b)
+    cfg, R0, summ = c5
+    ref = _oracle_panel_summary(cfg, R0.cpu().numpy(), b)
     got = summ[b]
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     assert np.array_equal(got[:, 0], ref[:, 0])                 # months per strategy
     m = ~np.isnan(ref)
     assert np.allclose(got[m], ref[m], rtol=1e-9, atol=1e-13), b
+
+
+def test_c5_boot_scan_equals_materialised(engine, c5):
+    """The bench path (csm_boot_scan, SweepConfig.boot_scan) against csm_bootstrap ->
+    multi-J scan -> decile pass on the whole C5 batch: the summary table bit for bit."""
+    import csmom
+    from dataclasses import replace
+    cfg, R0, summ = c5
+    off = csmom.SweepRunner(engine, replace(cfg, boot_scan=False)).run_bootstrap(
+        R0, 100, seed=5000, mean_block=6.0, batch=100).cpu().numpy()
+    assert bits_equal(summ, off)
