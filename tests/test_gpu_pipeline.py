@@ -241,8 +241,8 @@ def tune_wide(engine):
     def set_(chunked, merge):
         return lib.csm_tune(b"dec_chunked", chunked) == 0 and lib.csm_tune(b"dec_merge", merge) == 0
     yield set_
-    lib.csm_tune(b"dec_chunked", 1)
-    lib.csm_tune(b"dec_merge", 1)
+    lib.csm_tune(b"dec_chunked", 0)   # the library defaults: later tests compare bits with
+    lib.csm_tune(b"dec_merge", 1)     # fresh processes that run them
 
 
 @pytest.mark.parametrize("case", MERGE_CASES)
@@ -279,9 +279,9 @@ def test_deciles_ids_chunked_equals_merged_and_general(engine, tune_wide, case, 
     assert np.array_equal(np.isnan(a), np.isnan(rEW)) and max_rel(a, rEW) <= REL
 
 
-def test_pipeline_chunked_deciles_repeatable(engine):
-    """The chunked pass is deterministic (fixed summation order): two pipeline calls give the
-    same bits; labels equal the oracle's on every date."""
+def test_pipeline_deciles_repeatable(engine):
+    """The wide-row decile pass on ids is deterministic (fixed summation order): two pipeline
+    calls give the same bits; labels equal the oracle's on every date."""
     pan = _panel(N=36_000, T=900, seed=21)
     P, ms = _up(pan["P"]), _up(pan["month_start"])
     a = engine.pipeline(P, ms, 12, 1, 10)

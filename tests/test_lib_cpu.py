@@ -72,7 +72,7 @@ def test_tune_keys_documented_in_header_are_accepted():
     import csmom
     lib = csmom.load_library()
     cases = {b"signal_vec": ([1, 2], 2), b"signal_bwf": ([0, 1, 4], 0),
-             b"dec_merge": ([0, 1], 1), b"dec_narrow_max": ([0, 16384], 16384),
+             b"dec_merge": ([0, 1], 1), b"dec_chunked": ([0, 1], 0), b"dec_narrow_max": ([0, 16384], 16384),
              b"mj_reg": ([0, 1, 2], 2), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
              b"turn_gen_grid": ([1, 2048], 8192)}
