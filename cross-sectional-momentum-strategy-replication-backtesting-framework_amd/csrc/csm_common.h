@@ -30,8 +30,6 @@ struct csm_ctx {
   int n_cu;               // compute units of the device (decile kernel choice)
   int32_t* dec_flg;       // [dec_flg_n] rows the merged decile pass left to the general kernel
   int32_t dec_flg_n;      // (allocated at create, so a captured pipeline never allocates)
-  void* dws;              // context-owned workspace of the chunked wide-row decile pass
-  size_t dws_bytes;
   void* comm;             // RCCL communicator of csm_allgather_init (collective.hip), or NULL
   int comm_rank, comm_size;
 };
@@ -115,21 +113,6 @@ template <int NB>
 void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
                         int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg);
-
-// the general kernel alone for the rows flg marks (deciles_pre.hip)
-template <int NB>
-void launch_deciles_pre_flagged(int T_m, hipStream_t st, const double* M, const double* NR,
-                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                                int32_t* CNT, int32_t* NV, int64_t* tim, uint16_t* ids,
-                                int32_t* flg);
-
-// the chunked wide-row pass on ids (deciles_chunked.hip), NB in {2,3,4,5,10}: hist / sweep /
-// finish; rows it cannot take are flagged in flg for launch_deciles_pre_flagged
-size_t deciles_chunked_workspace(int T_m, int64_t N);
-template <int NB>
-void launch_deciles_chunked(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
-                            const QTab& q, int8_t* L, double* EW, int32_t* CNT, int32_t* NV,
-                            const uint16_t* ids, int32_t* flg, void* ws);
 
 // the same on narrow rows (deciles_npre.hip: 2048 buckets = the fixed map's ids >> 2)
 template <int NB>

@@ -1241,10 +1241,6 @@ static int g_tune_dec_merge = 1;
 static int g_tune_mj_reg = 2;
 // rows with at most this many assets take the narrow-row decile kernels
 static int64_t g_tune_dec_narrow_max = 16384;
-// wide rows on ids with decile means: 1 the chunked pass (deciles_chunked.hip: histogram /
-// load-balanced sweep / finish) | 0 the merged per-row pass (deciles.inc).  C4, same box,
-// interleaved: chunked 0.254 / 0.256 ms, merged 0.198 / 0.199 ms (profiles/r03/experiments/ab1_*)
-static int g_tune_dec_chunked = 0;
 
 extern "C" {
 
@@ -1262,7 +1258,6 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "dec_merge") && (value == 0 || value == 1)) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
-  if (!strcmp(key, "dec_chunked") && (value == 0 || value == 1)) { g_tune_dec_chunked = value; return CSM_OK; }
   return CSM_E_INVAL;
 }
 
@@ -1295,10 +1290,9 @@ int csm_create(int device, csm_ctx** out) {
 
 int csm_destroy(csm_ctx* ctx) {
   if (ctx) (void)csm_allgather_free(ctx);
-  if (ctx && (ctx->scratch || ctx->dec_flg || ctx->dws)) {
+  if (ctx && (ctx->scratch || ctx->dec_flg)) {
     (void)hipSetDevice(ctx->device);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
-    if (ctx->dws) (void)hipFree(ctx->dws);
     if (ctx->dec_flg) (void)hipFree(ctx->dec_flg);
   }
   free(ctx);
@@ -1611,30 +1605,6 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
       ctx->dec_flg_n = T_m;
     }
     flg = ctx->dec_flg;
-  }
-  // wide rows on ids with means: the chunked pass, the general kernel for the rows it flags
-  if (pre && NR && g_tune_dec_chunked && N > g_tune_dec_narrow_max &&
-      (n_bins == 2 || n_bins == 3 || n_bins == 4 || n_bins == 5 || n_bins == 10)) {
-    const size_t need = deciles_chunked_workspace(T_m, N);
-    if (ctx->dws_bytes < need) {   // grown on first use at a size (capture after a warm-up call)
-      if (ctx->dws) HIP_CHECK(ctx, hipFree(ctx->dws));
-      ctx->dws = nullptr;
-      ctx->dws_bytes = 0;
-      HIP_CHECK(ctx, hipMalloc(&ctx->dws, need));
-      ctx->dws_bytes = need;
-    }
-    int64_t* tm = g_dec_timing;
-    switch (n_bins) {
-#define DC_CASE(NB_)                                                                              \
-  case NB_:                                                                                       \
-    launch_deciles_chunked<NB_>(T_m, ctx->stream, M, NR, N, q, L, EW, CNT, NV, ids, flg, ctx->dws); \
-    launch_deciles_pre_flagged<NB_>(T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, tm, ids, flg); \
-    break;
-      DC_CASE(2) DC_CASE(3) DC_CASE(4) DC_CASE(5) DC_CASE(10)
-#undef DC_CASE
-    }
-    LAUNCH_CHECK(ctx, who);
-    return CSM_OK;
   }
   if (!NR) {
     launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, pre, flg);

@@ -26,22 +26,7 @@ void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* 
                      ids, flg);
 }
 
-// the general kernel alone, for the rows flg marks (the chunked pass's fallback rows)
-template <int NB>
-void launch_deciles_pre_flagged(int T_m, hipStream_t st, const double* M, const double* NR,
-                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
-                                int32_t* CNT, int32_t* NV, int64_t* tim, uint16_t* ids,
-                                int32_t* flg) {
-  hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, false>), dim3(T_m),
-                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
-                     ids, flg);
-}
-
 #define INST(NB)                                                                              \
-  template void launch_deciles_pre_flagged<NB>(int, hipStream_t, const double*, const double*, \
-                                               int64_t, int, const QTab&, int8_t*, double*,      \
-                                               int32_t*, int32_t*, int64_t*, uint16_t*,           \
-                                               int32_t*);                                        \
   template void launch_deciles_pre<NB>(int, hipStream_t, const double*, const double*, int64_t, \
                                        int, const QTab&, int8_t*, double*, int32_t*, int32_t*,  \
                                        int64_t*, uint16_t*, int32_t*);

@@ -233,52 +233,6 @@ def test_deciles_ids_merged_equals_general(engine, tune_merge, case):
     assert max_rel(a, rEW) <= REL
 
 
-@pytest.fixture
-def tune_wide(engine):
-    """(dec_chunked, dec_merge) setter for the wide-row decile paths on ids."""
-    lib = engine.lib
-
-    def set_(chunked, merge):
-        return lib.csm_tune(b"dec_chunked", chunked) == 0 and lib.csm_tune(b"dec_merge", merge) == 0
-    yield set_
-    lib.csm_tune(b"dec_chunked", 0)   # the library defaults: later tests compare bits with
-    lib.csm_tune(b"dec_merge", 1)     # fresh processes that run them
-
-
-@pytest.mark.parametrize("case", MERGE_CASES)
-@pytest.mark.parametrize("n_bins", [10, 3])
-def test_deciles_ids_chunked_equals_merged_and_general(engine, tune_wide, case, n_bins):
-    """The chunked wide-row pass (histogram / load-balanced sweep / finish; the general kernel
-    for the rows it flags) against the merged per-row pass and the general kernel alone: labels,
-    counts, ranked rows bit for bit, means within 1e-13, labels equal to the oracle's qcut and
-    counts / means to the oracle's portfolio.  Rows: the case, a momentum-like row, the case
-    with other next_ret, and 100,000 ranked cells followed by 100,000 NaN (a partial last
-    chunk of 3,392 cells)."""
-    rng = np.random.default_rng(11)
-    x = np.stack([_stress_row(case), _stress_row("lognormal_mild"), _stress_row(case),
-                  np.concatenate([_stress_row("lognormal_mild", n=100_000),
-                                  np.full(100_000, np.nan)])])
-    nr = rng.normal(0.01, 0.1, x.shape)
-    nr[rng.random(x.shape) < 0.03] = np.nan
-    M, NR, IDS = _up(x), _up(nr), _ids_dev(x)
-    got = {}
-    for mode in ((1, 1), (0, 1), (0, 0)):
-        assert tune_wide(*mode)
-        got[mode] = engine.deciles_ids(M, NR, IDS, n_bins, with_nv=True)
-    L1, EW1, C1, N1 = got[(1, 1)]
-    for mode in ((0, 1), (0, 0)):
-        L0, EW0, C0, N0 = got[mode]
-        assert torch.equal(L1, L0) and torch.equal(C1, C0) and torch.equal(N1, N0), (case, mode)
-        a, b = EW1.cpu().numpy(), EW0.cpu().numpy()
-        assert np.array_equal(np.isnan(a), np.isnan(b)) and max_rel(a, b) <= 1e-13, (case, mode)
-    refL = np.stack([_oracle_labels(x[r], n_bins) for r in range(x.shape[0])])
-    assert np.array_equal(L1.cpu().numpy(), refL), case
-    rEW, rCNT, _ = O.portfolio_ew(refL, nr, n_bins)
-    assert np.array_equal(C1.cpu().numpy(), rCNT)
-    a = EW1.cpu().numpy()
-    assert np.array_equal(np.isnan(a), np.isnan(rEW)) and max_rel(a, rEW) <= REL
-
-
 def test_pipeline_deciles_repeatable(engine):
     """The wide-row decile pass on ids is deterministic (fixed summation order): two pipeline
     calls give the same bits; labels equal the oracle's on every date."""

@@ -72,7 +72,7 @@ def test_tune_keys_documented_in_header_are_accepted():
     import csmom
     lib = csmom.load_library()
     cases = {b"signal_vec": ([1, 2], 2), b"signal_bwf": ([0, 1, 4], 0),
-             b"dec_merge": ([0, 1], 1), b"dec_chunked": ([0, 1], 0), b"dec_narrow_max": ([0, 16384], 16384),
+             b"dec_merge": ([0, 1], 1), b"dec_narrow_max": ([0, 16384], 16384),
              b"mj_reg": ([0, 1, 2], 2), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
              b"turn_gen_grid": ([1, 2048], 8192)}
@@ -87,7 +87,7 @@ def test_tune_keys_documented_in_header_are_accepted():
     for key in (b"dec_ablate", b"signal_store", b"signal_rr", b"signal_db", b"signal_mw",
                 b"dec_reg", b"dec_nreg", b"dec_wave_max", b"dec_ids", b"month_end_rows",
                 b"signal_nbuf", b"signal_bw", b"signal_bl", b"turn_list", b"sort_wave",
-                b"seg_stage2", b"turn_prep"):
+                b"seg_stage2", b"turn_prep", b"dec_chunked"):
         assert lib.csm_tune(key, 0) != 0 and lib.csm_tune(key, 1) != 0, key
     assert lib.csm_tune(None, 1) != 0
 
