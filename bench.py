@@ -69,8 +69,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-assets", type=int, default=150000)   # ~10-15 s of oracle time
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--no-ids", action="store_true",
-                    help="C4: decile pass streams mom_J (k_deciles) instead of the bucket ids the "
-                         "fused signal kernel writes (csm_signal_ids -> csm_deciles_ids)")
+                    help="C4 / C2: decile pass streams mom_J (k_deciles) instead of the bucket ids "
+                         "the signal kernel (C4: csm_signal_ids) or the time-chunked scan (C2: "
+                         "csm_momentum_chunked_ids) writes")
     ap.add_argument("--match-dates", type=int, default=0,
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -274,16 +275,22 @@ def main(argv=None):
     # fused + wide rows: the signal kernel writes each mom_J's fixed-map bucket id and the
     # decile pass histograms the 2-B ids instead of streaming mom_J three times
     use_ids = fused and pipe is None and not args.no_ids and N % 4 == 0 and N > 16384
-    IDS = eng.empty((T_m, N), torch.int16) if use_ids else None
     chunks = 1 if fused else eng.default_chunks(T_m, N, J, skip)
+    # narrow panels (C2): the time-chunked scan writes the bucket ids too and the narrow decile
+    # pass ranks from them (csm_momentum_chunked_ids -> csm_deciles_ids)
+    narrow_ids = (not fused and pipe is None and not args.no_ids and chunks > 1 and N % 4 == 0
+                  and N <= 16384)
+    IDS = eng.empty((T_m, N), torch.int16) if (use_ids or narrow_ids) else None
     ws = None
     if chunks > 1:
         nbytes = int(eng.lib.csm_momentum_chunked_workspace(T_m, N, J, skip, chunks))
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    scan_name = f"scan(k_momentum_chunked x{chunks})" if chunks > 1 else "scan(k_momentum)"
+    scan_name = (f"scan(k_momentum_chunked x{chunks}{' +ids' if narrow_ids else ''})" if chunks > 1
+                 else "scan(k_momentum)")
     stage_names = (["signal(k_signal+ids)", "deciles(k_deciles<ids>)", "long_short"] if use_ids else
                    ["signal(k_signal)", "deciles(k_deciles)", "long_short"] if fused else
-                   ["month_end(k_month_end)", scan_name, "deciles(k_deciles)", "long_short"])
+                   ["month_end(k_month_end)", scan_name,
+                    "deciles(k_deciles<ids>)" if narrow_ids else "deciles(k_deciles)", "long_short"])
     nst = len(stage_names) + 1
     step_events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst)]
                    for _ in range(args.steps)]
@@ -307,12 +314,13 @@ def main(argv=None):
             i += 1
             rec(ev[i])
             if chunks > 1:
-                eng.momentum_chunked(PM, J, skip, chunks=chunks, out=(None, M, NR), workspace=ws)
+                eng.momentum_chunked(PM, J, skip, chunks=chunks, out=(None, M, NR), workspace=ws,
+                                     ids=IDS if narrow_ids else None)
             else:
                 eng.momentum(PM, J, skip, out=(None, M, NR))
         i += 1
         rec(ev[i])
-        if use_ids:
+        if use_ids or narrow_ids:
             eng.deciles_ids(M, NR, IDS, nb, out=(L, EW, CNT, None))
         else:
             eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
@@ -450,6 +458,8 @@ def main(argv=None):
                              "k_month_end + carried k_momentum") if pipe is not None else
                             "fused k_signal (+ bucket ids) -> k_deciles on ids" if use_ids else
                             "fused k_signal" if fused else
+                            f"k_month_end + scan ({chunks} month chunks, + bucket ids) -> narrow "
+                            f"k_deciles on ids" if narrow_ids else
                             f"k_month_end + scan ({chunks} month chunks)"),
             "config": {"workload": cfg["name"] if args.assets is None and args.days is None
                        else f"custom: {N} assets x {T_d} bdays per GPU",

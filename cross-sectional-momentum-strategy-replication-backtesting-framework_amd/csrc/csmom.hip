@@ -304,7 +304,7 @@ __device__ __forceinline__ void momentum_body(
     double* ring_lds, const double* __restrict__ PM, int T_m, int64_t N, int J, int skip,
     double* __restrict__ R, double* __restrict__ M, double* __restrict__ NR,
     const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out);
+    double* __restrict__ carry_out, uint16_t* __restrict__ IDS = nullptr);
 
 __global__ __launch_bounds__(256) void k_momentum(
     const double* __restrict__ PM, int T_m, int64_t N, int J, int skip, double* __restrict__ R,
@@ -319,7 +319,8 @@ __global__ __launch_bounds__(256) void k_momentum(
 __global__ __launch_bounds__(256) void k_momentum_chunked(
     const double* __restrict__ PM, int T_m, int G, int64_t N, int J, int skip,
     double* __restrict__ R, double* __restrict__ M, double* __restrict__ NR,
-    const double* __restrict__ carry, const double* __restrict__ next_pm) {
+    const double* __restrict__ carry, const double* __restrict__ next_pm,
+    uint16_t* __restrict__ IDS) {
   extern __shared__ __attribute__((aligned(16))) double ring_lds[];
   const int g = blockIdx.y;
   int m0, m1;
@@ -328,14 +329,14 @@ __global__ __launch_bounds__(256) void k_momentum_chunked(
   const int64_t off = (int64_t)m0 * N;
   momentum_body(ring_lds, PM + off, m1 - m0, N, J, skip, R ? R + off : nullptr, M + off,
                 NR + off, g > 0 ? carry + (int64_t)g * (W + 2) * N : nullptr,
-                next_pm + (int64_t)g * N, nullptr);
+                next_pm + (int64_t)g * N, nullptr, IDS ? IDS + off : nullptr);
 }
 
 __device__ __forceinline__ void momentum_body(
     double* ring_lds, const double* __restrict__ PM, int T_m, int64_t N, int J, int skip,
     double* __restrict__ R, double* __restrict__ M, double* __restrict__ NR,
     const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out) {
+    double* __restrict__ carry_out, uint16_t* __restrict__ IDS) {
   const int W = J + skip;
   const int tid = threadIdx.x;
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + tid;
@@ -354,7 +355,8 @@ __device__ __forceinline__ void momentum_body(
     for (int j = 0; j < SCAN_CHUNK; ++j) {
       const int m = m0 + j;
       if (m >= T_m) break;
-      scan_step(s, buf[j], m, ring, RS, W, J, N, a, R, M, NR);
+      const double mom = scan_step(s, buf[j], m, ring, RS, W, J, N, a, R, M, NR);
+      if (IDS) IDS[(int64_t)m * N + a] = (uint16_t)csm_fid(mom);   // the decile pass's bucket id
     }
   }
   scan_finish(s, ring, RS, W, N, a, NR, next_pm, carry_out);
@@ -1780,9 +1782,9 @@ int64_t csm_momentum_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_
   return (int64_t)C * (S + (W + 2) + 1) * N * (int64_t)sizeof(double);
 }
 
-int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
-                         int32_t skip, int32_t C, double* R, double* M, double* NR,
-                         const double* next_pm, void* workspace) {
+static int momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                            int32_t skip, int32_t C, double* R, double* M, double* NR,
+                            const double* next_pm, void* workspace, uint16_t* IDS) {
   int r = prep(ctx);
   if (r) return r;
   if (!PM || !M || !NR || !workspace || N <= 0 || T_m < 0 || J < 1 || skip < 0 ||
@@ -1809,9 +1811,24 @@ int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_momentum_chunked, dim3((unsigned)((N + tpb - 1) / tpb), C), dim3(tpb), lds,
                      ctx->stream, PM, T_m, C, N, J, skip, R, M, NR, (const double*)carry,
-                     (const double*)npm);
+                     (const double*)npm, IDS);
   LAUNCH_CHECK(ctx, "k_momentum_chunked");
   return CSM_OK;
+}
+
+int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                         int32_t skip, int32_t C, double* R, double* M, double* NR,
+                         const double* next_pm, void* workspace) {
+  return momentum_chunked(ctx, PM, T_m, N, J, skip, C, R, M, NR, next_pm, workspace, nullptr);
+}
+
+int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                             int32_t skip, int32_t C, double* R, double* M, double* NR,
+                             const double* next_pm, uint16_t* ids, void* workspace) {
+  if (!ids || (N % 4) != 0 || ((uintptr_t)ids & 7u) != 0)
+    return set_err(ctx, CSM_E_INVAL, "csm_momentum_chunked_ids: ids must be non-NULL and 8-B "
+                   "aligned, N %% 4 == 0 (N=%lld)", (long long)N);
+  return momentum_chunked(ctx, PM, T_m, N, J, skip, C, R, M, NR, next_pm, workspace, ids);
 }
 
 }  // extern "C"

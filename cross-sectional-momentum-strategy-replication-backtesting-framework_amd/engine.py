@@ -213,8 +213,10 @@ class Engine:
         return int(max(1, min(want, T_m // max(2 * (J + skip + 1), 1), 256)))
 
     def momentum_chunked(self, PM, J=12, skip=1, chunks=None, with_ret=False, next_pm=None,
-                         out=None, workspace=None):
-        """csm_momentum_chunked: the scan split into `chunks` concurrent month ranges."""
+                         out=None, workspace=None, ids=None):
+        """csm_momentum_chunked: the scan split into `chunks` concurrent month ranges.  ids
+        (int16 [T_m][N], N % 4 == 0): also each mom_J's fixed-map bucket id
+        (csm_momentum_chunked_ids, for deciles_ids)."""
         T_m, N = PM.shape
         _need(PM, "PM", torch.float64, (T_m, N), self.device)
         C = self.default_chunks(T_m, N, J, skip) if chunks is None else int(chunks)
@@ -228,8 +230,13 @@ class Engine:
         nbytes = int(self.lib.csm_momentum_chunked_workspace(T_m, N, int(J), int(skip), C))
         if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
             workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
-        self._call("csm_momentum_chunked", _ptr(PM), T_m, N, int(J), int(skip), C, _ptr(R),
-                   _ptr(M), _ptr(NR), _ptr(next_pm), _ptr(workspace))
+        if ids is not None:
+            _need(ids, "ids", torch.int16, (T_m, N), self.device)
+            self._call("csm_momentum_chunked_ids", _ptr(PM), T_m, N, int(J), int(skip), C, _ptr(R),
+                       _ptr(M), _ptr(NR), _ptr(next_pm), _ptr(ids), _ptr(workspace))
+        else:
+            self._call("csm_momentum_chunked", _ptr(PM), T_m, N, int(J), int(skip), C, _ptr(R),
+                       _ptr(M), _ptr(NR), _ptr(next_pm), _ptr(workspace))
         return R, M, NR
 
     def signal(self, P, month_start, max_month_days, J=12, skip=1, with_pm=False,

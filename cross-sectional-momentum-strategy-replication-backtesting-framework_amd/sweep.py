@@ -22,6 +22,8 @@ oracle-backed adapter).
 """
 from __future__ import annotations
 
+import dataclasses
+import itertools
 from dataclasses import dataclass, field
 
 import torch
@@ -29,6 +31,7 @@ import torch.distributed as dist
 
 from .distributed import all_gather_stack
 
+JOIN_ROWS = 4096   # SweepConfig.join_js: batches below this many (month, panel) rows
 SUMMARY_FIELDS = ("months", "mean", "sharpe", "turnover", "cost", "net_mean", "net_sharpe")
 
 
@@ -116,6 +119,9 @@ class SweepConfig:
     # scanned for every J at once, one next_ret panel for every J -- instead of csm_bootstrap ->
     # multi-J scan (same labels and summary table, bit for bit)
     boot_scan: bool = True
+    # batches of fewer than JOIN_ROWS (month, panel) rows (C3's single panel): the Js' decile
+    # passes and accounting as one launch set over the Js side by side (_account_joined)
+    join_js: bool = True
     extra: dict = field(default_factory=dict)
 
     @property
@@ -150,12 +156,28 @@ class SweepRunner:
     def _run_batch(self, PMb, B, W, ADV, SIG, flag):
         return self._account(self._ranked(PMb, B), B, W, ADV, SIG, flag)
 
+    def _joined(self, T_m, B):
+        """Whether a batch this small runs its Js' decile passes and accounting as one launch
+        set over the Js side by side (join_js; every J's panels then live at once)."""
+        c = self.cfg
+        return (c.join_js and hasattr(self.st, "summary") and len(c.Js) > 1
+                and T_m * B < JOIN_ROWS)
+
     def _ranked(self, PMb, B):
         """(J, L, NR) per J of the grid from the month prices of a batch: one J's ranking
-        panels live at a time."""
+        panels live at a time (small joined batches: every J's scan, then one decile pass over
+        the Js' rows stacked)."""
         c, st = self.cfg, self.st
         T_m, BN = PMb.shape
         N = BN // B
+        if self._joined(T_m, B):
+            MN = [st.momentum(PMb, J, c.skip)[1:] for J in c.Js]
+            Lcat, _, _, _ = st.deciles(torch.cat([M.reshape(T_m * B, N) for M, _ in MN], 0), None,
+                                       c.n_bins)
+            R = T_m * B
+            for q, J in enumerate(c.Js):
+                yield J, Lcat[q * R:(q + 1) * R].reshape(T_m, BN), MN[q][1]
+            return
         # multi_j_scan (wide batches): every J from one scan of PMb (csm_momentum_multi, the
         # register shift ring: C5 scan stage 30.6 -> 28.9 ms/step; bit-identical per J)
         # The multi-J scan keeps every J's M and NR live at once (2 * len(Js) [T_m][B*N] f64
@@ -191,6 +213,11 @@ class SweepRunner:
         """Portfolio accounting of every (J, K) from the (J, L, NR) of `ranked` -> summary
         [B][S][F] and the per-strategy series {(J, K): PortfolioOut}."""
         c, st = self.cfg, self.st
+        ranked = iter(ranked)
+        first = next(ranked)
+        if self._joined(first[1].shape[0], B):
+            return self._account_joined([first] + list(ranked), B, W, ADV, SIG, flag)
+        ranked = itertools.chain([first], ranked)
         rows, series, summ = [], {}, {}
         kw = dict(W=W, B=B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum, ADV=ADV,
                   SIG=SIG, with_costs=c.costs)
@@ -217,6 +244,37 @@ class SweepRunner:
             else:
                 out = series[(J, K)]
                 rows.append(summarize(out.LS, out.TURN, out.COST, out.NET))
+        return torch.stack(rows, dim=1), series                  # [B][S][F]
+
+    def _account_joined(self, items, B, W, ADV, SIG, flag):
+        """_account for a small batch: the Js' labels / next_ret side by side as nJ * B panels
+        (panel q * B + b = J q's panel b; weights / ADV / vol repeated per J), one cohort pass, one
+        accounting launch set and one summary launch for the whole (J, K) grid instead of one per
+        J -- C3's single-panel rows are latency-bound per launch.  Same rules; partial sums in
+        another chunk order than per-J calls (within 1e-12)."""
+        c, st = self.cfg, self.st
+        nJ = len(items)
+        rep = lambda X: None if X is None else X.repeat(1, nJ)
+        L = torch.cat([it[1] for it in items], dim=1)
+        NR = torch.cat([it[2] for it in items], dim=1)
+        kw = dict(W=rep(W), B=nJ * B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum,
+                  ADV=rep(ADV), SIG=rep(SIG), with_costs=c.costs)
+        if flag is not None:
+            kw.update(legs_only=True, need_full=flag)
+        outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)
+        del L, NR
+        summ_all = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # [nK][nJ * B][F]
+        series, summ = {}, {}
+        cut = lambda X, sl: None if X is None else X[:, sl].contiguous()
+        for q, (J, _, _) in enumerate(items):
+            sl = slice(q * B, (q + 1) * B)
+            for k, K in enumerate(c.Ks):
+                o = outs[K]
+                series[(J, K)] = dataclasses.replace(o, PR=cut(o.PR, sl), LS=cut(o.LS, sl),
+                                                     TURN=cut(o.TURN, sl), COST=cut(o.COST, sl),
+                                                     NET=cut(o.NET, sl))
+                summ[(J, K)] = summ_all[k, sl]
+        rows = [summ[(J, K)] for (J, K) in c.strategies]
         return torch.stack(rows, dim=1), series                  # [B][S][F]
 
     def _boot_ok(self, T_m, N, B):

@@ -129,6 +129,14 @@ int64_t csm_momentum_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_
 int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
                          int32_t skip, int32_t C, double* R, double* M, double* NR,
                          const double* next_pm, void* workspace);
+/*
+ * csm_momentum_chunked that also writes ids[T_m][N] (uint16): each mom_J's fixed-map bucket id
+ * (as csm_signal_ids), so a narrow panel's decile pass (csm_deciles_ids, C2) reads 2-B ids and
+ * mom_J only near the bin edges.  Same R / M / NR bits.  N % 4 == 0, 8-B aligned ids.
+ */
+int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
+                             int32_t skip, int32_t C, double* R, double* M, double* NR,
+                             const double* next_pm, uint16_t* ids, void* workspace);
 
 /*
  * Fused month-end aggregation + scan in one pass over the daily panel (csm_month_end then

@@ -205,3 +205,23 @@ def test_c5_boot_scan_equals_materialised(engine, c5):
     off = csmom.SweepRunner(engine, replace(cfg, boot_scan=False)).run_bootstrap(
         R0, 100, seed=5000, mean_block=6.0, batch=100).cpu().numpy()
     assert bits_equal(summ, off)
+
+
+def test_c3_joined_js_equal_per_j(engine, c3):
+    """The bench's C3 step joins the four Js into one decile pass and one accounting launch set
+    (SweepConfig.join_js): the summary table equals the per-J launches' within 1e-12 (partial
+    sums in another chunk order), month counts exactly; the series keep their shapes."""
+    import csmom
+    from dataclasses import replace
+    PM, W, ADV = c3
+    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    a, sa = csmom.SweepRunner(engine, cfg).run_batch(PM, 1, W=W, ADV=ADV)
+    b, sb = csmom.SweepRunner(engine, replace(cfg, join_js=False)).run_batch(PM, 1, W=W, ADV=ADV)
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a[..., 0], b[..., 0])
+    assert max_rel(a, b) <= 1e-12
+    for key in cfg.strategies:
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            x, y = getattr(sa[key], f), getattr(sb[key], f)
+            assert x.shape == y.shape, (key, f)
+            assert max_rel(x.cpu().numpy(), y.cpu().numpy()) <= 1e-12, (key, f)

@@ -330,3 +330,47 @@ def test_sweep_batch_ids_equal_streaming(engine):
     a, _ = SweepRunner(engine, SweepConfig()).run_batch(PMb, B)
     b, _ = SweepRunner(engine, SweepConfig(decile_ids=False)).run_batch(PMb, B)
     assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+@pytest.mark.parametrize("N,T,J,skip,n_bins", [(5_000, 6_522, 12, 1, 10), (1_000, 2_600, 3, 0, 5),
+                                               (4_004, 1_500, 9, 2, 10)])
+def test_chunked_scan_ids_deciles(engine, N, T, J, skip, n_bins):
+    """The bench's C2 path (csm_month_end -> csm_momentum_chunked_ids -> csm_deciles_ids on
+    narrow rows -> csm_long_short) at C2 size: R / M / NR bit for bit the chunked scan's without
+    ids, ids = the fixed map of mom_J, labels / counts = the streaming decile pass's and the
+    oracle's qcut on every date, means and long-short within 1e-10 of the oracle's portfolio."""
+    pan = _panel(N=N, T=T, seed=23)
+    P, ms = _up(pan["P"]), _up(pan["month_start"])
+    PM, _ = engine.month_end(P, ms)
+    T_m = PM.shape[0]
+    C = engine.default_chunks(T_m, N, J, skip)
+    assert C > 1
+    IDS = engine.empty((T_m, N), torch.int16)
+    R1, M1, NR1 = engine.momentum_chunked(PM, J, skip, with_ret=True, ids=IDS)
+    R0, M0, NR0 = engine.momentum_chunked(PM, J, skip, with_ret=True)
+    for a, b in ((R1, R0), (M1, M0), (NR1, NR0)):
+        assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+    Mh = M1.cpu().numpy()
+    assert np.array_equal(IDS.cpu().numpy().view(np.uint16), fixed_ids(Mh))
+    L, EW, CNT, NV = engine.deciles_ids(M1, NR1, IDS, n_bins, with_nv=True)
+    Ls, EWs, CNTs, NVs = engine.deciles(M1, NR1, n_bins, with_nv=True)
+    assert torch.equal(L, Ls) and torch.equal(CNT, CNTs) and torch.equal(NV, NVs)
+    refL = O.assign_deciles(Mh, n_bins)
+    assert np.array_equal(L.cpu().numpy(), refL)
+    rEW, rCNT, _ = O.portfolio_ew(refL, NR1.cpu().numpy(), n_bins)
+    assert np.array_equal(CNT.cpu().numpy(), rCNT)
+
+    def same(a, b):   # NaN / inf cells equal (cent prices can reach 0: inf next_ret, as pandas)
+        fa, fb = np.isfinite(a), np.isfinite(b)
+        assert np.array_equal(fa, fb) and np.array_equal(a[~fa], b[~fb], equal_nan=True)
+        assert max_rel(a[fa], b[fb]) <= REL
+    same(EW.cpu().numpy(), rEW)
+    same(EWs.cpu().numpy(), rEW)
+    same(engine.long_short(EW, CNT).cpu().numpy(), O.long_short(rEW, rCNT))
+
+
+def test_chunked_scan_ids_rejects_bad_args(engine):
+    import csmom
+    PM = engine.empty((30, 1002))
+    with pytest.raises(csmom.CsmError):
+        engine.momentum_chunked(PM, 12, 1, chunks=2, ids=engine.empty((30, 1002), torch.int16))
