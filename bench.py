@@ -72,6 +72,8 @@ def parse(argv=None):
                     help="C4 / C2: decile pass streams mom_J (k_deciles) instead of the bucket ids "
                          "the signal kernel (C4: csm_signal_ids) or the time-chunked scan (C2: "
                          "csm_momentum_chunked_ids) writes")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="C2: month chunks of the time-chunked scan (0 = Engine.default_chunks)")
     ap.add_argument("--match-dates", type=int, default=0,
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -275,7 +277,7 @@ def main(argv=None):
     # fused + wide rows: the signal kernel writes each mom_J's fixed-map bucket id and the
     # decile pass histograms the 2-B ids instead of streaming mom_J three times
     use_ids = fused and pipe is None and not args.no_ids and N % 4 == 0 and N > 16384
-    chunks = 1 if fused else eng.default_chunks(T_m, N, J, skip)
+    chunks = 1 if fused else (args.chunks or eng.default_chunks(T_m, N, J, skip))
     # narrow panels (C2): the time-chunked scan writes the bucket ids too and the narrow decile
     # pass ranks from them (csm_momentum_chunked_ids -> csm_deciles_ids)
     narrow_ids = (not fused and pipe is None and not args.no_ids and chunks > 1 and N % 4 == 0

@@ -206,11 +206,13 @@ class Engine:
     @staticmethod
     def default_chunks(T_m, N, J=12, skip=1):
         """Chunks for the time-chunked scan: enough (chunk, asset) lanes to fill the chip
-        (~2^17), chunks no shorter than ~2 windows."""
+        (~2^17), chunks no shorter than one window (C2, 300 months: 20 chunks, scan 0.078 ->
+        0.068 ms against 10 chunks of two windows; the fold chains through any number of
+        earlier chunks, so the outputs are the same bits)."""
         if T_m <= 0:
             return 1
         want = max(1, -(-131072 // max(N, 1)))
-        return int(max(1, min(want, T_m // max(2 * (J + skip + 1), 1), 256)))
+        return int(max(1, min(want, T_m // max(J + skip + 1, 1), 256)))
 
     def momentum_chunked(self, PM, J=12, skip=1, chunks=None, with_ret=False, next_pm=None,
                          out=None, workspace=None, ids=None):
