@@ -93,6 +93,9 @@ def parse(argv=None):
     ap.add_argument("--no-boot-scan", action="store_true",
                     help="C5: csm_bootstrap -> multi-J scan on materialised panels instead of "
                          "csm_boot_scan (the panel generated in registers, one shared next_ret)")
+    ap.add_argument("--no-share-nr", action="store_true",
+                    help="C5: each J's cohort pass reads the shared next_ret itself instead of one "
+                         "pass staging each month's row for every J (csm_cohort_sums_js)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group: nccl (= RCCL over xGMI, one GPU per rank) or gloo "
                          "(device tensors staged through host memory; the 1-GPU rehearsal of the "
@@ -549,6 +552,12 @@ class TimedStages:
         return self._wrap("portfolio(k_cohort+k_turnover+k_overlap+k_ls)", per * T_m * BN,
                           self.eng.portfolio_multi, L, NR, n_bins, **k)
 
+    def portfolio_multi_js(self, Ls, NR, n_bins=10, **k):
+        T_m, BN = NR.shape   # algorithmic: each J's labels, the shared next_ret once
+        return self._wrap("portfolio(k_cohort+k_turnover+k_overlap+k_ls)",
+                          (1.0 * len(Ls) + 8.0) * T_m * BN, self.eng.portfolio_multi_js, Ls, NR,
+                          n_bins, **k)
+
     def summary(self, LS, TURN=None, COST=None, NET=None, **k):
         return self._wrap("summary(k_summary)", 8.0 * LS.numel() * (4 if TURN is not None else 1),
                           self.eng.summary, LS, TURN, COST, NET, **k)
@@ -622,7 +631,8 @@ def sweep_main(args):
     ts = TimedStages(eng)
     scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
                              multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids,
-                             legs_only=not args.full_deciles, boot_scan=not args.no_boot_scan)
+                             legs_only=not args.full_deciles, boot_scan=not args.no_boot_scan,
+                             share_nr=not args.no_share_nr)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":

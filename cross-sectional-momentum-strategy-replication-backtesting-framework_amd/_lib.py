@@ -72,6 +72,8 @@ SIGNATURES = {
                                                         _i32, _i32, _p, _f64, _f64, _f64, _p,
                                                         _p, _p, _p, _p, _p, _p, _p]),
     "csm_cohort_sums_legs": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i32, _i64, _i32, _i32, _p]),
+    "csm_cohort_sums_js": (ctypes.c_int, [_p, _i32, _p, _p, _i32, _i32, _i64, _i32, _i32, _i32,
+                                          _p]),
     "csm_portfolio_from_cohorts_legs": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
                                                        _i32, _i32, _p, _f64, _f64, _f64, _p,
                                                        _p, _p, _p, _p, _p, _p, _p, _p]),

@@ -459,18 +459,34 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
 // LEGS: the (age, leg) segments only (ND = 2 per age: deciles 0 and NB - 1); the partial
 // slots of the other deciles are not written (k_overlap skips them).
 #define SEG_STAGE_U 12
+// SJ: the label-sorted segments of up to SEG_MAXJ look-backs J that share one next_ret panel
+// (the bootstrap sweep's shared next_ret, csm_boot_scan): the month's return row is staged once
+// and the segments of every J walked from it -- one read of next_ret instead of one per J.  Each
+// J's sums come out bit for bit as from its own launch (same segments, groups and order).
+#define SEG_MAXJ 4
+struct SegJ {
+  const uint16_t* PERM[SEG_MAXJ];
+  const int32_t* OFF[SEG_MAXJ];
+  double* SWR[SEG_MAXJ];
+  double* SW[SEG_MAXJ];
+  int n;
+};
 template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
-    const double* __restrict__ NR, const uint16_t* __restrict__ PERM,
-    const int32_t* __restrict__ OFF, const double* __restrict__ WSRT, int T_m, int B, int64_t N,
-    int K, int C, int Cs, int xcd, int stage2, double* __restrict__ SWRp, double* __restrict__ SWp) {
+    const double* __restrict__ NR, SegJ sj, const double* __restrict__ WSRT, int T_m, int B,
+    int64_t N, int K, int C, int Cs, int xcd, int stage2) {
   constexpr int ND = LEGS ? 2 : NB;   // segments per age
   auto dec_of = [](int e) { return LEGS ? (e ? NB - 1 : 0) : e; };
   // the return row of month t (N values), NaN at slot N
   extern __shared__ __attribute__((aligned(16))) double rl[];
-  // then the K * (NB + 1) segment offsets, in the same dynamic allocation: sized to the launch,
-  // so a 5k-asset row's workgroup needs 40.5 KB and four fit a CU (a fixed 2 KB table made 3)
-  int32_t* offs = reinterpret_cast<int32_t*>(rl + N + 1);
+  // then each J's K * (NB + 1) segment offsets, in the same dynamic allocation: sized to the
+  // launch, so a 5k-asset row's workgroup needs 40.5 KB and four fit a CU (a fixed 2 KB table
+  // made 3)
+  // (LEGS: only the two legs' segment bounds, as u16 -- offsets are row positions <= SEG_MAXN:
+  // four per age, so four J's tables still leave four 5k-asset workgroups per CU)
+  typedef typename std::conditional<LEGS, uint16_t, int32_t>::type OffT;
+  constexpr int OE = LEGS ? 4 : NB + 1;   // offsets per age
+  OffT* offs_all = reinterpret_cast<OffT*>(rl + N + 1);
   int c = 0;
   int64_t tb;
   int t;
@@ -492,20 +508,24 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   const int tid = threadIdx.x;
   const int grp = tid / SEG_G, sl = tid % SEG_G;
   const int kmax = t + 1 < K ? t + 1 : K;
+  const int KD = K * OE;
   if (c >= Cs) {   // chunks beyond the Cs working ones only hold zeros
-    for (int g = tid; g < K * ND; g += PF_THREADS) {
-      const int k = g / ND, d = dec_of(g - k * ND);
-      const int64_t ob = ((tb * K + k) * C + c) * NB + d;
-      SWRp[ob] = 0.0;
-      SWp[ob] = 0.0;
-    }
+    for (int jq = 0; jq < sj.n; ++jq)
+      for (int g = tid; g < K * ND; g += PF_THREADS) {
+        const int k = g / ND, d = dec_of(g - k * ND);
+        const int64_t ob = ((tb * K + k) * C + c) * NB + d;
+        sj.SWR[jq][ob] = 0.0;
+        sj.SW[jq][ob] = 0.0;
+      }
     return;
   }
   const double* NRr = NR + tb * N;
-  for (int i = tid; i < kmax * (NB + 1); i += PF_THREADS) {
-    const int k = i / (NB + 1), e = i - k * (NB + 1);
-    offs[i] = OFF[(tb - (int64_t)k * B) * (NB + 1) + e];
-  }
+  for (int jq = 0; jq < sj.n; ++jq)
+    for (int i = tid; i < kmax * OE; i += PF_THREADS) {
+      const int k = i / OE, e = i - k * OE;
+      const int es = LEGS ? (e < 2 ? e : NB - 3 + e) : e;   // legs: bounds 0, 1, NB - 1, NB
+      offs_all[jq * KD + i] = (OffT)sj.OFF[jq][(tb - (int64_t)k * B) * (NB + 1) + es];
+    }
   if ((N & 1) == 0 && stage2) {
     // 16-B loads, up to SEG_STAGE_U per lane issued before any LDS store: a 6144-value row
     // in flight at once (row starts are 16-B aligned for even N)
@@ -531,6 +551,11 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   }
   if (tid == 0) rl[N] = qnan();
   __syncthreads();
+  for (int jq = 0; jq < sj.n; ++jq) {   // every J sharing the staged row, in order
+  const uint16_t* PERM = sj.PERM[jq];
+  const OffT* offs = offs_all + jq * KD;
+  double* __restrict__ SWRp = sj.SWR[jq];
+  double* __restrict__ SWp = sj.SW[jq];
   // working chunk c < Cs owns the segments g = c (mod Cs) whole and writes zeros for the
   // others (exact under the chunk-order sum of k_overlap); each working chunk stages the
   // whole return row, so Cs stays small
@@ -558,8 +583,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     q.ob = ((tb * K + k) * C + c) * NB + d;
     q.live = k < kmax;
     const int64_t srow = tb - (int64_t)(q.live ? k : 0) * B;
-    q.w0 = q.live ? offs[k * (NB + 1) + d] >> 2 : 0;
-    q.w1 = q.live ? offs[k * (NB + 1) + d + 1] >> 2 : 0;
+    const int oi = LEGS ? k * 4 + (d == 0 ? 0 : 2) : k * (NB + 1) + d;
+    q.w0 = q.live ? (int64_t)offs[oi] >> 2 : 0;
+    q.w1 = q.live ? (int64_t)offs[oi + 1] >> 2 : 0;
     q.P8 = (const uint64_t*)(PERM + srow * PS);
     q.Ws = VW ? WSRT + srow * PS : nullptr;
     return q;
@@ -630,6 +656,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     finish(q1, sr1, sw1, n1);
     if (two) finish(q2, sr2, sw2, n2);
   }
+  }   // J
 }
 
 // ------------------------------------------------------------------------------ E4, E5
@@ -1376,19 +1403,22 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     uint16_t* PERM = (uint16_t*)(segws + perm_b);
     int32_t* OFF = (int32_t*)(segws + off_b);
     double* WSRT = (double*)(segws + wsrt_b);
+    SegJ sj;
+    sj.n = 1;
+    sj.PERM[0] = PERM; sj.OFF[0] = OFF; sj.SWR[0] = SWRp; sj.SW[0] = SWp;
     const int xcd = pl.C == 1 && B >= 8;
     const int64_t rows = (int64_t)T_m * B;
     const int Cs = (int)std::min<int64_t>(pl.C, std::max<int64_t>(1, (1024 + rows - 1) / rows));
     const dim3 g1((unsigned)(T_m * B)),
         g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(pl.C * T_m * B));
-    const size_t lds = (size_t)(N + 1) * sizeof(double) + (size_t)K * (NB + 1) * sizeof(int32_t);
+    const size_t lds = (size_t)(N + 1) * sizeof(double) +
+                       (legs ? (size_t)K * 4 * sizeof(uint16_t) : (size_t)K * (NB + 1) * sizeof(int32_t));
     if (legs) {
       if (W) {
         hipLaunchKernelGGL((k_label_sort<NB, true, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N,
                            pl.C, PERM, OFF, WSRT, FWp);
-        hipLaunchKernelGGL((k_cohort_seg<NB, true, true>), g2, dim3(PF_THREADS), lds, st, NR,
-                           (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
-                           N, K, pl.C, Cs, xcd, 1, SWRp, SWp);
+        hipLaunchKernelGGL((k_cohort_seg<NB, true, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
+                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
       } else {
         if ((N & 3) == 0)   // one wave per row (C5's equal-weight legs)
           hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
@@ -1396,22 +1426,19 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
         else
           hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N,
                              pl.C, PERM, OFF, WSRT, FWp);
-        hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR,
-                           (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B,
-                           N, K, pl.C, Cs, xcd, 1, SWRp, SWp);
+        hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
+                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
       }
     } else if (W) {
       hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
-      hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR,
-                         (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, Cs, xcd, 1, SWRp, SWp);
+      hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
+                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
     } else {
       hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp);
-      hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR,
-                         (const uint16_t*)PERM, (const int32_t*)OFF, (const double*)WSRT, T_m, B, N,
-                         K, pl.C, Cs, xcd, 1, SWRp, SWp);
+      hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR, sj,
+                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
     }
     return;
   }
@@ -1431,6 +1458,48 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
   else
     hipLaunchKernelGGL((k_cohort<NB, false>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
                        pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp);
+}
+
+// Equal-weight cohort sums of nJ look-backs sharing one next_ret panel (segment path, one chunk
+// per row): each J's label sort, then ONE k_cohort_seg launch staging each month's return row
+// once for every J.  ws[q]: J q's workspace base; the partials land where launch_cohort puts
+// them, bit for bit the same values.
+template <int NB>
+static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int8_t* const* L,
+                             const double* NR, int T_m, int B, int64_t N, int K, char* const* ws,
+                             int64_t swr_b, int64_t sw_b, int64_t fw_b, int64_t perm_b,
+                             int64_t off_b, bool legs) {
+  const int xcd = B >= 8;
+  const dim3 g1((unsigned)(T_m * B)),
+      g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(T_m * B));
+  SegJ sj;
+  sj.n = nJ;
+  for (int q = 0; q < nJ; ++q) {
+    uint16_t* PERM = (uint16_t*)(ws[q] + perm_b);
+    int32_t* OFF = (int32_t*)(ws[q] + off_b);
+    double* FWp = (double*)(ws[q] + fw_b);
+    if (legs && (N & 3) == 0)
+      hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
+                         dim3(PF_THREADS), 0, st, L[q], N, 1, (int64_t)T_m * B, PERM, OFF, FWp);
+    else if (legs)
+      hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L[q],
+                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp);
+    else
+      hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L[q],
+                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp);
+    sj.PERM[q] = PERM;
+    sj.OFF[q] = OFF;
+    sj.SWR[q] = (double*)(ws[q] + swr_b);
+    sj.SW[q] = (double*)(ws[q] + sw_b);
+  }
+  const size_t lds = (size_t)(N + 1) * sizeof(double) +
+                     (legs ? (size_t)nJ * K * 4 * sizeof(uint16_t) : (size_t)nJ * K * (NB + 1) * sizeof(int32_t));
+  if (legs)
+    hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
+                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1);
+  else
+    hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR, sj,
+                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1);
 }
 
 // Workspace layout of the cohort partials for (T_m, B, N, n_bins, Kmax): SWRp, SWp
@@ -1533,6 +1602,54 @@ static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const do
 int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
                     int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, void* workspace) {
   return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, false);
+}
+
+int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const double* NR,
+                       int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
+                       int32_t legs, void* const* workspaces) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!L || !NR || !workspaces || nJ < 1 || nJ > SEG_MAXJ || T_m < 0 || B < 1 || N <= 0 ||
+      Kmax < 1 || Kmax > TO_MAXK || (int64_t)T_m * B > 0x7FFFFFFF)
+    return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_js: bad arguments (nJ=%d T_m=%d B=%d N=%lld "
+                   "Kmax=%d; 1 <= nJ <= %d)", nJ, T_m, B, (long long)N, Kmax, SEG_MAXJ);
+  if (legs && N > SEG_MAXN)
+    return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_js: legs on rows of <= %d assets (N=%lld)",
+                   SEG_MAXN, (long long)N);
+  for (int q = 0; q < nJ; ++q)
+    if (!L[q] || !workspaces[q])
+      return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_js: L[%d] or workspace[%d] is NULL", q, q);
+  if (T_m == 0) return CSM_OK;
+  const PfLayout lay = pf_layout(T_m, B, N, n_bins, Kmax);
+  // one staged return row for every J: the segment path with one chunk per row; otherwise the
+  // per-J passes (the same partials)
+  const bool shared = g_tune_cohort_seg && lay.seg && lay.p.C == 1 && !lay.p.kpar &&
+                      (legs ? nJ * Kmax * 4 : nJ * Kmax * (n_bins + 1)) <= SEG_MAXKD &&
+                      (n_bins == 2 || n_bins == 3 || n_bins == 4 || n_bins == 5 || n_bins == 10 ||
+                       n_bins == 20 || n_bins == 30);
+  if (!shared) {
+    for (int q = 0; q < nJ; ++q) {
+      r = cohort_sums(ctx, L[q], NR, nullptr, T_m, B, N, n_bins, Kmax, workspaces[q], legs != 0);
+      if (r) return r;
+    }
+    return CSM_OK;
+  }
+  hipStream_t st = ctx->stream;
+  char* ws[SEG_MAXJ];
+  for (int q = 0; q < nJ; ++q) ws[q] = (char*)workspaces[q];
+  switch (n_bins) {
+#define PJ_CASE(NBV) case NBV: launch_cohort_js<NBV>(st, lay.p, nJ, L, NR, T_m, B, N, Kmax, ws, lay.swr * 8, lay.sw * 8, lay.fw * 8, lay.perm_b, lay.off_b, legs != 0); break;
+    PJ_CASE(2) PJ_CASE(3) PJ_CASE(4) PJ_CASE(5) PJ_CASE(10) PJ_CASE(20) PJ_CASE(30)
+#undef PJ_CASE
+  }
+  LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret)");
+  for (int q = 0; q < nJ; ++q) {
+    double* w = (double*)workspaces[q];
+    hipLaunchKernelGGL(k_fw_fold, dim3((unsigned)((2 * lay.rows + 255) / 256)), dim3(256), 0, st,
+                       (const double*)(w + lay.fw), lay.rows, lay.p.C, w + lay.fwt);
+  }
+  LAUNCH_CHECK(ctx, "k_fw_fold");
+  return CSM_OK;
 }
 
 int csm_cohort_sums_legs(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,

@@ -433,7 +433,58 @@ class Engine:
             workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
         self._call("csm_cohort_sums_legs" if legs_only else "csm_cohort_sums", _ptr(L), _ptr(NR),
                    _ptr(W), T_m, int(B), N, int(n_bins), Kmax, _ptr(workspace))
+        flag = need_full
+        if legs_only and need_full is None:
+            flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        res, stacked = self._from_cohorts(L, W, T_m, B, N, n_bins, Ks, half_spread, k_impact,
+                                          aum, ADV, SIG, with_costs, workspace, legs_only, flag)
+        if legs_only and need_full is None and int(flag.item()):   # a panel lacks a leg's column
+            return self.portfolio_multi(L, NR, n_bins, Ks, W, B, half_spread, k_impact, aum,
+                                        ADV, SIG, with_costs, workspace, return_stacked)
+        if return_stacked:
+            return res, stacked
+        return res
+
+    def portfolio_multi_js(self, Ls, NR, n_bins=10, Ks=(1,), B=1, half_spread=0.0005,
+                           k_impact=0.1, aum=0.0, with_costs=True, legs_only=False, need_full=None):
+        """portfolio_multi (equal weights) for several label panels Ls that share ONE next_ret
+        panel NR (the bootstrap sweep's, boot_scan): one cohort pass for every J
+        (csm_cohort_sums_js: each month's return row read once), then each J's accounting.
+        Returns [(res, stacked)] per J, each equal bit for bit to portfolio_multi(L, NR, ...,
+        return_stacked=True)."""
+        T_m, BN = NR.shape
+        if B < 1 or BN % B:
+            raise ValueError(f"row width {BN} is not B={B} panels")
+        N = BN // B
+        _need(NR, "NR", torch.float64, (T_m, BN), self.device)
+        for L in Ls:
+            _need(L, "L", torch.int8, (T_m, BN), self.device)
+        Ks = [int(k) for k in Ks]
+        Kmax = max(Ks)
+        legs_only = bool(legs_only) and N <= LEGS_MAX_N
+        nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, N, int(n_bins), Kmax))
+        wss = [torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device) for _ in Ls]
+        nJ = len(Ls)
+        self._call("csm_cohort_sums_js", nJ, (ctypes.c_void_p * nJ)(*[L.data_ptr() for L in Ls]),
+                   _ptr(NR), T_m, int(B), N, int(n_bins), Kmax, 1 if legs_only else 0,
+                   (ctypes.c_void_p * nJ)(*[w.data_ptr() for w in wss]))
+        flag = need_full
+        if legs_only and need_full is None:
+            flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        outs = [self._from_cohorts(L, None, T_m, B, N, n_bins, Ks, half_spread, k_impact, aum,
+                                   None, None, with_costs, ws, legs_only, flag)
+                for L, ws in zip(Ls, wss)]
+        if legs_only and need_full is None and int(flag.item()):   # a panel lacks a leg's column
+            return self.portfolio_multi_js(Ls, NR, n_bins, Ks, B, half_spread, k_impact, aum,
+                                           with_costs, legs_only=False)
+        return outs
+
+    def _from_cohorts(self, L, W, T_m, B, N, n_bins, Ks, half_spread, k_impact, aum, ADV, SIG,
+                      with_costs, workspace, legs_only, need_full):
+        """The accounting half of portfolio_multi on a workspace holding the cohort sums ->
+        (res {K: PortfolioOut}, stacked PortfolioOut)."""
         nK = len(Ks)
+        Kmax = max(Ks)
         PR, LS = self.empty((nK, T_m, B, n_bins)), self.empty((nK, T_m, B))
         TURN = self.empty((nK, T_m, B)) if with_costs else None
         COST = self.empty((nK, T_m, B)) if with_costs else None
@@ -444,21 +495,13 @@ class Engine:
                 _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS), _ptr(TURN), _ptr(COST), _ptr(NET),
                 _ptr(workspace))
         if legs_only:
-            flag = (torch.zeros(1, dtype=torch.int32, device=self.device) if need_full is None
-                    else need_full)
-            self._call("csm_portfolio_from_cohorts_legs", *args, _ptr(flag))
-            if need_full is None and int(flag.item()):   # a panel lacks a leg's column
-                return self.portfolio_multi(L, NR, n_bins, Ks, W, B, half_spread, k_impact, aum,
-                                            ADV, SIG, with_costs, workspace, return_stacked)
+            self._call("csm_portfolio_from_cohorts_legs", *args, _ptr(need_full))
         else:
             self._call("csm_portfolio_from_cohorts_multi", *args)
         pick = lambda x, q: None if x is None else x[q]
         res = {K: PortfolioOut(PR=PR[q], LS=LS[q], TURN=pick(TURN, q), COST=pick(COST, q),
                                NET=pick(NET, q), legs_only=legs_only) for q, K in enumerate(Ks)}
-        if return_stacked:
-            return res, PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET,
-                                     legs_only=legs_only)
-        return res
+        return res, PortfolioOut(PR=PR, LS=LS, TURN=TURN, COST=COST, NET=NET, legs_only=legs_only)
 
     def summary(self, LS, TURN=None, COST=None, NET=None, freq=12.0):
         """csm_summary: [nS][B][7] (months, mean, Sharpe, turnover, cost, net mean, net

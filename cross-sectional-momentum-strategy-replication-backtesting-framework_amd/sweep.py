@@ -122,6 +122,9 @@ class SweepConfig:
     # batches of fewer than JOIN_ROWS (month, panel) rows (C3's single panel): the Js' decile
     # passes and accounting as one launch set over the Js side by side (_account_joined)
     join_js: bool = True
+    # bootstrap batches: the Js' cohort sums in one pass over the shared next_ret
+    # (csm_cohort_sums_js: each month's return row read once for every J; same table bit for bit)
+    share_nr: bool = True
     extra: dict = field(default_factory=dict)
 
     @property
@@ -308,14 +311,37 @@ class SweepRunner:
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS
             labels.append((J, L.reshape(T_m, B * N), NR))
-        out = self._account(labels, B, None, None, None, flag)
+        shared = (c.share_nr and hasattr(st, "portfolio_multi_js") and len(labels) > 1
+                  and not self._joined(T_m, B))
+        acc = self._account_shared if shared else self._account
+        out = acc(labels, B, None, None, None, flag)
         state = int((bad * 2 + (flag if legs else 0)).item())   # one sync for both flags
         if state & 2:   # (never on finite returns) the materialised path
             _, PMb = st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
             return self.run_batch(PMb, B)
         if state & 1:   # a panel lacks a leg's column: every decile (rare)
-            out = self._account(labels, B, None, None, None, None)
+            out = acc(labels, B, None, None, None, None)
         return out
+
+    def _account_shared(self, labels, B, W, ADV, SIG, flag):
+        """_account for Js that share one next_ret panel (bootstrap batches, no weights / ADV /
+        vol): one cohort pass for every J (portfolio_multi_js), then each J's accounting and
+        summary -- the same table and series as _account, bit for bit."""
+        c, st = self.cfg, self.st
+        assert W is None and ADV is None and SIG is None
+        NR = labels[0][2]
+        outs = st.portfolio_multi_js([L for _, L, _ in labels], NR, c.n_bins, Ks=c.Ks, B=B,
+                                     half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum,
+                                     with_costs=c.costs, legs_only=flag is not None,
+                                     need_full=flag)
+        series, summ = {}, {}
+        for (J, _, _), (res, stk) in zip(labels, outs):
+            summ_j = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)
+            for q, K in enumerate(c.Ks):
+                summ[(J, K)] = summ_j[q]
+                series[(J, K)] = res[K]
+        rows = [summ[(J, K)] for (J, K) in c.strategies]
+        return torch.stack(rows, dim=1), series                  # [B][S][F]
 
     def run_bootstrap(self, R_base: torch.Tensor, n_panels: int, seed: int = 5000,
                       mean_block: float = 6.0, batch: int = 64):

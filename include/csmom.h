@@ -318,6 +318,16 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
  * 0 by the caller) becomes 1 and the caller reruns the full csm_cohort_sums /
  * csm_portfolio_from_cohorts_multi.
  */
+/*
+ * Equal-weight cohort sums of nJ (<= 4) label panels L[q] that share one next_ret panel NR (the
+ * bootstrap sweep's shared next_ret, csm_boot_scan): each workspace[q] (csm_portfolio_workspace
+ * bytes) ends up as csm_cohort_sums(_legs)(L[q], NR, NULL, ..., workspace[q]) leaves it, bit for
+ * bit, but each month's return row is read once for every J (one launch) where the segment path
+ * applies.  legs: 1 = csm_cohort_sums_legs.  Then csm_portfolio_from_cohorts_* per J.
+ */
+int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const double* NR,
+                       int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
+                       int32_t legs, void* const* workspaces);
 int csm_cohort_sums_legs(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,
                          int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
                          void* workspace);

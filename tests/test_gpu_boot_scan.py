@@ -88,6 +88,61 @@ def test_sweep_runner_boot_scan_bit_identical(engine, legs, ids):
     assert bits_equal(a, b)
 
 
+@pytest.mark.parametrize("N,B,Js,Ks,n_bins,legs", [
+    (1500, 6, (3, 6, 9, 12), (3, 6, 9, 12), 10, True),    # C5's grid: legs, one shared pass
+    (1500, 6, (3, 6, 9, 12), (1, 3), 10, False),          # every decile, shared
+    (1500, 6, (3, 6, 9, 12), (3, 6, 9, 12), 10, False),   # offsets too many: per-J passes
+    (1202, 9, (3, 12), (2, 5), 5, True),                  # N % 4 != 0: the general label sort
+    (640, 3, (4,), (6,), 3, False),
+])
+def test_cohort_sums_js_equal_per_j(engine, N, B, Js, Ks, n_bins, legs):
+    """csm_cohort_sums_js (one staged next_ret row for every J) leaves every J's partials and
+    the accounting on them bit for bit as csm_cohort_sums(_legs) per J."""
+    R = _base_returns(engine, N, seed=13)
+    T_m = R.shape[0]
+    _, outs, NR, bad = engine.boot_scan(R, B, Js, 1, b0=5, with_ids=False)
+    assert int(bad.item()) == 0
+    Ls = []
+    for M, _ in outs:
+        L, _, _, _ = engine.deciles(M.reshape(T_m * B, N), None, n_bins)
+        Ls.append(L.reshape(T_m, B * N))
+    got = engine.portfolio_multi_js(Ls, NR, n_bins, Ks=Ks, B=B, legs_only=legs)
+    for L, (res, stk) in zip(Ls, got):
+        ref, rstk = engine.portfolio_multi(L, NR, n_bins, Ks=Ks, B=B, legs_only=legs,
+                                           return_stacked=True)
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(stk, f).cpu().numpy(), getattr(rstk, f).cpu().numpy()), f
+        assert stk.legs_only == rstk.legs_only
+
+
+@pytest.mark.parametrize("legs", [True, False])
+def test_sweep_runner_share_nr_bit_identical(engine, legs):
+    """A bootstrap batch above JOIN_ROWS rows takes the shared cohort pass (share_nr): the table
+    equals share_nr off and boot_scan off bit for bit."""
+    import csmom
+    from csmom.sweep import JOIN_ROWS
+    R = _base_returns(engine, 1000, seed=14)
+    batch = JOIN_ROWS // R.shape[0] + 2
+    kw = dict(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, legs_only=legs)
+    run = lambda **o: csmom.SweepRunner(engine, csmom.SweepConfig(**kw, **o)).run_bootstrap(
+        R, batch + 3, seed=5000, mean_block=6.0, batch=batch).cpu().numpy()
+    a = run()
+    assert bits_equal(a, run(share_nr=False))
+    assert bits_equal(a, run(boot_scan=False))
+
+
+def test_cohort_sums_js_rejects_bad_args(engine):
+    import csmom
+    R = _base_returns(engine, 500, T_d=700)
+    _, outs, NR, _ = engine.boot_scan(R, 2, (3, 6, 9, 12), 1, with_ids=False)
+    T_m = R.shape[0]
+    L = engine.deciles(outs[0][0].reshape(T_m * 2, 500), None, 10)[0].reshape(T_m, 1000)
+    with pytest.raises(csmom.CsmError):
+        engine.portfolio_multi_js([L] * 5, NR, 10, Ks=(3,), B=2)   # more than 4 J
+    with pytest.raises(ValueError):
+        engine.portfolio_multi_js([L], NR, 10, Ks=(3,), B=3)       # width not B panels
+
+
 def test_boot_scan_rejects_bad_args(engine):
     import csmom
     R = _base_returns(engine, 500, T_d=700)
