@@ -831,7 +831,9 @@ __device__ __forceinline__ void turnover_body(
     auto beq = [](uint32_t z) {   // 0x80 in each byte of z that is zero
       return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
     };
-    constexpr int TU = 2;
+    // (TU = 5: a 5k-asset row's label words all in flight in one trip; counts are exact
+    // integers, so the trip shape does not change a result)
+    constexpr int TU = 5;
     for (int64_t a = a0 + 4 * tid; a < a1; a += 4 * TU * PF_THREADS) {
       uint32_t w1[TU], w0[TU][TO_MAXQ];
 #pragma unroll
@@ -910,8 +912,8 @@ __device__ __forceinline__ void turnover_body(
     const int jmax = kq < t ? kq : t;   // ages with a formation month s = t - j >= 0
     if (CNT && kq <= 31) {
       // equal weight: a cell's leg memberships over the ages are two bit masks; the sums of
-      // inverse totals run over the set bits only (ascending age, the same order and values
-      // as the dense loop below)
+      // inverse totals take the member ages only (ascending age, the same order and values as
+      // the dense loop below)
       const uint32_t topw = (uint32_t)dtop * 0x01010101u;
       auto beq = [](uint32_t z) { return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u; };
       // ages whose cohort is empty on both legs contribute nothing (their bits add inv 0.0,
@@ -919,6 +921,12 @@ __device__ __forceinline__ void turnover_body(
       // their label loads are skipped (the first months of a panel: most ages are empty)
       uint32_t amask = 0;
       for (int j = 0; j <= jmax; ++j) amask |= (inv[0][j] != 0.0 || inv[1][j] != 0.0) ? 1u << j : 0u;
+      // the (q, leg) pairs whose windows are full (counts, like the steady rows) as a row-uniform
+      // bit mask, read once
+      uint32_t fullm = 0;
+      for (int q = 0; q < nq; ++q)
+        fullm |= (full[q][0] ? 1u : 0u) << (2 * q) | (full[q][1] ? 1u : 0u) << (2 * q + 1);
+      const bool anyfree = fullm != (1u << (2 * nq)) - 1u;
       for (int64_t a4 = a0 + cw * tid; a4 < a1 && amask; a4 += cw * PF_THREADS) {
         uint32_t mt4[4] = {0, 0, 0, 0}, mb4[4] = {0, 0, 0, 0};
         if (cw == 4) {
@@ -949,31 +957,59 @@ __device__ __forceinline__ void turnover_body(
             mb4[0] |= (lab == 0 ? 1u : 0u) << j;
           }
         }
+        const int ne = (int)(a1 - a4 < cw ? a1 - a4 : cw);   // cells of this lane's group
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (e >= cw || a4 + e >= a1) break;
-        const uint32_t mt = mt4[e], mb = mb4[e];
-        // (an age whose cohort is empty on a leg has inv 0 there: its bit adds 0.0)
-        const uint32_t e1 = (mt & 1u) | ((mb & 1u) << 16);
-        s1 += e1;
+        for (int e = 0; e < 4; ++e) {
+          if (e >= ne) break;
+          const uint32_t mt = mt4[e], mb = mb4[e];
+          const uint32_t e1 = (mt & 1u) | ((mb & 1u) << 16);
+          s1 += e1;
 #pragma unroll
-        for (int q = 0; q < TO_MAXQ; ++q) {
-          if (q >= nq) break;
-          const int K = ks.K[q];
-          const uint32_t e0 = ((mt >> K) & 1u) | (((mb >> K) & 1u) << 16);
-          s0[q] += e0;
-          sb[q] += e1 & e0;
-#pragma unroll
-          for (int li = 0; li < 2; ++li) {
-            if (full[q][li]) continue;
-            const uint32_t mm = li == 0 ? mt : mb;
-            double x1 = 0.0, x0 = 0.0;
-            for (uint32_t r = mm & ((1u << K) - 1u); r; r &= r - 1u) x1 += inv[li][__ffs(r) - 1];
-            for (uint32_t r = mm & (((2u << K) - 1u) & ~1u); r; r &= r - 1u) x0 += inv[li][__ffs(r) - 1];
-            charge(q, fabs(x1 * sk[q][li][0] - x0 * sk[q][li][1]), 0.0, 0.02);
+          for (int q = 0; q < TO_MAXQ; ++q) {
+            if (q >= nq) break;
+            const int K = ks.K[q];
+            const uint32_t e0 = ((mt >> K) & 1u) | (((mb >> K) & 1u) << 16);
+            s0[q] += e0;
+            sb[q] += e1 & e0;
           }
         }
-      }
+        if (anyfree) {
+          // legs that are not full: x1 = sum of inv over the member ages 0..K-1 (month t's
+          // window), x0 over 1..K (month t-1's), both ascending.  One walk over the ages for
+          // every (cell, leg) with inv read once per age (a broadcast): an age the cell is not
+          // in adds 0.0, exact for these non-negative sums, so x1 / x0 are the sums over the set
+          // bits in ascending order.  Pair q is charged at age K_q, cells and legs in order.
+          double sa[4][2], sz[4][2];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { sa[e][0] = sa[e][1] = 0.0; sz[e][0] = sz[e][1] = 0.0; }
+#pragma unroll 1
+          for (int j = 0; j <= kq; ++j) {
+            asm volatile("" ::: "memory");   // the factors are re-read (broadcasts), not held
+            const double iv0 = inv[0][j], iv1 = inv[1][j];
+            // pairs q with K_q == j are charged now: x1 = sa (ages < j), x0 = sz + v (ages 1..j)
+            uint32_t cq = 0;
+#pragma unroll
+            for (int q = 0; q < TO_MAXQ; ++q)
+              cq |= (q < nq && ks.K[q] == j) ? (3u << (2 * q)) & ~fullm : 0u;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+#pragma unroll
+              for (int li = 0; li < 2; ++li) {
+                const uint32_t mm = li == 0 ? mt4[e] : mb4[e];
+                const double v = ((mm >> j) & 1u) ? (li == 0 ? iv0 : iv1) : 0.0;
+                if (cq && e < ne) {
+#pragma unroll
+                  for (int q = 0; q < TO_MAXQ; ++q)
+                    if ((cq >> (2 * q + li)) & 1u)
+                      charge(q, fabs(sa[e][li] * sk[q][li][0] - (sz[e][li] + v) * sk[q][li][1]),
+                             0.0, 0.02);
+                }
+                sa[e][li] += v;
+                if (j >= 1) sz[e][li] += v;
+              }
+            }
+          }
+        }
       }
     } else if constexpr (!BM) {
     for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS)

@@ -290,9 +290,7 @@ class Engine:
     def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False):
         """csm_deciles_ids: deciles() from the ids of signal_ids / momentum_multi(with_ids=True)
         (same labels / counts).  Rows of <= 16384 assets take the narrow kernel (2048 buckets:
-        the fixed map's ids >> 2); wider rows with next_ret the chunked pass (histogram /
-        load-balanced sweep / finish);
-        needs N % 4 == 0."""
+        the fixed map's ids >> 2), wider rows the 8192-bucket merged pass; needs N % 4 == 0."""
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)
         _need(IDS, "IDS", torch.int16, (T_m, N), self.device)
