@@ -650,6 +650,17 @@ def sweep_main(args):
             ADV = W * turn_rate                # dollar ADV for the square-root impact
             summ, _ = runner.run_batch(PM, 1, W=W, ADV=ADV)
             return summ
+
+        flag_acc = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def step_defer():   # the same step with no device sync (hipGraph capture): the
+            ts.month_end(panel.P, panel.month_start, PM=PM)   # legs flag is accumulated and
+            W = PM.abs() * shares                             # read after the timed loop
+            ADV = W * turn_rate
+            summ, _, fl = runner.run_batch(PM, 1, W=W, ADV=ADV, defer=True)
+            if fl is not None:
+                flag_acc.add_(fl)
+            return summ
         units = float(N) * T_d * S * world
         unit = "asset-day-strategies/s"
         scaling = "weak"
@@ -669,18 +680,38 @@ def sweep_main(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ts.on = True
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    # C3 (one panel, ~40 launches a step): the step defers its legs-flag check (no device sync
+    # inside the step), so the host queues step k + 1 while step k runs; the accumulated flag is
+    # read after the timed loop and, if a panel ever lacked a leg's column, the loop is timed
+    # again with the synchronous step (which reruns such a panel with every decile)
+    defer = args.config == "c3"
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            o = fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0, o
+
+    # the timed loop runs uninstrumented (HIP events per stage call cost host time the
+    # launch-bound C3 step would pay); per-stage device times come from a second, untimed pass
+    if defer:
+        flag_acc.zero_()
+    elapsed, out = timed(step_defer if defer else step)
+    if defer and int(flag_acc.item()):
+        defer = False
+        elapsed, out = timed(step)
     elapsed = allreduce_host([elapsed], dist.ReduceOp.MAX if world > 1 else None, dev)[0]
+    ts.on = True
+    for _ in range(args.steps):
+        (step_defer if defer else step)()
+    torch.cuda.synchronize()
+    ts.on = False
     stages = ts.stage_report(args.steps)
     line = None
     if rank == 0:

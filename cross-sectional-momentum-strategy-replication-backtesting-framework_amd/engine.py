@@ -120,8 +120,10 @@ class Engine:
 
     # ------------------------------------------------------------------ plumbing
     def _bind_stream(self):
-        s = torch.cuda.current_stream(self.device)
-        self.lib.csm_set_stream(self.ctx, ctypes.c_void_p(s.cuda_stream))
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != getattr(self, "_bound_stream", None):   # one ctypes call per stream change
+            self.lib.csm_set_stream(self.ctx, ctypes.c_void_p(s))
+            self._bound_stream = s
 
     def _call(self, name, *args):
         self._bind_stream()

@@ -145,13 +145,19 @@ class SweepRunner:
         self.G = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
 
-    def run_batch(self, PMb: torch.Tensor, B: int, W=None, ADV=None, SIG=None):
+    def run_batch(self, PMb: torch.Tensor, B: int, W=None, ADV=None, SIG=None, defer=False):
         """PMb [T_m][B*N] month prices of B panels -> summary [B][S][F] and the per-strategy
-        long-short series {(J, K): PortfolioOut}."""
+        long-short series {(J, K): PortfolioOut} (small joined batches: strided views of the
+        joined outputs).  defer=True: no device sync -- returns
+        (summary, series, need_full) with need_full a device int32 [1] flag (None without the
+        legs-only accounting); when it reads non-zero the caller reruns with
+        SweepConfig(legs_only=False) (rare: a panel lacks a leg's column).  For hipGraph capture."""
         c = self.cfg
         legs = c.legs_only and hasattr(self.st, "summary")
         flag = torch.zeros(1, dtype=torch.int32, device=PMb.device) if legs else None
         out = self._run_batch(PMb, B, W, ADV, SIG, flag)
+        if defer:
+            return out[0], out[1], flag
         if legs and int(flag.item()):   # a panel lacks a leg's column: every decile (rare)
             out = self._run_batch(PMb, B, W, ADV, SIG, None)
         return out
@@ -268,7 +274,9 @@ class SweepRunner:
         del L, NR
         summ_all = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # [nK][nJ * B][F]
         series, summ = {}, {}
-        cut = lambda X, sl: None if X is None else X[:, sl].contiguous()
+        # per-(J, K) series as views of the joined outputs (a copy each was 80 small kernels a
+        # step on C3, host-bound)
+        cut = lambda X, sl: None if X is None else X[:, sl]
         for q, (J, _, _) in enumerate(items):
             sl = slice(q * B, (q + 1) * B)
             for k, K in enumerate(c.Ks):
@@ -294,12 +302,20 @@ class SweepRunner:
         the summary table equals run_batch on csm_bootstrap's panel bit for bit.  A batch whose
         generated prices leave the shared next_ret's domain (a price not finite and non-zero) is
         rerun that way."""
+        out, state, redo = self._boot_batch(R_base, B, b0, seed, mean_block)
+        v = int(state.item())
+        return redo(v) if v else out
+
+    def _boot_batch(self, R_base, B, b0, seed, mean_block, legs=True):
+        """run_boot_batch without the device sync: (out, state, redo) with state a device int32
+        [1] (bit 1: a generated price left the shared next_ret's domain, bit 0: a panel lacks a
+        leg's column) and redo(int(state)) the batch's final (summary, series)."""
         c, st = self.cfg, self.st
         T_m, N = R_base.shape
         ids = c.decile_ids and hasattr(st, "deciles_ids") and N % 4 == 0
         _, outs, NR, bad = st.boot_scan(R_base, B, c.Js, c.skip, b0=b0, seed=seed,
                                         mean_block=mean_block, with_ids=ids)
-        legs = c.legs_only and hasattr(st, "summary")
+        legs = legs and c.legs_only and hasattr(st, "summary")
         flag = torch.zeros(1, dtype=torch.int32, device=NR.device) if legs else None
         labels = []
         for q, J in enumerate(c.Js):
@@ -315,13 +331,20 @@ class SweepRunner:
                   and not self._joined(T_m, B))
         acc = self._account_shared if shared else self._account
         out = acc(labels, B, None, None, None, flag)
-        state = int((bad * 2 + (flag if legs else 0)).item())   # one sync for both flags
-        if state & 2:   # (never on finite returns) the materialised path
-            _, PMb = st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
-            return self.run_batch(PMb, B)
-        if state & 1:   # a panel lacks a leg's column: every decile (rare)
-            out = acc(labels, B, None, None, None, None)
-        return out
+        del labels, NR
+        state = bad * 2 + (flag if legs else 0)
+
+        def redo(v):   # holds no panel: a flagged batch is recomputed from its seed
+            if v & 2:   # (never on finite returns) the materialised path
+                _, PMb = st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
+                return self.run_batch(PMb, B)
+            if v & 1:   # a panel lacks a leg's column: every decile (rare)
+                o, st2, _ = self._boot_batch(R_base, B, b0, seed, mean_block, legs=False)
+                if int(st2.item()) & 2:
+                    return redo(2)
+                return o
+            return None
+        return out, state, redo
 
     def _account_shared(self, labels, B, W, ADV, SIG, flag):
         """_account for Js that share one next_ret panel (bootstrap batches, no weights / ADV /
@@ -351,15 +374,22 @@ class SweepRunner:
         T_m, N = R_base.shape
         p0, p1 = panel_partition(n_panels, self.G)[self.rank]
         S, F = len(self.cfg.strategies), len(SUMMARY_FIELDS)
-        mine = []
+        mine, pend = [], []
         for b0 in range(p0, p1, batch):
             B = min(batch, p1 - b0)
             if self._boot_ok(T_m, N, B):
-                summ, _ = self.run_boot_batch(R_base, B, b0, seed, mean_block)
+                # no sync per batch: the batches' flags are read once after the last launch
+                (summ, _), state, redo = self._boot_batch(R_base, B, b0, seed, mean_block)
+                pend.append((len(mine), state, redo))
             else:
                 _, PMb = self.st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
                 summ, _ = self.run_batch(PMb, B)
             mine.append(summ)
+        if pend:
+            states = torch.cat([s for _, s, _ in pend]).tolist()   # one sync for every batch
+            for (i, _, redo), v in zip(pend, states):
+                if v:   # rare: rerun that batch (materialised panel / every decile)
+                    mine[i] = redo(v)[0]
         local = (torch.cat(mine, 0) if mine else
                  torch.empty((0, S, F), dtype=R_base.dtype, device=R_base.device))
         if self.G == 1:

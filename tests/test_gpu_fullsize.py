@@ -136,8 +136,9 @@ def test_c3_sweep_runner_summary(engine, c3):
     summ, series = csmom.SweepRunner(engine, cfg).run_batch(PM, 1, W=W, ADV=ADV)
     assert tuple(summ.shape) == (1, 16, 7)
     for s, (J, K) in enumerate(cfg.strategies):
-        o = series[(J, K)]
-        one = engine.summary(o.LS, o.TURN, o.COST, o.NET)[0, 0]
+        o = series[(J, K)]   # (strided views of the joined outputs)
+        c = lambda x: x.contiguous()
+        one = engine.summary(c(o.LS), c(o.TURN), c(o.COST), c(o.NET))[0, 0]
         assert bits_equal(summ[0, s].cpu().numpy(), one.cpu().numpy()), (J, K)
 
 
