@@ -521,10 +521,10 @@ class TimedStages:
         T_m, N = PM.shape
         return self._wrap("scan(k_momentum*)", 24.0 * N * T_m, self.eng.momentum, PM, J, skip, **k)
 
-    def momentum_multi(self, PM, Js, skip=1, with_ids=False):
+    def momentum_multi(self, PM, Js, skip=1, with_ids=False, chunks=1):
         T_m, N = PM.shape
         return self._wrap("scan(k_momentum*)", (8.0 + 16.0 * len(Js)) * N * T_m,
-                          self.eng.momentum_multi, PM, Js, skip, with_ids=with_ids)
+                          self.eng.momentum_multi, PM, Js, skip, with_ids=with_ids, chunks=chunks)
 
     def default_chunks(self, *a, **k):
         return self.eng.default_chunks(*a, **k)

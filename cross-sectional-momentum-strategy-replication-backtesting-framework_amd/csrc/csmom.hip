@@ -530,10 +530,18 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg(const double* __rest
 // store: a wave moves 1 KiB per load / store instruction.  Same arithmetic per asset in the
 // same order as k_momentum_multi_reg: bit-identical outputs.  N even, 16-B aligned buffers.
 #define MJ2_CHUNK 8
-template <int RW>
+// CH (csm_momentum_multi_chunked): chunk blockIdx.y of G scans its month range [ms, me) from
+// the carry k_fold_carry rebuilt for max(J) (the last max(J) + skip factors, the month price
+// pff) plus each J's subset-ffilled price psf[g][q] -- a smaller J's ring is the newest J + skip
+// of the same factors -- and finishes its pending rows with npm[g] (the next chunk's first
+// present price), as k_momentum_chunked does per J: the same bits.
+template <int RW, bool CH = false>
 __global__ __launch_bounds__(256) void k_momentum_multi_reg2(const double* __restrict__ PM,
                                                              int T_m, int64_t N, int nJ, int skip,
-                                                             MJSet mj) {
+                                                             MJSet mj, int G = 1,
+                                                             const double* __restrict__ carry = nullptr,
+                                                             const double* __restrict__ npm = nullptr,
+                                                             const double* __restrict__ psf = nullptr) {
   const int64_t a0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (a0 >= N) return;
   const double NaN = qnan();
@@ -545,23 +553,50 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg2(const double* __res
   double pff[2] = {NaN, NaN};
   double psff[2][MJ_MAX];
   int prev[2][MJ_MAX], lo[MJ_MAX];
+  int Wmax = 0;
 #pragma unroll
   for (int q = 0; q < MJ_MAX; ++q) {
     psff[0][q] = psff[1][q] = NaN;
     prev[0][q] = prev[1][q] = -1;
     lo[q] = RW - mj.J[q] - skip;   // window = slots [lo, RW - skip)
+    if (q < nJ && mj.J[q] + skip > Wmax) Wmax = mj.J[q] + skip;
   }
   const int hi = RW - skip;
-  for (int m0 = 0; m0 < T_m; m0 += MJ2_CHUNK) {
+  int ms = 0, me = T_m;
+  const int g = CH ? (int)blockIdx.y : 0;
+  if (CH) {
+    chunk_range(T_m, G, g, ms, me);
+    if (g > 0) {   // the carried state: ring slots [RW - Wmax, RW) oldest first, pff, psff per J
+      const double* cg = carry + (int64_t)g * (Wmax + 2) * N + a0;
+#pragma unroll
+      for (int k = 0; k < RW; ++k)
+        if (k >= RW - Wmax) {
+          const double2 v = *reinterpret_cast<const double2*>(cg + (int64_t)(k - (RW - Wmax)) * N);
+          f[0][k] = v.x;
+          f[1][k] = v.y;
+        }
+      const double2 pv = *reinterpret_cast<const double2*>(cg + (int64_t)Wmax * N);
+      pff[0] = pv.x;
+      pff[1] = pv.y;
+#pragma unroll
+      for (int q = 0; q < MJ_MAX; ++q)
+        if (q < nJ) {
+          const double2 v = *reinterpret_cast<const double2*>(psf + ((int64_t)g * MJ_MAX + q) * N + a0);
+          psff[0][q] = v.x;
+          psff[1][q] = v.y;
+        }
+    }
+  }
+  for (int m0 = ms; m0 < me; m0 += MJ2_CHUNK) {
     double2 buf[MJ2_CHUNK];
 #pragma unroll
     for (int j = 0; j < MJ2_CHUNK; ++j)
-      buf[j] = (m0 + j < T_m) ? *reinterpret_cast<const double2*>(PM + (int64_t)(m0 + j) * N + a0)
-                              : make_double2(absent_val(), absent_val());
+      buf[j] = (m0 + j < me) ? *reinterpret_cast<const double2*>(PM + (int64_t)(m0 + j) * N + a0)
+                             : make_double2(absent_val(), absent_val());
 #pragma unroll
     for (int j = 0; j < MJ2_CHUNK; ++j) {
       const int m = m0 + j;
-      if (m >= T_m) break;
+      if (m >= me) break;
       const double xs[2] = {buf[j].x, buf[j].y};
       const int64_t o = (int64_t)m * N + a0;
       bool ab[2], xv[2];
@@ -617,11 +652,21 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg2(const double* __res
       }
     }
   }
+  // pending ranked rows: next_ret from the next chunk's first present price (CH), else NaN
 #pragma unroll
-  for (int q = 0; q < MJ_MAX; ++q)
+  for (int c = 0; c < 2; ++c) {
+    const double x = CH ? npm[(int64_t)g * N + a0 + c] : absent_val();
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-      if (q < nJ && prev[c][q] >= 0) mj.NR[q][(int64_t)prev[c][q] * N + a0 + c] = NaN;
+    for (int q = 0; q < MJ_MAX; ++q)
+      if (q < nJ && prev[c][q] >= 0) {
+        double nr = NaN;
+        if (CH && !is_absent(x)) {
+          const double ps_new = isnan_d(x) ? psff[c][q] : x;
+          nr = ps_new / psff[c][q] - 1.0;
+        }
+        mj.NR[q][(int64_t)prev[c][q] * N + a0 + c] = nr;
+      }
+  }
 }
 
 #define MJ_REG_W 16
@@ -943,11 +988,19 @@ __global__ __launch_bounds__(256) void k_shard_summary_chunked(const double* __r
   o[5 * N + a] = first;
 }
 
+// psq (csm_momentum_multi_chunked): also the subset-ffilled price of every look-back jq.J[q]
+// of the multi-J scan (the ranked subset starts J + skip present rows after the first valid
+// price), [G][MJ_MAX][N]; the ring and pff are J's own for J = max(J) and shared by the others.
+struct FoldJs {
+  int n;
+  int J[MJ_MAX];
+};
 __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ sm, int G, int g,
                                                     int64_t N, int J, int skip,
                                                     double* __restrict__ carry,
                                                     double* __restrict__ next_pm,
-                                                    const double* __restrict__ tail_pm) {
+                                                    const double* __restrict__ tail_pm,
+                                                    FoldJs jq, double* __restrict__ psq) {
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= N) return;
   const int W = J + skip, T = W + 1, S = SUM_SCALARS + T;
@@ -996,24 +1049,30 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
   double lastv = NaN;
   for (int h = g - 1; h >= 0; --h) if (!isnan_d(at(h, 3))) { lastv = at(h, 3); break; }
   carry[(int64_t)W * N + a] = lastv;
-  double psff = NaN;
   int64_t off = 0, f = -1;
   for (int h = 0; h < g; ++h) {
     if (f < 0 && at(h, 1) >= 0.0) f = off + (int64_t)at(h, 1);
     off += (int64_t)at(h, 0);
   }
-  if (f >= 0) {
-    int64_t offh = off;
-    for (int h = g - 1; h >= 0; --h) {
-      offh -= (int64_t)at(h, 0);
-      if (at(h, 2) >= 0.0) {
-        const int64_t li = offh + (int64_t)at(h, 2);
-        if (li >= f + J + skip) psff = at(h, 3);
-        break;
+  // last valid price among the ranked rows of look-back Jq (rows >= f + Jq + skip)
+  auto psff_of = [&](int Jq) {
+    double ps = NaN;
+    if (f >= 0) {
+      int64_t offh = off;
+      for (int h = g - 1; h >= 0; --h) {
+        offh -= (int64_t)at(h, 0);
+        if (at(h, 2) >= 0.0) {
+          const int64_t li = offh + (int64_t)at(h, 2);
+          if (li >= f + Jq + skip) ps = at(h, 3);
+          break;
+        }
       }
     }
-  }
-  carry[(int64_t)(W + 1) * N + a] = psff;
+    return ps;
+  };
+  carry[(int64_t)(W + 1) * N + a] = psff_of(J);
+  if (psq)
+    for (int q = 0; q < jq.n; ++q) psq[((int64_t)g * MJ_MAX + q) * N + a] = psff_of(jq.J[q]);
 }
 
 // =====================================================================================
@@ -1716,7 +1775,8 @@ int csm_fold_carry(csm_ctx* ctx, const double* summaries, int32_t G, int32_t g, 
     return set_err(ctx, CSM_E_INVAL, "csm_fold_carry: bad arguments");
   const unsigned blocks = (unsigned)((N + 255) / 256);
   hipLaunchKernelGGL(k_fold_carry, dim3(blocks), dim3(256), 0, ctx->stream, summaries, G, g, N, J,
-                     skip, carry, next_pm, (const double*)nullptr);
+                     skip, carry, next_pm, (const double*)nullptr, FoldJs{0, {0, 0, 0, 0}},
+                     (double*)nullptr);
   LAUNCH_CHECK(ctx, "k_fold_carry");
   return CSM_OK;
 }
@@ -1802,7 +1862,7 @@ static int momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t
                      T, C, sm);
   LAUNCH_CHECK(ctx, "k_shard_summary_chunked");
   hipLaunchKernelGGL(k_fold_carry, dim3(bx, C), dim3(256), 0, ctx->stream, (const double*)sm, C,
-                     -1, N, J, skip, carry, npm, next_pm);
+                     -1, N, J, skip, carry, npm, next_pm, FoldJs{0, {0, 0, 0, 0}}, (double*)nullptr);
   LAUNCH_CHECK(ctx, "k_fold_carry");
   const int tpb = W <= 64 ? SCAN_THREADS : 64;
   const size_t lds = (size_t)W * tpb * sizeof(double);
@@ -1820,6 +1880,71 @@ int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
                          int32_t skip, int32_t C, double* R, double* M, double* NR,
                          const double* next_pm, void* workspace) {
   return momentum_chunked(ctx, PM, T_m, N, J, skip, C, R, M, NR, next_pm, workspace, nullptr);
+}
+
+int64_t csm_momentum_multi_chunked_workspace(int32_t T_m, int64_t N, int32_t Jmax, int32_t skip,
+                                             int32_t C) {
+  if (N <= 0 || C < 1 || Jmax < 1 || skip < 0) return 0;
+  const int64_t W = Jmax + skip, S = SUM_SCALARS + W + 1;
+  (void)T_m;
+  return (int64_t)C * (S + (W + 2) + 1 + MJ_MAX) * N * (int64_t)sizeof(double);
+}
+
+int csm_momentum_multi_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                               const int32_t* Js, int32_t nJ, int32_t skip, int32_t C,
+                               double* const* M, double* const* NR, uint16_t* const* IDS,
+                               void* workspace) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!PM || !Js || !M || !NR || !workspace || N <= 0 || T_m < 0 || nJ < 1 || nJ > MJ_MAX ||
+      skip < 0 || C < 1 || C > 65535)
+    return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi_chunked: bad arguments (N=%lld T_m=%d "
+                   "nJ=%d C=%d; 1 <= nJ <= %d)", (long long)N, T_m, nJ, C, MJ_MAX);
+  MJSet mj;
+  FoldJs fj;
+  fj.n = nJ;
+  int Jmax = 0;
+  bool al = (N % 2) == 0 && aligned16(PM) && aligned16(workspace);
+  for (int q = 0; q < MJ_MAX; ++q) {
+    const bool on = q < nJ;
+    mj.J[q] = fj.J[q] = on ? Js[q] : 1;
+    mj.M[q] = on ? M[q] : nullptr;
+    mj.NR[q] = on ? NR[q] : nullptr;
+    mj.IDS[q] = (on && IDS) ? IDS[q] : nullptr;
+    if (on && (Js[q] < 1 || !M[q] || !NR[q] || (IDS && !IDS[q])))
+      return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi_chunked: J[%d]=%d or its outputs invalid",
+                     q, on ? Js[q] : 0);
+    if (on) {
+      al = al && aligned16(M[q]) && aligned16(NR[q]) && (!IDS || ((uintptr_t)IDS[q] & 3u) == 0);
+      Jmax = Js[q] > Jmax ? Js[q] : Jmax;
+    }
+  }
+  const int W = Jmax + skip;
+  if (W > MJ_REG_W || !al)
+    return set_err(ctx, CSM_E_INVAL, "csm_momentum_multi_chunked: needs max(J) + skip <= %d, even N "
+                   "and 16-B aligned PM / M / NR / workspace, 4-B aligned ids (W=%d N=%lld)",
+                   MJ_REG_W, W, (long long)N);
+  if (T_m == 0) return CSM_OK;
+  if (C > T_m) C = T_m;
+  const int T = W + 1, S = SUM_SCALARS + T;
+  double* sm = (double*)workspace;
+  double* carry = sm + (int64_t)C * S * N;
+  double* npm = carry + (int64_t)C * (W + 2) * N;
+  double* psq = npm + (int64_t)C * N;
+  const unsigned bx = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(k_shard_summary_chunked, dim3(bx, C), dim3(256), 0, ctx->stream, PM, T_m, N,
+                     T, C, sm);
+  LAUNCH_CHECK(ctx, "k_shard_summary_chunked");
+  hipLaunchKernelGGL(k_fold_carry, dim3(bx, C), dim3(256), 0, ctx->stream, (const double*)sm, C,
+                     -1, N, Jmax, skip, carry, npm, (const double*)nullptr, fj, psq);
+  LAUNCH_CHECK(ctx, "k_fold_carry");
+  const int tpb = SCAN_THREADS;
+  hipLaunchKernelGGL((k_momentum_multi_reg2<MJ_REG_W, true>),
+                     dim3((unsigned)((N / 2 + tpb - 1) / tpb), (unsigned)C), dim3(tpb), 0,
+                     ctx->stream, PM, T_m, N, nJ, skip, mj, C, (const double*)carry,
+                     (const double*)npm, (const double*)psq);
+  LAUNCH_CHECK(ctx, "k_momentum_multi_reg2 (chunked)");
+  return CSM_OK;
 }
 
 int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,

@@ -177,11 +177,13 @@ class Engine:
                    _ptr(NR), _ptr(carry), _ptr(next_pm), _ptr(carry_out))
         return R, M, NR
 
-    def momentum_multi(self, PM, Js, skip=1, with_ids=False):
+    def momentum_multi(self, PM, Js, skip=1, with_ids=False, chunks=1):
         """csm_momentum_multi: one scan for several look-backs (up to 4 per launch).  Returns
         [(M, NR)] in the order of Js, each equal bit for bit to momentum(PM, J, skip).
         with_ids (csm_momentum_multi_ids): [(M, NR, IDS)], IDS the fixed-map bucket id of
-        every mom_J (uint16 [T_m][N], read by deciles_ids on rows of any width)."""
+        every mom_J (uint16 [T_m][N], read by deciles_ids on rows of any width).  chunks > 1
+        (narrow panels; max(J) + skip <= 16, even N): the time-chunked multi-J scan
+        (csm_momentum_multi_chunked), the same bits."""
         T_m, N = PM.shape
         _need(PM, "PM", torch.float64, (T_m, N), self.device)
         Js = [int(J) for J in Js]
@@ -193,7 +195,17 @@ class Engine:
             jarr = (ctypes.c_int32 * len(grp))(*grp)
             marr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in Ms])
             narr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in NRs])
-            if with_ids:
+            if chunks > 1:
+                IDs = [self.empty((T_m, N), torch.int16) for _ in grp] if with_ids else None
+                iarr = ((ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in IDs])
+                        if with_ids else None)
+                nbytes = int(self.lib.csm_momentum_multi_chunked_workspace(
+                    T_m, N, max(grp), int(skip), int(chunks)))
+                ws = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
+                self._call("csm_momentum_multi_chunked", _ptr(PM), T_m, N, jarr, len(grp),
+                           int(skip), int(chunks), marr, narr, iarr, _ptr(ws))
+                outs.extend(zip(Ms, NRs, IDs) if with_ids else zip(Ms, NRs))
+            elif with_ids:
                 IDs = [self.empty((T_m, N), torch.int16) for _ in grp]
                 iarr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in IDs])
                 self._call("csm_momentum_multi_ids", _ptr(PM), T_m, N, jarr, len(grp), int(skip),

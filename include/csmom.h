@@ -137,6 +137,21 @@ int csm_momentum_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
 int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t J,
                              int32_t skip, int32_t C, double* R, double* M, double* NR,
                              const double* next_pm, uint16_t* ids, void* workspace);
+/*
+ * The two together for narrow sweep panels (C3): every look-back Js[q] (1 <= nJ <= 4, host
+ * arrays as csm_momentum_multi) from ONE time-chunked scan -- one summary / fold for max(J) (plus
+ * each J's subset-ffilled price) and one chunked multi-J scan instead of three launches per J.
+ * Each (M[q], NR[q], ids[q]) equals csm_momentum(PM, Js[q], skip) (+ its ids) bit for bit.  ids
+ * nullable (else a host array of device uint16 [T_m][N]).  max(J) + skip <= 16, even N, 16-B
+ * aligned PM / M / NR / workspace.  workspace: csm_momentum_multi_chunked_workspace(T_m, N,
+ * max(J), skip, C) bytes.
+ */
+int64_t csm_momentum_multi_chunked_workspace(int32_t T_m, int64_t N, int32_t Jmax, int32_t skip,
+                                             int32_t C);
+int csm_momentum_multi_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
+                               const int32_t* Js, int32_t nJ, int32_t skip, int32_t C,
+                               double* const* M, double* const* NR, uint16_t* const* ids,
+                               void* workspace);
 
 /*
  * Fused month-end aggregation + scan in one pass over the daily panel (csm_month_end then

@@ -374,3 +374,53 @@ def test_chunked_scan_ids_rejects_bad_args(engine):
     PM = engine.empty((30, 1002))
     with pytest.raises(csmom.CsmError):
         engine.momentum_chunked(PM, 12, 1, chunks=2, ids=engine.empty((30, 1002), torch.int16))
+
+
+@pytest.mark.parametrize("N,T,Js,skip,C", [
+    (5_000, 6_522, (3, 6, 9, 12), 1, None),   # C3's panel and grid, default chunks
+    (1_000, 2_600, (3, 12), 1, 7),
+    (2_002, 1_500, (2, 5, 9), 0, 3),          # N % 4 != 0: no ids
+    (640, 2_600, (12, 3, 6, 9), 1, 40),       # chunks shorter than a window
+    (1_000, 2_600, (4,), 2, 5),
+])
+def test_multi_chunked_scan_equals_per_j(engine, N, T, Js, skip, C):
+    """csm_momentum_multi_chunked (one summary / fold for max(J) + each J's subset-ffilled
+    price, one chunked multi-J scan): every J's M / NR bit for bit the plain per-J scan's, ids the
+    fixed map of mom_J."""
+    pan = _panel(N=N, T=T, seed=29)
+    PM, _ = engine.month_end(_up(pan["P"]), _up(pan["month_start"]))
+    T_m = PM.shape[0]
+    C = C or engine.default_chunks(T_m, N, max(Js), skip)
+    assert C > 1
+    ids = N % 4 == 0
+    outs = engine.momentum_multi(PM, Js, skip, with_ids=ids, chunks=C)
+    for J, o in zip(Js, outs):
+        _, M0, NR0 = engine.momentum(PM, J, skip, chunked="never")
+        assert bits_equal(o[0].cpu().numpy(), M0.cpu().numpy()), J
+        assert bits_equal(o[1].cpu().numpy(), NR0.cpu().numpy()), J
+        if ids:
+            assert np.array_equal(o[2].cpu().numpy().view(np.uint16), fixed_ids(M0.cpu().numpy())), J
+
+
+def test_joined_sweep_multi_chunked_equals_per_j(engine):
+    """A single-panel sweep batch (C3's joined path) ranks from the chunked multi-J scan's ids:
+    the summary table equals the per-J chunked scans' bit for bit."""
+    import csmom
+    pan = _panel(N=5_000, T=6_522, seed=31)
+    PM, _ = engine.month_end(_up(pan["P"]), _up(pan["month_start"]))
+    W = PM.abs() * 1e6
+    ADV = W * 0.01
+    kw = dict(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    a, _ = csmom.SweepRunner(engine, csmom.SweepConfig(**kw)).run_batch(PM, 1, W=W, ADV=ADV)
+    b, _ = csmom.SweepRunner(engine, csmom.SweepConfig(multi_j_scan=False, **kw)).run_batch(
+        PM, 1, W=W, ADV=ADV)
+    assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+def test_multi_chunked_scan_rejects_bad_args(engine):
+    import csmom
+    pm = _up(_month_panel(1_000, 120, 5))
+    with pytest.raises(csmom.CsmError):
+        engine.momentum_multi(pm, (16,), 1, chunks=4)             # max(J) + skip > 16
+    with pytest.raises(csmom.CsmError):
+        engine.momentum_multi(_up(_month_panel(999, 120, 5)), (3,), 1, chunks=4)   # odd N
