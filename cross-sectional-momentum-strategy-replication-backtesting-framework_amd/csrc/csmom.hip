@@ -535,7 +535,33 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg(const double* __rest
 // pff) plus each J's subset-ffilled price psf[g][q] -- a smaller J's ring is the newest J + skip
 // of the same factors -- and finishes its pending rows with npm[g] (the next chunk's first
 // present price), as k_momentum_chunked does per J: the same bits.
-template <int RW, bool CH = false>
+// FIX: the default grid J = 3, 6, 9, 12 (in that order), skip 1, in a 13-slot ring with
+// compile-time windows (J - 1 multiplies each, no predicated slots): the same oldest-first
+// product (1.0 * x == x), about half the code -- the predicated chunked kernel was 85 KB, past
+// the instruction cache.
+template <int RW, bool FIX>
+__device__ __forceinline__ double mj_window(const double (&f)[RW], int q, int lo, int hi) {
+  if constexpr (FIX) {
+    constexpr int Jq[4] = {3, 6, 9, 12};
+    double acc = 0.0;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      if (qq != q) continue;
+      const int l = RW - Jq[qq] - 1;
+      double a = f[l];
+#pragma unroll
+      for (int k = l + 1; k < RW - 1; ++k) a = a * f[k];
+      acc = a;
+    }
+    return acc;
+  }
+  double acc = 1.0;
+#pragma unroll
+  for (int k = 0; k < RW; ++k) acc = (k >= lo && k < hi) ? acc * f[k] : acc;
+  return acc;
+}
+
+template <int RW, bool CH = false, bool FIX = false>
 __global__ __launch_bounds__(256) void k_momentum_multi_reg2(const double* __restrict__ PM,
                                                              int T_m, int64_t N, int nJ, int skip,
                                                              MJSet mj, int G = 1,
@@ -620,9 +646,7 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg2(const double* __res
         bool wc[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          double acc = 1.0;
-#pragma unroll
-          for (int k = 0; k < RW; ++k) acc = (k >= lo[q] && k < hi) ? acc * f[c][k] : acc;
+          const double acc = mj_window<RW, FIX>(f[c], q, lo[q], hi);
           mom[c] = ab[c] ? NaN : acc - 1.0;
           const double ps_new = xv[c] ? xs[c] : psff[c][q];
           wp[c] = (!ab[c] && prev[c][q] >= 0) ? prev[c][q] : -1;
@@ -942,6 +966,9 @@ __global__ __launch_bounds__(256) void k_shard_summary(const double* __restrict_
   out[5 * N + a] = first;
 }
 
+// Month loads in batches of SUM_U (independent loads issued together; the walks below were
+// one dependent round trip per month: C2 summary 15.5 us, fold 28.3 us).
+#define SUM_U 8
 __global__ __launch_bounds__(256) void k_shard_summary_chunked(const double* __restrict__ PM,
                                                                int T_m, int64_t N, int T, int G,
                                                                double* __restrict__ out) {
@@ -957,28 +984,42 @@ __global__ __launch_bounds__(256) void k_shard_summary_chunked(const double* __r
   const int tm = m1 - m0;
   int64_t n = 0, fv = -1, lvi = -1;
   double lv = qnan(), first = absent_val();
-  for (int m = 0; m < tm; ++m) {
-    const double x = pm[(int64_t)m * N + a];
-    if (is_absent(x)) continue;
-    if (n == 0) first = x;
-    if (!isnan_d(x)) { if (fv < 0) fv = n; lvi = n; lv = x; }
-    ++n;
+  for (int mb = 0; mb < tm; mb += SUM_U) {
+    double xs[SUM_U];
+#pragma unroll
+    for (int u = 0; u < SUM_U; ++u) xs[u] = mb + u < tm ? pm[(int64_t)(mb + u) * N + a] : absent_val();
+#pragma unroll
+    for (int u = 0; u < SUM_U; ++u) {
+      const double x = xs[u];
+      if (is_absent(x)) continue;
+      if (n == 0) first = x;
+      if (!isnan_d(x)) { if (fv < 0) fv = n; lvi = n; lv = x; }
+      ++n;
+    }
   }
   const int k = (int)(n < T ? n : T);
   int got = 0;
   double head = qnan();
   for (int j = 0; j < T - k; ++j) o[(int64_t)(SUM_SCALARS + j) * N + a] = absent_val();
-  int m = tm - 1;
-  for (; m >= 0 && got < k; --m) {
-    const double x = pm[(int64_t)m * N + a];
-    if (is_absent(x)) continue;
-    o[(int64_t)(SUM_SCALARS + T - 1 - got) * N + a] = x;
-    ++got;
-  }
-  for (; m >= 0; --m) {
-    const double x = pm[(int64_t)m * N + a];
-    if (is_absent(x)) continue;
-    if (!isnan_d(x)) { head = x; break; }
+  // backward: the last k present rows (oldest first in the record), then the last valid price
+  // before them
+  bool done = false;
+  for (int mb = tm - 1; mb >= 0 && !done; mb -= SUM_U) {
+    double xs[SUM_U];
+#pragma unroll
+    for (int u = 0; u < SUM_U; ++u) xs[u] = mb - u >= 0 ? pm[(int64_t)(mb - u) * N + a] : absent_val();
+#pragma unroll
+    for (int u = 0; u < SUM_U; ++u) {
+      const double x = xs[u];
+      if (done || mb - u < 0 || is_absent(x)) continue;
+      if (got < k) {
+        o[(int64_t)(SUM_SCALARS + T - 1 - got) * N + a] = x;
+        ++got;
+      } else if (!isnan_d(x)) {
+        head = x;
+        done = true;
+      }
+    }
   }
   o[0 * N + a] = (double)n;
   o[1 * N + a] = (double)fv;
@@ -1037,22 +1078,40 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
   int c = 0;
   for (int h = src_h; h >= 0 && h < g; ++h) {
     const int kh = (int)fmin(at(h, 0), (double)T);
-    for (int j = (h == src_h) ? src_j : T - kh; j < T; ++j, ++c) {
-      const double x = at(h, SUM_SCALARS + j);
-      const double nx = isnan_d(x) ? pff : x;
-      const double ret = nx / pff - 1.0;
-      pff = nx;
-      const int pos = c - (nv - W);
-      if (pos >= 0) carry[(int64_t)pos * N + a] = 1.0 + ret;
+    for (int jb = (h == src_h) ? src_j : T - kh; jb < T; jb += SUM_U) {   // SUM_U rows in flight
+      double xs[SUM_U];
+#pragma unroll
+      for (int u = 0; u < SUM_U; ++u) xs[u] = jb + u < T ? at(h, SUM_SCALARS + jb + u) : NaN;
+#pragma unroll
+      for (int u = 0; u < SUM_U; ++u) {
+        if (jb + u >= T) break;
+        const double x = xs[u];
+        const double nx = isnan_d(x) ? pff : x;
+        const double ret = nx / pff - 1.0;
+        pff = nx;
+        const int pos = c - (nv - W);
+        if (pos >= 0) carry[(int64_t)pos * N + a] = 1.0 + ret;
+        ++c;
+      }
     }
   }
   double lastv = NaN;
   for (int h = g - 1; h >= 0; --h) if (!isnan_d(at(h, 3))) { lastv = at(h, 3); break; }
   carry[(int64_t)W * N + a] = lastv;
   int64_t off = 0, f = -1;
-  for (int h = 0; h < g; ++h) {
-    if (f < 0 && at(h, 1) >= 0.0) f = off + (int64_t)at(h, 1);
-    off += (int64_t)at(h, 0);
+  for (int hb = 0; hb < g; hb += SUM_U) {   // every earlier chunk's counts, SUM_U in flight
+    double cn[SUM_U], fi[SUM_U];
+#pragma unroll
+    for (int u = 0; u < SUM_U; ++u) {
+      cn[u] = hb + u < g ? at(hb + u, 0) : 0.0;
+      fi[u] = hb + u < g ? at(hb + u, 1) : -1.0;
+    }
+#pragma unroll
+    for (int u = 0; u < SUM_U; ++u) {
+      if (hb + u >= g) break;
+      if (f < 0 && fi[u] >= 0.0) f = off + (int64_t)fi[u];
+      off += (int64_t)cn[u];
+    }
   }
   // last valid price among the ranked rows of look-back Jq (rows >= f + Jq + skip)
   auto psff_of = [&](int Jq) {
@@ -1420,6 +1479,10 @@ int csm_momentum(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N, int32_t
   return CSM_OK;
 }
 
+static bool mj_fixed_grid(const int32_t* Js, int nJ, int skip) {
+  return nJ == 4 && skip == 1 && Js[0] == 3 && Js[1] == 6 && Js[2] == 9 && Js[3] == 12;
+}
+
 static int momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N,
                           const int32_t* Js, int32_t nJ, int32_t skip, double* const* M,
                           double* const* NR, uint16_t* const* IDS) {
@@ -1452,8 +1515,14 @@ static int momentum_multi(csm_ctx* ctx, const double* PM, int32_t T_m, int64_t N
   for (int q = 0; q < nJ; ++q)
     al = al && aligned16(M[q]) && aligned16(NR[q]) && (!IDS || ((uintptr_t)IDS[q] & 3u) == 0);
   if (W <= MJ_REG_W && g_tune_mj_reg == 2 && al) {   // register shift ring, two assets per lane
-    hipLaunchKernelGGL(k_momentum_multi_reg2<MJ_REG_W>, dim3((unsigned)((N / 2 + tpb - 1) / tpb)),
-                       dim3(tpb), 0, ctx->stream, PM, T_m, N, nJ, skip, mj);
+    if (mj_fixed_grid(Js, nJ, skip))
+      hipLaunchKernelGGL((k_momentum_multi_reg2<13, false, true>), dim3((unsigned)((N / 2 + tpb - 1) / tpb)),
+                         dim3(tpb), 0, ctx->stream, PM, T_m, N, nJ, skip, mj, 1,
+                         (const double*)nullptr, (const double*)nullptr, (const double*)nullptr);
+    else
+      hipLaunchKernelGGL(k_momentum_multi_reg2<MJ_REG_W>, dim3((unsigned)((N / 2 + tpb - 1) / tpb)),
+                         dim3(tpb), 0, ctx->stream, PM, T_m, N, nJ, skip, mj, 1,
+                         (const double*)nullptr, (const double*)nullptr, (const double*)nullptr);
     LAUNCH_CHECK(ctx, "k_momentum_multi_reg2");
     return CSM_OK;
   }
@@ -1939,10 +2008,15 @@ int csm_momentum_multi_chunked(csm_ctx* ctx, const double* PM, int32_t T_m, int6
                      -1, N, Jmax, skip, carry, npm, (const double*)nullptr, fj, psq);
   LAUNCH_CHECK(ctx, "k_fold_carry");
   const int tpb = SCAN_THREADS;
-  hipLaunchKernelGGL((k_momentum_multi_reg2<MJ_REG_W, true>),
-                     dim3((unsigned)((N / 2 + tpb - 1) / tpb), (unsigned)C), dim3(tpb), 0,
-                     ctx->stream, PM, T_m, N, nJ, skip, mj, C, (const double*)carry,
-                     (const double*)npm, (const double*)psq);
+  const dim3 grid((unsigned)((N / 2 + tpb - 1) / tpb), (unsigned)C);
+  if (mj_fixed_grid(Js, nJ, skip))
+    hipLaunchKernelGGL((k_momentum_multi_reg2<13, true, true>), grid, dim3(tpb), 0, ctx->stream,
+                       PM, T_m, N, nJ, skip, mj, C, (const double*)carry, (const double*)npm,
+                       (const double*)psq);
+  else
+    hipLaunchKernelGGL((k_momentum_multi_reg2<MJ_REG_W, true>), grid, dim3(tpb), 0, ctx->stream,
+                       PM, T_m, N, nJ, skip, mj, C, (const double*)carry, (const double*)npm,
+                       (const double*)psq);
   LAUNCH_CHECK(ctx, "k_momentum_multi_reg2 (chunked)");
   return CSM_OK;
 }
