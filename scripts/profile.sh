@@ -5,6 +5,8 @@
 #   2. two separate --pmc passes, FETCH_SIZE and WRITE_SIZE (they cannot share a pass);
 #   3. scripts/profile_summary.py (gfx950 FETCH_SIZE correction, per-instantiation keys).
 #   bash scripts/profile.sh <tag> <c4|c2|c3|c5> <git-head> [extra bench args]
+# NT / NP: step executions per traced / pmc run -- warmup + timed, + 1 graph replay and an
+# untimed eager stage pass of the same length (C2's hipGraph), + the sweeps' untimed stage pass
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG="${1:?tag}"
@@ -18,10 +20,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 case "$CFG" in
   c4) N=100000; TD=10000; RUN="--steps 20 --warmup 5"; NT=25; PMC="--steps 2 --warmup 1"; NP=3; STAGE="" ;;
-  c2) N=5000; TD=6522; RUN="--steps 50 --warmup 5"; NT=55; PMC="--steps 2 --warmup 1"; NP=3; STAGE="" ;;
-  c3) N=5000; TD=6522; RUN="--steps 10 --warmup 2"; NT=12; PMC="--steps 3 --warmup 1"; NP=4
+  c2) N=5000; TD=6522; RUN="--steps 50 --warmup 5"; NT=106; PMC="--steps 2 --warmup 1"; NP=6; STAGE="" ;;
+  c3) N=5000; TD=6522; RUN="--steps 10 --warmup 2"; NT=22; PMC="--steps 3 --warmup 1"; NP=7
       STAGE="--stage portfolio(k_cohort+k_turnover+k_overlap+k_ls)=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turn_prep,k_turnover,k_overlap,k_overlap_rows,k_ls" ;;
-  c5) N=5000; TD=6522; RUN="--steps 2 --warmup 1"; NT=3; PMC="--steps 1 --warmup 1"; NP=2
+  c5) N=5000; TD=6522; RUN="--steps 2 --warmup 1"; NT=5; PMC="--steps 1 --warmup 1"; NP=3
       STAGE="--stage portfolio(k_cohort+k_turnover+k_overlap+k_ls)=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turn_prep,k_turnover,k_overlap,k_overlap_rows,k_ls" ;;
   *) echo "unknown config $CFG"; exit 2 ;;
 esac
