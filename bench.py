@@ -429,7 +429,11 @@ def main(argv=None):
             achieved = alg_me / (me_ms * 1e-3) / 1e9
             # the committed rocprofv3 run of this exact bench command on this build (else null)
             prof = committed_profile(args.config, N, T_d, lib_sha256())
-            pk = (prof or {}).get("kernels", {}).get(kname, {})
+            # the profile keys kernels per template instantiation ("k_signal<23, 2, ...>"): the
+            # dominant kernel is the instantiation of kname with the most device time
+            kern = (prof or {}).get("kernels", {})
+            pk = max((v for k, v in kern.items() if k == kname or k.startswith(kname + "<")),
+                     key=lambda v: v.get("total_ns", 0.0), default={})
             traffic = pk.get("hbm_bytes_per_launch")
             roofline = dict(bound="hbm", kernel=kname, achieved=round(achieved, 1),
                             peak=HBM_PEAK_GBS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
