@@ -84,6 +84,10 @@ def monthly_replication(daily_df, shares_info=None, lookback_months=12, skip_mon
     ew = pd.DataFrame(np.where(cnt_h > 0, ew_h, np.nan)[rows][:, cols],
                       index=pd.DatetimeIndex(panel.month_end[rows], name="date"),
                       columns=pd.Index(np.nonzero(cols)[0].astype(np.float64), name="decile"))
+    if ew.empty:   # run_demo.py:55-58 (unreachable once a count is positive; mirrored)
+        if verbose:
+            print("No decile returns calculated.")
+        return None
     keep = ~np.isnan(ls_h)
     mom_ret = pd.Series(ls_h[keep], index=pd.DatetimeIndex(panel.month_end[keep], name="date"))
     if mom_ret.empty:
