@@ -91,10 +91,12 @@ struct QTab {
 // a row the map fits badly falls back to key-space refinement (slower, same labels).
 #define CSM_FB_BUCKETS 8192
 #define CSM_FB_NAN 0xFFFFu
+// (bits >> 42 of the double, taken as the high word's arithmetic >> 10: the same value with
+// 32-bit operations -- the id is computed for every asset-month by the VALU-bound scans)
 __device__ __forceinline__ int csm_fbucket(double x) {
-  const int64_t b = ((int64_t)__double_as_longlong(1.0 + x)) >> 42;
-  const int64_t k = b - (0x3FB0000000000000LL >> 42);   // bits(1/16) >> 42
-  return (int)(k < 0 ? 0 : (k > CSM_FB_BUCKETS - 1 ? CSM_FB_BUCKETS - 1 : k));
+  const int b = __double2hiint(1.0 + x) >> 10;
+  const int k = b - (0x3FB00000 >> 10);   // bits(1/16) >> 42
+  return k < 0 ? 0 : (k > CSM_FB_BUCKETS - 1 ? CSM_FB_BUCKETS - 1 : k);
 }
 __device__ __forceinline__ uint32_t csm_fid(double x) {
   return x == x ? (uint32_t)csm_fbucket(x) : CSM_FB_NAN;

@@ -91,7 +91,6 @@ __global__ __launch_bounds__(BS_THREADS, BS_MINB) void k_boot_scan(
   double pff[2] = {NaN, NaN};
   double prv[2] = {p0, p0};     // the bootstrap price product
   int pc[2] = {-1, -1};         // last present row (the shared next_ret)
-  double px[2] = {NaN, NaN};
   bool badp = false;
   int lo[BS_MAXJ];
 #pragma unroll
@@ -112,7 +111,7 @@ __global__ __launch_bounds__(BS_THREADS, BS_MINB) void k_boot_scan(
       const int m = m0 + j;
       if (m >= T_m) break;
       const double rs[2] = {rr[j].x, rr[j].y};
-      double xs[2];
+      double xs[2], rt[2];
       bool ab[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -126,8 +125,11 @@ __global__ __launch_bounds__(BS_THREADS, BS_MINB) void k_boot_scan(
         const double x = prv[c];
         xs[c] = x;
         if (!ab[c] && !(fabs(x) < INFINITY && x != 0.0)) badp = true;
-        // k_momentum_multi_reg2's step on a present x (never NaN here)
+        // k_momentum_multi_reg2's step on a present x (never NaN here).  pff and px (the shared
+        // next_ret's previous price) are both the last present price, so ret doubles as the
+        // pending row's next_ret below: one f64 division per asset-month instead of two
         const double ret = x / pff[c] - 1.0;
+        rt[c] = ret;
         pff[c] = ab[c] ? pff[c] : x;
 #pragma unroll
         for (int k = 0; k + 1 < RW; ++k) f[c][k] = ab[c] ? f[c][k] : f[c][k + 1];
@@ -140,8 +142,8 @@ __global__ __launch_bounds__(BS_THREADS, BS_MINB) void k_boot_scan(
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           wp[c] = (!ab[c] && pc[c] >= 0) ? pc[c] : -1;
-          vp[c] = xs[c] / px[c] - 1.0;
-          if (!ab[c]) { pc[c] = m; px[c] = xs[c]; }
+          vp[c] = rt[c];   // == x / (last present price) - 1.0
+          if (!ab[c]) pc[c] = m;
         }
         if (wp[0] >= 0 && wp[0] == wp[1]) {
           *reinterpret_cast<double2*>(NR + (int64_t)wp[0] * BN + c0) = make_double2(vp[0], vp[1]);
