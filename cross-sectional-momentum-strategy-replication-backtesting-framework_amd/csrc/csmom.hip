@@ -48,6 +48,40 @@ __global__ __launch_bounds__(256) void k_month_end(const double* __restrict__ P,
   const double* p = P + d0 * N + a;
   const double* v = WITH_VOL ? V + d0 * N + a : nullptr;
   int64_t d = d0;
+  // prices only, a business month (<= 24 rows): every row load in flight at once, one round
+  // trip per thread (the 8-row batches and the serial tail below took three to eight); rows
+  // past the month are ABSENT placeholders, which change nothing
+  constexpr int MD = 24;
+  if (!WITH_VOL && d1 - d0 <= MD) {
+    const int nd = (int)(d1 - d0);
+    double x[MD][VEC];
+#pragma unroll
+    for (int j = 0; j < MD; ++j) {
+      if (j < nd) {
+        if (VEC == 2) {
+          const double2 t = *reinterpret_cast<const double2*>(p + (int64_t)j * N);
+          x[j][0] = t.x; x[j][VEC - 1] = t.y;
+        } else {
+          x[j][0] = p[(int64_t)j * N];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[j][k] = absent_val();
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MD; ++j) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const bool pr = !is_absent(x[j][k]);
+        const bool ok = pr && !isnan_d(x[j][k]);
+        anyp[k] |= pr;
+        anyv[k] |= ok;
+        last[k] = ok ? x[j][k] : last[k];
+      }
+    }
+    d = d1;
+  }
   // 8-day batches keep 8 row loads in flight per lane before the dependent selects.
   for (; d + 8 <= d1; d += 8) {
     double x[8][VEC];
