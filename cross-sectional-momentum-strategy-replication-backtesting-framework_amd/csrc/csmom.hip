@@ -1084,34 +1084,48 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
     carry += (int64_t)g * (W + 2) * N;
     next_pm += (int64_t)g * N;
   }
+  const double NaN = qnan();
+  // the neighbours' scalars in one round trip (the walks below start there and usually end
+  // there): chunk g - 1's record scalars, chunk g + 1's count and first price
+  double pg[SUM_SCALARS], ng0 = 0.0, ng5 = absent_val();
+#pragma unroll
+  for (int r = 0; r < SUM_SCALARS; ++r) pg[r] = g > 0 ? sm[((int64_t)(g - 1) * S + r) * N + a] : NaN;
+  if (g + 1 < G) {
+    ng0 = sm[((int64_t)(g + 1) * S) * N + a];
+    ng5 = sm[((int64_t)(g + 1) * S + 5) * N + a];
+  }
   auto at = [&](int h, int r) -> double { return sm[((int64_t)h * S + r) * N + a]; };
+  // a record scalar (r a constant < SUM_SCALARS): chunk g - 1's from registers
+  auto sc = [&](int h, int r) -> double { return h == g - 1 ? pg[r] : at(h, r); };
   // next_pm: first present row after shard g
   double npm = (tail_pm && g == G - 1) ? tail_pm[a] : absent_val();
-  for (int h = g + 1; h < G; ++h) if (at(h, 0) > 0.0) { npm = at(h, 5); break; }
+  if (g + 1 < G) {
+    if (ng0 > 0.0) npm = ng5;
+    else for (int h = g + 2; h < G; ++h) if (sc(h, 0) > 0.0) { npm = sc(h, 5); break; }
+  }
   if (tail_pm && g < G - 1 && is_absent(npm)) npm = tail_pm[a];
   next_pm[a] = npm;
-  const double NaN = qnan();
   // locate the oldest of the last T present rows of shards < g
   int nv = 0, src_h = -1, src_j = -1;
   for (int h = g - 1; h >= 0 && nv < T; --h) {
-    const int k = (int)fmin(at(h, 0), (double)T);
+    const int k = (int)fmin(sc(h, 0), (double)T);
     const int take = k < T - nv ? k : T - nv;
     if (take > 0) { nv += take; src_h = h; src_j = T - take; }
   }
   double pff_before = NaN;
   if (nv > 0) {
-    const int k0 = (int)fmin(at(src_h, 0), (double)T);
+    const int k0 = (int)fmin(sc(src_h, 0), (double)T);
     for (int j = src_j - 1; j > T - 1 - k0; --j) { const double x = at(src_h, SUM_SCALARS + j); if (!isnan_d(x)) { pff_before = x; break; } }
-    if (isnan_d(pff_before)) pff_before = at(src_h, 4);
+    if (isnan_d(pff_before)) pff_before = sc(src_h, 4);
     if (isnan_d(pff_before))
-      for (int h = src_h - 1; h >= 0; --h) if (!isnan_d(at(h, 3))) { pff_before = at(h, 3); break; }
+      for (int h = src_h - 1; h >= 0; --h) if (!isnan_d(sc(h, 3))) { pff_before = sc(h, 3); break; }
   }
   // replay oldest -> newest; the newest W rets become the ring (as factors fl(1+ret))
   double pff = pff_before;
   for (int k = 0; k < W; ++k) carry[(int64_t)k * N + a] = NaN;
   int c = 0;
   for (int h = src_h; h >= 0 && h < g; ++h) {
-    const int kh = (int)fmin(at(h, 0), (double)T);
+    const int kh = (int)fmin(sc(h, 0), (double)T);
     for (int jb = (h == src_h) ? src_j : T - kh; jb < T; jb += SUM_U) {   // SUM_U rows in flight
       double xs[SUM_U];
 #pragma unroll
@@ -1130,7 +1144,7 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
     }
   }
   double lastv = NaN;
-  for (int h = g - 1; h >= 0; --h) if (!isnan_d(at(h, 3))) { lastv = at(h, 3); break; }
+  for (int h = g - 1; h >= 0; --h) if (!isnan_d(sc(h, 3))) { lastv = sc(h, 3); break; }
   carry[(int64_t)W * N + a] = lastv;
   int64_t off = 0, f = -1;
   for (int hb = 0; hb < g; hb += SUM_U) {   // every earlier chunk's counts, SUM_U in flight
@@ -1153,10 +1167,10 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
     if (f >= 0) {
       int64_t offh = off;
       for (int h = g - 1; h >= 0; --h) {
-        offh -= (int64_t)at(h, 0);
-        if (at(h, 2) >= 0.0) {
-          const int64_t li = offh + (int64_t)at(h, 2);
-          if (li >= f + Jq + skip) ps = at(h, 3);
+        offh -= (int64_t)sc(h, 0);
+        if (sc(h, 2) >= 0.0) {
+          const int64_t li = offh + (int64_t)sc(h, 2);
+          if (li >= f + Jq + skip) ps = sc(h, 3);
           break;
         }
       }
