@@ -86,6 +86,30 @@ def test_c4_default_decile_kernel_agrees(engine, c4):
     assert np.array_equal(np.isnan(a), np.isnan(b)) and max_rel(a, b) <= 1e-13
 
 
+def test_c2_c3_full_panel_bit_exact(engine):
+    """C2 / C3's panel (5,000 assets x 6,522 days, every column): the month-end kernel's month
+    prices, the time-chunked scan's mom_J / next_ret (+ ids) and the chunked multi-J scan of
+    the sweep against the oracle's month-end and scan, bit for bit."""
+    from csmom.synth import bday_calendar, make_device_panel
+    N, T_d = 5_000, 6_522
+    days, ms_h, _ = bday_calendar("2000-01-03", T_d)
+    pan = make_device_panel(N, days, ms_h, seed=2 * 1000, device="cuda:0")
+    PM, _ = engine.month_end(pan.P, pan.month_start)
+    PM_r, _ = O.month_end(pan.P.cpu().numpy(), ms_h)
+    assert bits_equal(PM.cpu().numpy(), PM_r)
+    T_m = PM.shape[0]
+    IDS = engine.empty((T_m, N), torch.int16)
+    _, M, NR = engine.momentum_chunked(PM, 12, 1, ids=IDS)
+    _, M_r, NR_r, _ = O.momentum_scan(PM_r, 12, 1)
+    assert bits_equal(M.cpu().numpy(), M_r) and bits_equal(NR.cpu().numpy(), NR_r)
+    outs = engine.momentum_multi(PM, (3, 6, 9, 12), 1, with_ids=True,
+                                 chunks=engine.default_chunks(T_m, N, 12, 1))
+    for J, (Mq, NRq, _) in zip((3, 6, 9, 12), outs):
+        _, Mj, NRj, _ = O.momentum_scan(PM_r, J, 1)
+        assert bits_equal(Mq.cpu().numpy(), Mj), J
+        assert bits_equal(NRq.cpu().numpy(), NRj), J
+
+
 # ------------------------------------------------------------------------------------ C3
 @pytest.fixture(scope="module")
 def c3(engine):
