@@ -23,6 +23,7 @@ oracle-backed adapter).
 from __future__ import annotations
 
 import dataclasses
+from collections.abc import Mapping
 import itertools
 from dataclasses import dataclass, field
 
@@ -130,6 +131,30 @@ class SweepConfig:
     @property
     def strategies(self):
         return strategy_grid(self.Js, self.Ks)
+
+
+class _JoinedSeries(Mapping):
+    """{(J, K): PortfolioOut} over a joined batch's outputs (panel q * B + b = J q's panel b),
+    each entry built on access as strided views; a repeated J maps to its last position, as a
+    dict filled in order would."""
+
+    def __init__(self, outs, Js, B):
+        self._outs, self._B = outs, B
+        self._q = {J: q for q, J in enumerate(Js)}
+
+    def __getitem__(self, key):
+        J, K = key
+        q, o = self._q[J], self._outs[K]
+        sl = slice(q * self._B, (q + 1) * self._B)
+        cut = lambda X: None if X is None else X[:, sl]
+        return dataclasses.replace(o, PR=cut(o.PR), LS=cut(o.LS), TURN=cut(o.TURN),
+                                   COST=cut(o.COST), NET=cut(o.NET))
+
+    def __iter__(self):
+        return iter([(J, K) for J in self._q for K in self._outs])
+
+    def __len__(self):
+        return len(self._q) * len(self._outs)
 
 
 class SweepRunner:
@@ -286,18 +311,18 @@ class SweepRunner:
         outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)
         del L, NR
         summ_all = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # [nK][nJ * B][F]
-        series, summ = {}, {}
-        # per-(J, K) series as views of the joined outputs (a copy each was 80 small kernels a
-        # step on C3, host-bound)
-        cut = lambda X, sl: None if X is None else X[:, sl]
-        for q, (J, _, _) in enumerate(items):
-            sl = slice(q * B, (q + 1) * B)
+        Js = [it[0] for it in items]
+        # per-(J, K) series: strided views of the joined outputs, built when read (C3's step is
+        # host-bound: 16 strategies x 5 views a step cost more than the GPU work they describe)
+        series = _JoinedSeries(outs, Js, B)
+        nK, nJ, F = len(c.Ks), len(Js), summ_all.shape[-1]
+        if len(set(Js)) == nJ and len(set(c.Ks)) == nK and Js == [int(J) for J in c.Js]:
+            # strategy s = J index * nK + K index (strategy_grid): one permuted copy
+            return summ_all.view(nK, nJ, B, F).permute(2, 1, 0, 3).reshape(B, nJ * nK, F), series
+        summ = {}
+        for q, J in enumerate(Js):
             for k, K in enumerate(c.Ks):
-                o = outs[K]
-                series[(J, K)] = dataclasses.replace(o, PR=cut(o.PR, sl), LS=cut(o.LS, sl),
-                                                     TURN=cut(o.TURN, sl), COST=cut(o.COST, sl),
-                                                     NET=cut(o.NET, sl))
-                summ[(J, K)] = summ_all[k, sl]
+                summ[(J, K)] = summ_all[k, q * B:(q + 1) * B]
         rows = [summ[(J, K)] for (J, K) in c.strategies]
         return torch.stack(rows, dim=1), series                  # [B][S][F]
 
