@@ -1415,14 +1415,12 @@ extern "C" {
 int csm_abi_version(void) { return CSM_ABI_VERSION; }
 
 int csm_tune_portfolio(const char* key, int value);  // portfolio.hip
-int csm_tune_boot(const char* key, int value);       // sweep_boot.hip
 
 int csm_tune(const char* key, int value) {
   if (!key) return CSM_E_INVAL;
   if (!strcmp(key, "cohort_lds") || !strcmp(key, "cohort_seg") || !strcmp(key, "turn_want") ||
       !strcmp(key, "overlap_rows") || !strcmp(key, "turn_gen_grid"))
     return csm_tune_portfolio(key, value);
-  if (!strcmp(key, "boot_occ")) return csm_tune_boot(key, value);
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_bwf") && (value == 0 || value == 1 || value == 4)) { g_tune_signal_bwf = value; return CSM_OK; }
   if (!strcmp(key, "dec_merge") && (value == 0 || value == 1)) { g_tune_dec_merge = value; return CSM_OK; }

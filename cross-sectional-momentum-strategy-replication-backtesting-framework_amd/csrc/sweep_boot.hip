@@ -27,8 +27,6 @@
 // test per cell: C5 rank stage 118 ms/step against 55 for bootstrap + scan + decile pass.
 #include "csm_common.h"
 
-#include <string.h>
-
 #define BS_MAXJ 4
 #define BS_RW 16        // generic register ring: max(J) + skip <= 16
 #ifndef BS_CHUNK
@@ -74,11 +72,8 @@ __device__ __forceinline__ double win_prod(const double (&f)[RW], int q, int lo,
 // One lane per two adjacent assets of one panel (N even): column c0 = b * N + a0 of the
 // [T_m][B * N] layout.  R rows are gathered by the panel's source months, BS_CHUNK months in
 // flight.
-// CH months of R rows in flight per lane, MB workgroups per CU the registers must allow:
-// (8, 1) holds 161 VGPRs (three waves per SIMD: a C5 batch's 3908 waves run in two rounds);
-// (1, 4) fits 122 (all waves resident at once, one month in flight each)
-template <int RW, bool FIX, int CH = BS_CHUNK, int MB = BS_MINB>
-__global__ __launch_bounds__(BS_THREADS, MB) void k_boot_scan(
+template <int RW, bool FIX>
+__global__ __launch_bounds__(BS_THREADS, BS_MINB) void k_boot_scan(
     const double* __restrict__ R, int T_m, int64_t N, int B, const int32_t* __restrict__ src,
     double p0, int nJ, int skip, BSSet js, double* __restrict__ NR, int32_t* __restrict__ bad) {
   const int64_t BN = (int64_t)B * N;
@@ -102,17 +97,17 @@ __global__ __launch_bounds__(BS_THREADS, MB) void k_boot_scan(
   for (int q = 0; q < BS_MAXJ; ++q) lo[q] = RW - js.J[q] - skip;
   const int hi = RW - skip;
   const bool with_ids = js.IDS[0] != nullptr;
-  for (int m0 = 0; m0 < T_m; m0 += CH) {
-    int s[CH];
+  for (int m0 = 0; m0 < T_m; m0 += BS_CHUNK) {
+    int s[BS_CHUNK];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) s[j] = (m0 + j < T_m) ? sb[m0 + j] : 0;
-    double2 rr[CH];
+    for (int j = 0; j < BS_CHUNK; ++j) s[j] = (m0 + j < T_m) ? sb[m0 + j] : 0;
+    double2 rr[BS_CHUNK];
 #pragma unroll
-    for (int j = 0; j < CH; ++j)
+    for (int j = 0; j < BS_CHUNK; ++j)
       rr[j] = (m0 + j < T_m) ? *reinterpret_cast<const double2*>(R + (int64_t)s[j] * N + a0)
                              : make_double2(NaN, NaN);
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
+    for (int j = 0; j < BS_CHUNK; ++j) {
       const int m = m0 + j;
       if (m >= T_m) break;
       const double rs[2] = {rr[j].x, rr[j].y};
@@ -185,19 +180,7 @@ __global__ __launch_bounds__(BS_THREADS, MB) void k_boot_scan(
 void launch_bootstrap_index(hipStream_t st, int T_m, int B, int64_t b0, uint64_t seed,
                             double p_new, int32_t* src);
 
-// k_boot_scan occupancy (csm_tune "boot_occ", result-preserving): 0 eight months of R rows in
-// flight, three waves per SIMD | 1 one month in flight, four waves per SIMD
-static int g_tune_boot_occ = 0;
-
 extern "C" {
-
-int csm_tune_boot(const char* key, int value) {
-  if (key && !strcmp(key, "boot_occ") && (value == 0 || value == 1)) {
-    g_tune_boot_occ = value;
-    return CSM_OK;
-  }
-  return CSM_E_INVAL;
-}
 
 int csm_boot_scan(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t B, int64_t b0,
                   uint64_t seed, double mean_block, double p0, const int32_t* Js, int32_t nJ,
@@ -229,10 +212,7 @@ int csm_boot_scan(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t
   LAUNCH_CHECK(ctx, "k_bootstrap_index");
   const int64_t BN = (int64_t)B * N;
   const unsigned blocks = (unsigned)((BN / 2 + BS_THREADS - 1) / BS_THREADS);
-  if (fix && g_tune_boot_occ == 1)   // all waves resident, one month in flight each
-    hipLaunchKernelGGL((k_boot_scan<13, true, 1, 4>), dim3(blocks), dim3(BS_THREADS), 0, ctx->stream,
-                       R, T_m, N, B, (const int32_t*)src, p0, nJ, skip, js, NR, bad);
-  else if (fix)   // J = 3, 6, 9, 12, skip 1: a 13-slot ring, compile-time windows
+  if (fix)   // J = 3, 6, 9, 12, skip 1: a 13-slot ring, compile-time windows
     hipLaunchKernelGGL((k_boot_scan<13, true>), dim3(blocks), dim3(BS_THREADS), 0, ctx->stream, R,
                        T_m, N, B, (const int32_t*)src, p0, nJ, skip, js, NR, bad);
   else

@@ -51,9 +51,8 @@ int csm_abi_version(void);
  * register sums), "turn_want" (turnover workgroups per launch, default 4096; set before sizing
  * the portfolio workspace), "turn_gen_grid" (workgroups of the general-row turnover launch,
  * default 8192), "overlap_rows" (1 one thread per (month, panel, decile) for single-chunk
- * plans | 0 one per (K, month, panel, decile)), "boot_occ" (csm_boot_scan: 0 eight months of
- * base-return rows in flight per lane | 1 one month, four waves per SIMD).  Returns
- * CSM_E_INVAL for an unknown key or value. */
+ * plans | 0 one per (K, month, panel, decile)).  Returns CSM_E_INVAL for an unknown key or
+ * value. */
 int csm_tune(const char* key, int value);
 /* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
  * wall-clock ticks (100 MHz) at its phase boundaries (NULL switches it off). */

@@ -153,19 +153,3 @@ def test_boot_scan_rejects_bad_args(engine):
     R2 = _base_returns(engine, 501, T_d=700)
     with pytest.raises(csmom.CsmError):
         engine.boot_scan(R2, 2, (3,), 1, with_ids=False)   # odd N
-
-
-def test_boot_scan_occupancy_variant_bit_identical(engine):
-    """csm_tune("boot_occ", 1) (one month of rows in flight, four waves per SIMD) writes the
-    same source months, mom_J, ids and shared next_ret as the default, bit for bit."""
-    R = _base_returns(engine, 2000, seed=15)
-    a = engine.boot_scan(R, 7, (3, 6, 9, 12), 1, b0=3)
-    assert engine.lib.csm_tune(b"boot_occ", 1) == 0
-    try:
-        b = engine.boot_scan(R, 7, (3, 6, 9, 12), 1, b0=3)
-    finally:
-        assert engine.lib.csm_tune(b"boot_occ", 0) == 0
-    assert torch.equal(a[0], b[0]) and int(a[3].item()) == int(b[3].item()) == 0
-    assert bits_equal(a[2].cpu().numpy(), b[2].cpu().numpy())
-    for (M0, I0), (M1, I1) in zip(a[1], b[1]):
-        assert bits_equal(M0.cpu().numpy(), M1.cpu().numpy()) and torch.equal(I0, I1)
