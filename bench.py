@@ -2,9 +2,11 @@
 """Benchmark: asset-days backtested per second on the fused signal -> rank -> portfolio pass.
 
 Workload (BASELINE.json north_star / configs[3]): C4 = 100,000 assets x 10,000 business days
-per GPU (bdate_range('1985-01-01'), 461 months), J=12 skip=1 K=1 equal-weight deciles,
-long-short.  N GPUs = one process per GPU (torchrun), date-sharded in whole months; with
---scaling weak (default) every rank owns a C4-sized month range of an N x 10,000-day panel.
+(bdate_range('1985-01-01'), 461 months), J=12 skip=1 K=1 equal-weight deciles, long-short.
+N GPUs = one process per GPU over RCCL: `python bench.py --gpus N` starts the N worker
+processes itself (or run it under torchrun).  C4 at N > 1 date-shards the FIXED 100k x 10k
+panel in whole months (--scaling strong, the default); --scaling weak gives every rank a
+C4-sized month range of an N x 10,000-day panel.
 
 A step = one full pass over the resident panel: month-end aggregation, [summary all-gather +
 carry fold when N>1], ret/mom/next_ret scan, per-date qcut labels fused with decile means,
@@ -35,7 +37,7 @@ SWEEP_CONFIGS = {
 }
 CONFIGS = {
     "c4": dict(N=100_000, days=10_000, start="1985-01-01",
-               name="C4: 100k assets x 10k bdays per GPU, J=12 skip=1 K=1 EW decile long-short"),
+               name="C4: 100k assets x 10k bdays, J=12 skip=1 K=1 EW decile long-short"),
     "c2": dict(N=5_000, days=6_522, start="2000-01-03",
                name="C2: 5k assets x 25y bdays (6522), J=12 skip=1 K=1 EW decile long-short"),
 }
@@ -61,7 +63,9 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=100, help="C5: panels per device batch")
     ap.add_argument("--assets", type=int, default=None)
     ap.add_argument("--days", type=int, default=None)
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="C4 / C2 at N > 1: strong = the fixed panel date-sharded over the ranks "
+                         "(BASELINE C4), weak = every rank a full-size month range")
     ap.add_argument("--shard-mode", default="fused", choices=["fused", "unfused"],
                     help="N>1 date shards: speculative fused signal + repair, or month-end + "
                          "carried scan")
@@ -78,7 +82,8 @@ def parse(argv=None):
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the step as one captured hipGraph (auto: the unfused narrow "
-                         "panels, C2, where launch gaps are a large share of the step)")
+                         "panels, C2, where launch gaps are a large share of the step; C3 on one "
+                         "GPU with 'on')")
     ap.add_argument("--tune", action="append", default=[],
                     help="csm_tune key=value applied before the run (kernel A/B), repeatable")
     ap.add_argument("--full-deciles", action="store_true",
@@ -175,17 +180,70 @@ def cpu_baseline_sweep(config: str, n_assets: int, days: int, start: str):
                        f"on {B} panels x {n_assets} assets x {T_m} months, {dt:.1f} s")
 
 
+def spawn_workers(argv):
+    """`bench.py --gpus N` outside torchrun: start N worker processes of this script with
+    torchrun's environment (RANK = LOCAL_RANK = the GPU index, WORLD_SIZE = N, MASTER_* on
+    127.0.0.1) and wait for them.  This process never touches the GPU (nothing here imports
+    torch), so no process that initialised the GPU is replaced; the workers inherit stdout and
+    rank 0 prints the JSON line.  If a worker fails the others are stopped and the first
+    failing status is returned."""
+    import signal
+    import socket
+    import subprocess
+
+    args = parse(argv)
+    n = args.gpus
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = [subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *argv],
+                              env=dict(base, RANK=str(r), LOCAL_RANK=str(r)))
+             for r in range(n)]
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.2)
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.send_signal(signal.SIGTERM)
+        for p in live:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def dist_setup(args):
-    """(world, rank, device) from the torchrun environment; the process group for N > 1 on
-    args.backend (nccl = RCCL, one GPU per rank; gloo = host-staged, the 1-GPU rehearsal)."""
+    """(world, rank, device) from the torchrun environment (set by spawn_workers or torchrun);
+    the process group for N > 1 on args.backend (nccl = RCCL, one GPU per rank; gloo =
+    host-staged, the 1-GPU rehearsal, where ranks beyond the visible GPUs share them)."""
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N>1 must be launched with torchrun (one process per GPU)")
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        if args.backend != "gloo":
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but {ndev} visible GPUs (RCCL needs "
+                             f"one GPU per rank; --backend gloo shares them)")
+        local %= ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 and not dist.is_initialized():
@@ -240,6 +298,11 @@ def committed_profile(config, N, T_d, lib_hash):
 
 def main(argv=None):
     args = parse(argv)
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        rc = spawn_workers(list(sys.argv[1:] if argv is None else argv))
+        if rc:
+            raise SystemExit(rc)
+        return None
     if args.config in SWEEP_CONFIGS:
         return sweep_main(args)
     import torch
@@ -412,7 +475,7 @@ def main(argv=None):
         np.savez(args.dump, LS=LSh.cpu().numpy(), EW=EWh.cpu().numpy(), CNT=CNTh.cpu().numpy())
 
     ms_per_step = 1000.0 * elapsed / args.steps
-    units = N * T_d * world if args.scaling == "weak" else N * total_days
+    units = N * total_days            # the whole panel (all ranks' date shards)
     value = units * args.steps / elapsed
     out = None
     if rank == 0:
@@ -470,9 +533,13 @@ def main(argv=None):
                             f"k_month_end + scan ({chunks} month chunks, + bucket ids) -> narrow "
                             f"k_deciles on ids" if narrow_ids else
                             f"k_month_end + scan ({chunks} month chunks)"),
-            "config": {"workload": cfg["name"] if args.assets is None and args.days is None
-                       else f"custom: {N} assets x {T_d} bdays per GPU",
-                       "assets": N, "bdays_per_gpu": T_d, "months_per_gpu": T_m, "J": J,
+            "config": {"workload": (cfg["name"] if args.assets is None and args.days is None
+                                    else f"custom: {N} assets x {total_days} bdays") +
+                                   (f", date-sharded across {world} GPUs" if world > 1 else "") +
+                                   (" (weak scaling: 10k bdays per GPU)"
+                                    if world > 1 and args.scaling == "weak" else ""),
+                       "assets": N, "bdays": total_days, "bdays_rank0": T_d, "months_rank0": T_m,
+                       "J": J,
                        "skip": skip, "K": 1, "n_bins": nb, "weighting": "equal",
                        "parallelism": f"date-shard x{world}"},
             "roofline": roofline,
@@ -615,8 +682,9 @@ def sweep_profile(config, N, T_d, stage, alg_bytes):
 
 
 def sweep_main(args):
-    """C3 / C5: the (J, K) sweep (SweepRunner) on one panel (C3, weak scaling: each rank its own
-    panel) or on bootstrap panels (C5, strong scaling: the panels are split across ranks)."""
+    """C3 / C5: the (J, K) sweep (SweepRunner) on one panel (C3: at N > 1 the 16 strategies are
+    split across the ranks, SweepRunner.run_batch_sharded, strong scaling of the fixed grid) or
+    on bootstrap panels (C5, strong scaling: the panels are split across ranks)."""
     import torch
     import torch.distributed as dist
 
@@ -640,7 +708,7 @@ def sweep_main(args):
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":
-        seed = args.seed * 1000 + 3 + rank
+        seed = args.seed * 1000 + 3      # the same panel on every rank (strategy shards)
         panel = make_device_panel(N, days, ms_host, seed=seed, device=dev)
         g = torch.Generator(device=dev)
         g.manual_seed(seed)
@@ -652,23 +720,25 @@ def sweep_main(args):
             ts.month_end(panel.P, panel.month_start, PM=PM)
             W = PM.abs() * shares              # market cap at formation (value weights)
             ADV = W * turn_rate                # dollar ADV for the square-root impact
-            summ, _ = runner.run_batch(PM, 1, W=W, ADV=ADV)
+            summ, _ = run_grid(PM, 1, W=W, ADV=ADV)
             return summ
 
         flag_acc = torch.zeros(1, dtype=torch.int32, device=dev)
+        # N > 1: each rank runs its block of the (J, K) grid, one all-gather of the summary
+        run_grid = runner.run_batch_sharded if world > 1 else runner.run_batch
 
         def step_defer():   # the same step with no device sync (hipGraph capture): the
             ts.month_end(panel.P, panel.month_start, PM=PM)   # legs flag is accumulated and
             W = PM.abs() * shares                             # read after the timed loop
             ADV = W * turn_rate
-            summ, _, fl = runner.run_batch(PM, 1, W=W, ADV=ADV, defer=True)
+            summ, _, fl = run_grid(PM, 1, W=W, ADV=ADV, defer=True)
             if fl is not None:
                 flag_acc.add_(fl)
             return summ
-        units = float(N) * T_d * S * world
+        units = float(N) * T_d * S
         unit = "asset-day-strategies/s"
-        scaling = "weak"
-        n_panels = world
+        scaling = "strong"
+        n_panels = 1
     else:
         n_panels = args.panels or cfg["panels"]
         panel = make_device_panel(N, days, ms_host, seed=args.seed * 1000 + 5, device=dev)
@@ -702,13 +772,36 @@ def sweep_main(args):
             dist.barrier()
         return time.perf_counter() - t0, o
 
+    # C3 on one GPU with --graph on: the deferred step captured as one hipGraph and replayed
+    # (replay-safe, tests/test_gpu_capture.py).  Not the default: the step is device-bound, the
+    # graph measured 0.675 vs 0.672 ms eager (profiles/r04/experiments).  N > 1 keeps the eager
+    # step (its all-gather is a host-staged gloo call or an RCCL call outside the graph).
+    graph = None
+    if defer and world == 1 and args.graph == "on":
+        s_cap = torch.cuda.Stream()
+        s_cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_cap):      # warm-up on a side stream (torch's capture recipe)
+            step_defer()
+        torch.cuda.current_stream().wait_stream(s_cap)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_out = step_defer()
+        graph.replay()
+        torch.cuda.synchronize()
+
+        def step_graph():
+            graph.replay()
+            return g_out
     # the timed loop runs uninstrumented (HIP events per stage call cost host time the
     # launch-bound C3 step would pay); per-stage device times come from a second, untimed pass
     if defer:
         flag_acc.zero_()
-    elapsed, out = timed(step_defer if defer else step)
-    if defer and int(flag_acc.item()):
-        defer = False
+    elapsed, out = timed(step_graph if graph is not None else step_defer if defer else step)
+    if defer and allreduce_host([float(flag_acc.item())],
+                                dist.ReduceOp.SUM if world > 1 else None, dev)[0]:
+        defer = False   # (every rank decides alike: the rerun's barriers need them all)
+        graph = None
         elapsed, out = timed(step)
     elapsed = allreduce_host([elapsed], dist.ReduceOp.MAX if world > 1 else None, dev)[0]
     ts.on = True
@@ -739,7 +832,7 @@ def sweep_main(args):
             "config": {"workload": cfg["name"], "assets": N, "bdays": T_d, "months": T_m,
                        "strategies": S, "panels": n_panels, "weighting": "value" if args.config == "c3" else "equal",
                        "costs": "spread/2 + 0.1*vol*sqrt(size/ADV), AUM 1e8" if args.config == "c3" else "spread/2",
-                       "parallelism": f"{'panel' if args.config == 'c5' else 'replica'}-shard x{world}"},
+                       "parallelism": f"{'panel' if args.config == 'c5' else 'strategy'}-shard x{world}"},
             "roofline": {"bound": "hbm", "kernel": dname, "achieved": round(ach, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                          "traffic": sweep_traffic(args.config, N, T_d, dname),
@@ -751,6 +844,7 @@ def sweep_main(args):
                                   "frac": round(alg_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                   "algorithmic_bytes_per_step_rank0": alg_step},
             "stage_ms": {k: round(v[0], 4) for k, v in stages.items()},
+            "hipgraph": graph is not None,
             "result_means": res_summary,
             "cpu_baseline": None,
         }

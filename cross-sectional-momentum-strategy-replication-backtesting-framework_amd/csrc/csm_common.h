@@ -66,6 +66,25 @@ static inline int prep(csm_ctx* c) {
 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// Whether the context's stream is being captured into a hipGraph.  Context-owned buffers are
+// baked into a captured graph by address, so they are never (re)allocated while capturing.
+static inline bool capturing(csm_ctx* c) {
+  hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(c->stream, &s) == hipSuccess && s != hipStreamCaptureStatusNone;
+}
+
+// Device counters / flags the library resets before a launch that accumulates into them are
+// zeroed by a kernel, not by hipMemsetAsync: a kernel node replays the same way in a captured
+// graph as eagerly (the turnover work-list counter, the boot-scan domain flag).
+static __global__ void k_zero_i32(int32_t* __restrict__ p, int n) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) p[i] = 0;
+}
+static inline hipError_t zero_i32_async(int32_t* p, int n, hipStream_t st) {
+  hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, p, n);
+  return hipGetLastError();
+}
+
 // ---- shared by the decile kernels (csmom.hip and deciles_narrow.hip) -------------------------
 #define MAXQ 21  // n_bins + 1 <= 21
 #define MAXT 42  // distinct target ranks (2 per interior quantile + min + max)

@@ -1415,11 +1415,12 @@ extern "C" {
 int csm_abi_version(void) { return CSM_ABI_VERSION; }
 
 int csm_tune_portfolio(const char* key, int value);  // portfolio.hip
+int csm_tune_ptr_portfolio(const char* key, void* p);  // portfolio.hip
 
 int csm_tune(const char* key, int value) {
   if (!key) return CSM_E_INVAL;
   if (!strcmp(key, "cohort_lds") || !strcmp(key, "cohort_seg") || !strcmp(key, "turn_want") ||
-      !strcmp(key, "overlap_rows") || !strcmp(key, "turn_gen_grid"))
+      !strcmp(key, "overlap_rows") || !strcmp(key, "turn_gen_grid") || !strcmp(key, "gen_reset"))
     return csm_tune_portfolio(key, value);
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_bwf") && (value == 0 || value == 1 || value == 4)) { g_tune_signal_bwf = value; return CSM_OK; }
@@ -1432,7 +1433,7 @@ int csm_tune(const char* key, int value) {
 int csm_tune_ptr(const char* key, void* p) {
   if (!key) return CSM_E_INVAL;
   if (!strcmp(key, "dec_timing")) { g_dec_timing = (int64_t*)p; return CSM_OK; }
-  return CSM_E_INVAL;
+  return csm_tune_ptr_portfolio(key, p);
 }
 
 int csm_create(int device, csm_ctx** out) {
@@ -1775,7 +1776,11 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
                             uint16_t* ids, bool pre) {
   int32_t* flg = nullptr;
   if (pre) {
-    if (ctx->dec_flg_n < T_m) {   // beyond the create-time capacity (not capture-safe)
+    if (ctx->dec_flg_n < T_m) {   // beyond the create-time capacity
+      if (capturing(ctx))           // a captured graph would keep the freed buffer's address
+        return set_err(ctx, CSM_E_INVAL, "%s: %d rows exceed the context's row-flag buffer (%d) "
+                       "during stream capture; run the call once before capturing", who, T_m,
+                       ctx->dec_flg_n);
       if (ctx->dec_flg) HIP_CHECK(ctx, hipFree(ctx->dec_flg));
       ctx->dec_flg = nullptr;
       ctx->dec_flg_n = 0;
@@ -1847,6 +1852,10 @@ int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const in
   if (want_ids) {
     const size_t need = (size_t)T_m * (size_t)N * sizeof(uint16_t);
     if (ctx->scratch_bytes < need) {
+      if (capturing(ctx))
+        return set_err(ctx, CSM_E_INVAL, "csm_pipeline: the bucket-id scratch (%zu B) must grow to "
+                       "%zu B during stream capture; run the call once before capturing",
+                       ctx->scratch_bytes, need);
       if (ctx->scratch) HIP_CHECK(ctx, hipFree(ctx->scratch));
       ctx->scratch = nullptr;
       ctx->scratch_bytes = 0;

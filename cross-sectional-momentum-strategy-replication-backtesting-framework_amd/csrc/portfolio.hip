@@ -31,6 +31,7 @@
 #define PF_THREADS 256
 #define PF_WAVES (PF_THREADS / 64)
 #define PF_CHUNK_MIN 256     // assets per chunk, at least one per thread
+#define PF_PLAN_MIN_B 4      // chunk plans of smaller batches are those of 4 panels (pf_plan)
 #define TO_MAXK 240
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -822,7 +823,10 @@ __device__ __forceinline__ void turnover_body(
     for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
   }
   if (all_full == GEN) {   // the other launch's row
-    if (!GEN && gen_list && tid == 0) gen_list[atomicAdd(gen_count, 1)] = bid;   // onto its work list
+    if (!GEN && gen_list && tid == 0) {   // onto its work list (capacity: one slot per workgroup
+      const int slot = atomicAdd(gen_count, 1);   // of this launch; a counter that was not reset
+      if (slot < rows * Ct) gen_list[slot] = bid;   // can never write past it)
+    }
     return;
   }
   if (!GEN && CNT && (N & 3) == 0) {
@@ -1154,7 +1158,9 @@ __global__ __launch_bounds__(PF_THREADS, BM ? TO_MINB_BM : 1) void k_turnover(
                                   half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp, gen_list,
                                   gen_count, TPv, TPm);
   } else {   // the general rows the steady launch put on the work list
-    const int n = *(volatile int32_t*)gen_count;   // written by the previous launch
+    const int cap = T_m * B * Ct;                   // the list's capacity
+    const int n0 = *(volatile int32_t*)gen_count;   // written by the previous launch
+    const int n = n0 < cap ? n0 : cap;
     for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
       turnover_body<VW, IMP, true, BM>(gen_list[i], L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH,
                                    Ct, half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp,
@@ -1382,6 +1388,16 @@ static int64_t g_tune_turn_gen_grid = 8192;   // C5 portfolio: 512 49.1, 2048 40
 // 1: k_overlap_rows (one thread per (t, b, decile) serving every K of the set) for single-chunk
 // cohort plans, 0: k_overlap always
 static int g_tune_overlap_rows = 1;
+// Diagnosis of the round-3 graph-replay fault (tests/test_gpu_capture.py): how the turnover
+// work-list counter is reset before the steady launch (1: k_zero_i32, the default; 0:
+// hipMemsetAsync, round 3's form), and an optional device int32 that receives the counter the
+// general launch read (csm_tune_ptr("gen_probe")).  Neither changes a result.
+static int g_tune_gen_reset = 1;
+static int32_t* g_gen_probe = nullptr;
+
+__global__ void k_copy_i32(const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
+  if (threadIdx.x == 0) dst[0] = *(volatile const int32_t*)src;
+}
 
 struct PfPlan {
   int C, kpar, Ct;
@@ -1394,7 +1410,11 @@ struct PfPlan {
 static int64_t g_tune_turn_want = 4096;
 static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
   PfPlan p;
-  const int64_t rows = (int64_t)T_m * B;
+  // Batches of up to PF_PLAN_MIN_B panels are planned as PF_PLAN_MIN_B panels: the sweeps join
+  // the four look-backs of a single-panel grid into one launch (B = 4) and a strategy-sharded
+  // rank runs fewer of them (B = 1, 2), so a panel's turnover chunks -- and with them the bits
+  // of its TURN / COST sums -- do not depend on how many look-backs share its launch.
+  const int64_t rows = (int64_t)T_m * (B < PF_PLAN_MIN_B ? PF_PLAN_MIN_B : B);
   const int64_t want = 4096;
   const int64_t cmax = (N + PF_CHUNK_MIN - 1) / PF_CHUNK_MIN;
   // the chunking depends on (rows, N) only, so a cohort pass gives the same partial sums
@@ -1600,6 +1620,18 @@ int csm_tune_portfolio(const char* key, int value) {
     g_tune_overlap_rows = value;
     return CSM_OK;
   }
+  if (key && !strcmp(key, "gen_reset") && (value == 0 || value == 1)) {
+    g_tune_gen_reset = value;
+    return CSM_OK;
+  }
+  return CSM_E_INVAL;
+}
+
+int csm_tune_ptr_portfolio(const char* key, void* p) {
+  if (key && !strcmp(key, "gen_probe")) {
+    g_gen_probe = (int32_t*)p;
+    return CSM_OK;
+  }
   return CSM_E_INVAL;
 }
 
@@ -1732,7 +1764,10 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
       // walks (C5 112.0 -> 108.9, C3 1.438 -> 1.405 ms/step against a second full grid)
       int32_t* gen_count = (int32_t*)((char*)workspace + lay.gen_b);
       int32_t* gen_list = gen_count + 1;
-      HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
+      if (g_tune_gen_reset)
+        HIP_CHECK(ctx, zero_i32_async(gen_count, 1, st));
+      else
+        HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
       const unsigned gen_grid = (unsigned)std::min<int64_t>(nblk, g_tune_turn_gen_grid);
       // steady equal-weight rows take their factors from k_turn_prep (no per-workgroup prologue)
       const bool prep = !W && !imp && (N & 3) == 0;
@@ -1757,6 +1792,10 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
                            (const double*)TPv, (const uint32_t*)TPm);
       }
       LAUNCH_CHECK(ctx, "k_turnover");
+      if (g_gen_probe) {
+        hipLaunchKernelGGL(k_copy_i32, dim3(1), dim3(64), 0, st, (const int32_t*)gen_count, g_gen_probe);
+        LAUNCH_CHECK(ctx, "k_copy_i32");
+      }
     }
     double* TURNq = TURN ? TURN + q0 * rb : nullptr;
     double* COSTq = COST ? COST + q0 * rb : nullptr;

@@ -207,7 +207,7 @@ int csm_boot_scan(csm_ctx* ctx, const double* R, int32_t T_m, int64_t N, int32_t
   }
   if (!aligned16(R) || !aligned16(NR))
     return set_err(ctx, CSM_E_INVAL, "csm_boot_scan: R and NR must be 16-B aligned");
-  HIP_CHECK(ctx, hipMemsetAsync(bad, 0, sizeof(int32_t), ctx->stream));
+  HIP_CHECK(ctx, zero_i32_async(bad, 1, ctx->stream));
   launch_bootstrap_index(ctx->stream, T_m, B, b0, seed, 1.0 / mean_block, src);
   LAUNCH_CHECK(ctx, "k_bootstrap_index");
   const int64_t BN = (int64_t)B * N;

@@ -187,6 +187,48 @@ class SweepRunner:
             out = self._run_batch(PMb, B, W, ADV, SIG, None)
         return out
 
+    def run_batch_sharded(self, PMb: torch.Tensor, B: int, W=None, ADV=None, SIG=None,
+                          defer=False):
+        """run_batch with the (J, K) grid split across the ranks (independent
+        (panel, J, K) units): every rank holds the month panel, rank r runs only the r-th
+        contiguous block of cfg.strategies (its look-backs' scans and decile passes, its holding
+        periods' accounting), and ONE all-gather of the [B][S_r][F] summary blocks assembles the
+        [B][S][F] table on every rank.  A block's strategies come out bit for bit as in the
+        unsharded run: every look-back's scan, labels and accounting are the same launches on
+        the same rows, and batches of up to four panels share one chunk plan (portfolio.hip
+        pf_plan), so whether four, two or one look-back share a launch does not change a bit.
+        Returns (summary, series of this rank's strategies) -- with defer=True also the legs
+        flag (device int32 [1], or None), as run_batch(defer=True)."""
+        c = self.cfg
+        strategies = c.strategies
+        S, F = len(strategies), len(SUMMARY_FIELDS)
+        s0, s1 = panel_partition(S, self.G)[self.rank]
+        mine = strategies[s0:s1]
+        flag, series = None, {}
+        if mine:
+            Js = tuple(dict.fromkeys(J for J, _ in mine))
+            Ks = tuple(dict.fromkeys(K for _, K in mine))
+            sub = SweepRunner(self.st, dataclasses.replace(c, Js=Js, Ks=Ks))
+            if defer:
+                summ, series, flag = sub.run_batch(PMb, B, W, ADV, SIG, defer=True)
+            else:
+                summ, series = sub.run_batch(PMb, B, W, ADV, SIG)
+            pos = {jk: i for i, jk in enumerate(sub.cfg.strategies)}
+            idx = [pos[jk] for jk in mine]
+            if idx != list(range(len(pos))):
+                summ = summ[:, idx]
+            series = {jk: series[jk] for jk in mine}
+        if self.G == 1:
+            return (summ, series, flag) if defer else (summ, series)
+        width = max(b - a for a, b in panel_partition(S, self.G))
+        pad = torch.full((B, width, F), float("nan"), dtype=PMb.dtype, device=PMb.device)
+        if mine:
+            pad[:, :s1 - s0] = summ
+        allp = all_gather_stack(pad, self.group)                   # the one collective
+        table = torch.cat([allp[g, :, :b - a] for g, (a, b) in
+                           enumerate(panel_partition(S, self.G))], 1)
+        return (table, series, flag) if defer else (table, series)
+
     def _run_batch(self, PMb, B, W, ADV, SIG, flag):
         return self._account(self._ranked(PMb, B), B, W, ADV, SIG, flag)
 

@@ -24,7 +24,7 @@ class DevicePanel:
     P: torch.Tensor              # [T_d][N] float64 in HBM
     month_start: torch.Tensor    # [T_m+1] int64 in HBM
     month_start_host: np.ndarray
-    days: pd.DatetimeIndex
+    days: pd.DatetimeIndex       # (datetime64[D] arrays past pandas' Timestamp range)
     month_end: pd.DatetimeIndex
 
     @property
@@ -33,8 +33,21 @@ class DevicePanel:
 
 
 def bday_calendar(start: str, periods: int):
-    days = pd.bdate_range(start, periods=periods)
-    ms, mend = month_offsets(days)
+    """pd.bdate_range(start, periods=periods) (Mon-Fri, start rolled forward) with its calendar
+    month offsets and 'ME' labels, computed on numpy datetime64[D] so that long weak-scaling
+    calendars (8 x 10,000 bdays from 1985 end in 2291) do not overflow pandas' nanosecond
+    Timestamps.  Days / labels come back as pd.DatetimeIndex when they fit, else as
+    datetime64[D] arrays."""
+    d0 = np.busday_offset(np.datetime64(start, "D"), 0, roll="forward")
+    days = np.busday_offset(d0, np.arange(periods, dtype=np.int64), roll="forward")
+    mkey = days.astype("datetime64[M]")
+    change = np.nonzero(mkey[1:] != mkey[:-1])[0] + 1
+    ms = np.concatenate([[0], change, [periods]]).astype(np.int64) if periods else \
+        np.zeros(1, dtype=np.int64)
+    mend = (mkey[ms[:-1]] + 1).astype("datetime64[D]") - np.timedelta64(1, "D")
+    if periods == 0 or mend[-1] < np.datetime64("2262-04-01"):
+        return (pd.DatetimeIndex(days.astype("datetime64[ns]")), ms,
+                pd.DatetimeIndex(mend.astype("datetime64[ns]")))
     return days, ms, mend
 
 
@@ -138,6 +151,10 @@ def make_device_panel(N: int, days: pd.DatetimeIndex, month_start: np.ndarray, s
         P[d0:d1] = blk.view(torch.float64)
         del lr, c, blk, gone, nanc
     ms_dev = torch.from_numpy(np.ascontiguousarray(month_start, dtype=np.int64)).to(device)
-    mend = (days[month_start[:-1]] + pd.offsets.MonthEnd(0)) if T_m else pd.DatetimeIndex([])
+    dd = np.asarray(days).astype("datetime64[D]")
+    mend = ((dd[np.asarray(month_start[:-1])].astype("datetime64[M]") + 1).astype("datetime64[D]")
+            - np.timedelta64(1, "D")) if T_m else dd[:0]
+    if T_m == 0 or mend[-1] < np.datetime64("2262-04-01"):
+        mend = pd.DatetimeIndex(mend.astype("datetime64[ns]"))
     return DevicePanel(P=P, month_start=ms_dev, month_start_host=np.asarray(month_start),
-                       days=days, month_end=pd.DatetimeIndex(mend))
+                       days=days, month_end=mend)

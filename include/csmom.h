@@ -51,11 +51,13 @@ int csm_abi_version(void);
  * register sums), "turn_want" (turnover workgroups per launch, default 4096; set before sizing
  * the portfolio workspace), "turn_gen_grid" (workgroups of the general-row turnover launch,
  * default 8192), "overlap_rows" (1 one thread per (month, panel, decile) for single-chunk
- * plans | 0 one per (K, month, panel, decile)).  Returns CSM_E_INVAL for an unknown key or
- * value. */
+ * plans | 0 one per (K, month, panel, decile)), "gen_reset" (1 the turnover work-list counter
+ * reset by a kernel | 0 by hipMemsetAsync, round 3's form, kept for the graph-replay diagnosis
+ * of tests/test_gpu_capture.py).  Returns CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
-/* Profiling aid: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
- * wall-clock ticks (100 MHz) at its phase boundaries (NULL switches it off). */
+/* Profiling aids: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
+ * wall-clock ticks (100 MHz) at its phase boundaries; "gen_probe" = device int32 that receives
+ * the turnover work-list length the general-row launch read (NULL switches either off). */
 int csm_tune_ptr(const char* key, void* p);
 
 /* Create a context bound to HIP device `device` (stream = the null stream). */

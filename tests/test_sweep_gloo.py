@@ -127,3 +127,67 @@ def test_sweep_shards_gloo(world):
         m = ~np.isnan(ref)
         # summary reductions run over differently shaped batches: equal to rounding
         assert np.allclose(tab[m], ref[m], rtol=1e-12, atol=1e-15)
+
+
+# ------------------------------------------------------------------------------------------------
+# (J, K)-grid sharding (SweepRunner.run_batch_sharded, bench C3 at N > 1): every rank holds the
+# month panel and runs its contiguous block of the strategy grid; one all-gather of the summary
+# blocks.  Oracle stages: the table equals the 1-process run_batch bit for bit.
+def _panel_pm():
+    from conftest import load_golden
+    z = load_golden("edge")
+    PM, _ = O.month_end(z["P"], z["month_start"].astype(np.int64))
+    return torch.from_numpy(PM)
+
+
+def _grid_cfg():
+    import csmom
+    return csmom.SweepConfig(Js=(3, 6, 12), Ks=(1, 3), skip=1)
+
+
+def _grid_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import csmom
+        runner = csmom.SweepRunner(OracleSweepStages(), _grid_cfg())
+        tab, series = runner.run_batch_sharded(_panel_pm(), 1)
+        q.put((rank, tab.numpy(), sorted(series)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_strategy_shards_gloo(world):
+    import csmom
+    from csmom.sweep import panel_partition
+    ref, _ = csmom.SweepRunner(OracleSweepStages(), _grid_cfg()).run_batch(_panel_pm(), 1)
+    ref = ref.numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    strategies = _grid_cfg().strategies
+    for rank, tab, keys in res:   # every rank: the whole table, bit for bit the 1-process one
+        assert tab.shape == ref.shape == (1, len(strategies), len(csmom.SUMMARY_FIELDS))
+        assert np.array_equal(np.isnan(tab), np.isnan(ref))
+        m = ~np.isnan(ref)
+        assert np.array_equal(tab[m], ref[m])
+        a, b = panel_partition(len(strategies), world)[rank]
+        assert keys == sorted(strategies[a:b])                  # its own strategies' series
+
+
+def test_strategy_shards_single_process_is_run_batch():
+    import csmom
+    runner = csmom.SweepRunner(OracleSweepStages(), _grid_cfg())
+    a, _ = runner.run_batch_sharded(_panel_pm(), 1)
+    b, _ = runner.run_batch(_panel_pm(), 1)
+    assert np.array_equal(np.isnan(a.numpy()), np.isnan(b.numpy()))
+    m = ~np.isnan(b.numpy())
+    assert np.array_equal(a.numpy()[m], b.numpy()[m])
