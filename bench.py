@@ -648,6 +648,10 @@ class TimedStages:
     def device(self):
         return self.eng.device
 
+    @property
+    def lib(self):
+        return self.eng.lib
+
     def stage_report(self, steps):
         agg = {}
         for name, e0, e1, nb in self.rec:

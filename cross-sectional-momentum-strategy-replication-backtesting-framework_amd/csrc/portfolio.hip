@@ -760,9 +760,9 @@ __device__ __forceinline__ void turnover_body(
   __shared__ double inv[2][TO_MAXK + 1];      // [leg][j]: 1/total of cohort s = t - j (0 = empty)
   __shared__ double sk[TO_MAXQ][2][2];        // [q][leg][month t, t-1]: 1/K_u (0 if none)
   __shared__ int full[TO_MAXQ][2];
-  // steady equal-weight rows with k_turn_prep's factors: no prologue, the row's label loads
+  // steady rows with k_turn_prep's factors: no prologue, the row's label (and weight) loads
   // start at once (the factors are per-row uniforms, read where they are used)
-  const bool pre = !GEN && !VW && !IMP && TPm != nullptr && (N & 3) == 0;
+  const bool pre = !GEN && TPm != nullptr;
   if (!pre) {
   for (int j = tid; j <= Kmax; j += PF_THREADS) {
     const int s = t - j;
@@ -865,7 +865,23 @@ __device__ __forceinline__ void turnover_body(
     }
   } else if (!GEN) {
     // steady state (value weights or impact costs): w_t - w_{t-1} needs the month-t and month
-    // t-K_q labels only; TU cells per lane per trip (stride PF_THREADS), all loads in flight
+    // t-K_q labels only; TU cells per lane per trip (stride PF_THREADS), all loads in flight.
+    // The row's factors (1 / leg totals of months t and t - K_q, 1 / K_u) from k_turn_prep
+    // (row-uniform loads) or the prologue's LDS tables -- the same values.
+    double f1[2], f0[TO_MAXQ][2], fs[TO_MAXQ][2];
+    {
+      const double* tp = pre ? TPv + (int64_t)tb * TP_STRIDE : nullptr;
+#pragma unroll
+      for (int li = 0; li < 2; ++li) {
+        f1[li] = pre ? tp[li * (TO_MAXQ + 1)] : inv[li][0];
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          const bool on = q < nq;
+          f0[q][li] = !on ? 0.0 : pre ? tp[li * (TO_MAXQ + 1) + 1 + q] : inv[li][ks.K[q]];
+          fs[q][li] = !on ? 0.0 : pre ? tp[2 * (TO_MAXQ + 1) + 2 * q + li] : sk[q][li][0];
+        }
+      }
+    }
     constexpr int TU = 2;
     for (int64_t i0 = a0 + tid; i0 < a1; i0 += TU * PF_THREADS) {
       int l1[TU], l0[TU][TO_MAXQ];
@@ -894,13 +910,12 @@ __device__ __forceinline__ void turnover_body(
         for (int q = 0; q < TO_MAXQ; ++q) {
           if (q >= nq) break;
           const double vw0 = VW ? valid_w(x0[u][q]) : 1.0;
-          const int K = ks.K[q];
 #pragma unroll
           for (int li = 0; li < 2; ++li) {
             const int d = li == 0 ? dtop : 0;
-            const double w1 = (l1[u] == d ? vw1 : 0.0) * inv[li][0];
-            const double w0 = (l0[u][q] == d ? vw0 : 0.0) * inv[li][K];
-            charge(q, fabs(w1 - w0) * sk[q][li][0], adv[u], unit_sig);
+            const double w1 = (l1[u] == d ? vw1 : 0.0) * f1[li];
+            const double w0 = (l0[u][q] == d ? vw0 : 0.0) * f0[q][li];
+            charge(q, fabs(w1 - w0) * fs[q][li], adv[u], unit_sig);
           }
         }
       }
@@ -1408,7 +1423,7 @@ struct PfPlan {
 // turnover workgroups wanted per launch (the row split into chunks to reach it); A/B knob
 // "turn_want" -- set it before the portfolio workspace is sized
 static int64_t g_tune_turn_want = 4096;
-static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
+static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K, int32_t n_bins) {
   PfPlan p;
   // Batches of up to PF_PLAN_MIN_B panels are planned as PF_PLAN_MIN_B panels: the sweeps join
   // the four look-backs of a single-panel grid into one launch (B = 4) and a strategy-sharded
@@ -1425,6 +1440,13 @@ static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K) {
   p.kpar = 0;
   int64_t C = (want + rows - 1) / rows;
   C = C < 1 ? 1 : (C > cmax ? cmax : C);
+  // the label-sorted segment path (launch_cohort) owns every segment whole in one of its first
+  // ceil(1024 / rows) chunks and writes zeros in the others: plan only those (C3: 4 -> 1 chunk,
+  // a quarter of the cohort workgroups and overlap partials; the sums are the same bits)
+  if (g_tune_cohort_seg && N <= SEG_MAXN && (int64_t)K * (n_bins + 1) <= SEG_MAXKD) {
+    const int64_t cs = (1024 + rows - 1) / rows;
+    C = C < cs ? C : (cs < 1 ? 1 : cs);
+  }
   p.C = (int)C;
   p.CH = (N + C - 1) / C;
   int64_t Ct = (g_tune_turn_want + rows - 1) / rows;   // turnover chunks
@@ -1570,7 +1592,7 @@ struct PfLayout {
 };
 static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax) {
   PfLayout l;
-  l.p = pf_plan(T_m, B, N, Kmax);
+  l.p = pf_plan(T_m, B, N, Kmax, n_bins);
   l.rows = (int64_t)T_m * B;
   const int64_t cs = l.rows * Kmax * l.p.C * n_bins;
   l.swr = 0;
@@ -1769,8 +1791,9 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
       else
         HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
       const unsigned gen_grid = (unsigned)std::min<int64_t>(nblk, g_tune_turn_gen_grid);
-      // steady equal-weight rows take their factors from k_turn_prep (no per-workgroup prologue)
-      const bool prep = !W && !imp && (N & 3) == 0;
+      // steady rows take their factors from k_turn_prep (no per-workgroup prologue: equal
+      // weights since round 2, value weights / impact costs since round 4)
+      const bool prep = true;
       double* TPv = prep ? (double*)((char*)workspace + lay.tp_b) : nullptr;
       uint32_t* TPm = prep ? (uint32_t*)((char*)workspace + lay.tpm_b) : nullptr;
       if (prep)

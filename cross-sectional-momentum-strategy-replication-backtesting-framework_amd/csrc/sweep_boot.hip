@@ -130,6 +130,13 @@ __global__ __launch_bounds__(BS_THREADS, BS_MINB) void k_boot_scan(
         // pending row's next_ret below: one f64 division per asset-month instead of two
         const double ret = x / pff[c] - 1.0;
         rt[c] = ret;
+        // the shared next_ret also needs every factor fl(1 + ret) after the first present price
+        // finite and non-zero (x / pff can overflow or round to a zero factor even when both
+        // prices are): otherwise 0 * inf could leave a J's ranked row without a return
+        {
+          const double fr = 1.0 + ret;
+          if (!ab[c] && pff[c] == pff[c] && !(fabs(fr) < INFINITY && fr != 0.0)) badp = true;
+        }
         pff[c] = ab[c] ? pff[c] : x;
 #pragma unroll
         for (int k = 0; k + 1 < RW; ++k) f[c][k] = ab[c] ? f[c][k] : f[c][k + 1];

@@ -14,9 +14,10 @@ panels with the month-end aggregation done once per panel:
   * per (J, K, panel): a summary row (months, mean and Sharpe of the long-short as in
     src/utils.py:8-16 at 12 periods a year, mean turnover, mean cost, mean / Sharpe of net).
 
-Multi-GPU: sweep units are independent, so panels are split across ranks in contiguous
-ranges (a panel's bootstrap stream is keyed by its global id, never by the rank) and the only
-collective is one all-gather of the summary table at the end.  The stage implementation is
+Multi-GPU: sweep units are independent.  Bootstrap panels are split across ranks in contiguous
+ranges (a panel's bootstrap stream is keyed by its global id, never by the rank); a single
+panel's (J, K) grid is split across ranks in contiguous strategy blocks (run_batch_sharded).
+Either way the only collective is one all-gather of the summary table at the end.  The stage implementation is
 injected (`Engine` on the GPU; the CPU tests drive the same orchestration with gloo and an
 oracle-backed adapter).
 """
@@ -121,7 +122,9 @@ class SweepConfig:
     # multi-J scan (same labels and summary table, bit for bit)
     boot_scan: bool = True
     # batches of fewer than JOIN_ROWS (month, panel) rows (C3's single panel): the Js' decile
-    # passes and accounting as one launch set over the Js side by side (_account_joined)
+    # passes and accounting as one launch set over the Js side by side (_account_joined); the
+    # same table and series bit for bit (batches of up to four panels share one chunk plan,
+    # portfolio.hip pf_plan; tests/test_gpu_fullsize.py::test_c3_joined_js_equal_per_j)
     join_js: bool = True
     # bootstrap batches: the Js' cohort sums in one pass over the shared next_ret
     # (csm_cohort_sums_js: each month's return row read once for every J; same table bit for bit)
@@ -339,8 +342,8 @@ class SweepRunner:
         """_account for a small batch: the Js' labels / next_ret side by side as nJ * B panels
         (panel q * B + b = J q's panel b; weights / ADV / vol repeated per J), one cohort pass, one
         accounting launch set and one summary launch for the whole (J, K) grid instead of one per
-        J -- C3's single-panel rows are latency-bound per launch.  Same rules; partial sums in
-        another chunk order than per-J calls (within 1e-12)."""
+        J -- C3's single-panel rows are latency-bound per launch.  Same rules, same bits as the
+        per-J calls (one chunk plan for batches of up to four panels)."""
         c, st = self.cfg, self.st
         nJ = len(items)
         rep = lambda X: None if X is None else X.repeat(1, nJ)
@@ -371,7 +374,13 @@ class SweepRunner:
     def _boot_ok(self, T_m, N, B):
         c = self.cfg
         ids = c.decile_ids and hasattr(self.st, "deciles_ids") and N % 4 == 0
-        need = (8 + (2 if ids else 0)) * len(c.Js) * T_m * B * N + 8 * T_m * B * N
+        nJ = len(c.Js)
+        # live together: boot_scan's mom_J (+ ids) per J and the shared next_ret, then each J's
+        # int8 label panel and portfolio workspace (portfolio_multi_js allocates them at once)
+        need = (8 + (2 if ids else 0)) * nJ * T_m * B * N + 8 * T_m * B * N + nJ * T_m * B * N
+        lib = getattr(self.st, "lib", None)
+        if lib is not None and hasattr(lib, "csm_portfolio_workspace"):
+            need += nJ * int(lib.csm_portfolio_workspace(T_m, B, N, c.n_bins, max(c.Ks)))
         return (c.boot_scan and hasattr(self.st, "boot_scan") and N % 2 == 0
                 and 1 <= len(c.Js) <= 4 and max(c.Js) + c.skip <= 16
                 and need <= _free_bytes_dev(self.st) // 2)
