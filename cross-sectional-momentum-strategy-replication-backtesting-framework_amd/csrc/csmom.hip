@@ -1404,9 +1404,6 @@ static int64_t* g_dec_timing = nullptr;
 // PRE decile pass (csm_deciles_ids): 1 the merged sweep, then the general kernel for the rows it
 // leaves | 0 the general kernel only
 static int g_tune_dec_merge = 1;
-// 1: wide rows on ids take the split decile pass (plan, chunked sweep, finish; deciles.inc), 0: the
-// merged one-workgroup-per-row pass.  Same labels and counts; decile means in another fixed order
-static int g_tune_dec_split = 1;
 // csm_momentum_multi: 2 register shift ring, two assets per lane (even N, aligned) | 1 one asset
 // per lane | 0 the shared-memory ring (max(J) + skip > 16 always takes it)
 static int g_tune_mj_reg = 2;
@@ -1430,7 +1427,6 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "dec_merge") && (value == 0 || value == 1)) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
-  if (!strcmp(key, "dec_split") && (value == 0 || value == 1)) { g_tune_dec_split = value; return CSM_OK; }
   return CSM_E_INVAL;
 }
 
@@ -1463,11 +1459,10 @@ int csm_create(int device, csm_ctx** out) {
 
 int csm_destroy(csm_ctx* ctx) {
   if (ctx) (void)csm_allgather_free(ctx);
-  if (ctx && (ctx->scratch || ctx->dec_flg || ctx->dsplit)) {
+  if (ctx && (ctx->scratch || ctx->dec_flg)) {
     (void)hipSetDevice(ctx->device);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->dec_flg) (void)hipFree(ctx->dec_flg);
-    if (ctx->dsplit) (void)hipFree(ctx->dsplit);
   }
   free(ctx);
   return CSM_OK;
@@ -1775,32 +1770,6 @@ int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T
   return CSM_OK;
 }
 
-// The split decile pass's workspace for T_m rows of N cells (csm_common.h DecSplit), carved
-// from one context buffer; sized for n_bins up to MAXQ so one buffer serves every NB.
-static size_t dsplit_layout(int32_t T_m, int64_t N, DecSplit* sp, char* base) {
-  const int64_t C = (N + SPLIT_CELLS - 1) / SPLIT_CELLS;
-  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
-  size_t o = 0;
-  const size_t plan = o; o = al(o + (size_t)T_m * DSPLAN_BYTES);
-  const size_t tab = o;  o = al(o + (size_t)T_m * CSM_FB_BUCKETS);
-  const size_t ph = o;   o = al(o + (size_t)T_m * C * MAXQ * 8);
-  const size_t pl = o;   o = al(o + (size_t)T_m * C * MAXQ * 8);
-  const size_t pc = o;   o = al(o + (size_t)T_m * C * MAXQ * 4);
-  const size_t uc = o;   o = al(o + (size_t)T_m * C * SPLIT_WAVES * 4);
-  const size_t ul = o;   o = al(o + (size_t)T_m * C * SPLIT_WAVES * SPLIT_FL * 4);
-  if (sp) {
-    sp->plan = base + plan;
-    sp->tab = (int8_t*)(base + tab);
-    sp->ph = (double*)(base + ph);
-    sp->pl = (double*)(base + pl);
-    sp->pc = (int32_t*)(base + pc);
-    sp->ucnt = (int32_t*)(base + uc);
-    sp->ulist = (uint32_t*)(base + ul);
-    sp->C = (int)C;
-  }
-  return o;
-}
-
 static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
                             const double* M, const double* NR, int64_t N, int32_t n_bins,
                             const QTab& q, int8_t* L, double* EW, int32_t* CNT, int32_t* NV,
@@ -1819,36 +1788,6 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
       ctx->dec_flg_n = T_m;
     }
     flg = ctx->dec_flg;
-    // wide rows: the split pass (plan, chunked sweep, finish) when the row's (chunk, wave) lists
-    // fit the finish launch's merge
-    const int64_t C = (N + SPLIT_CELLS - 1) / SPLIT_CELLS;
-    if (g_tune_dec_split && g_tune_dec_merge && N > g_tune_dec_narrow_max &&
-        C * SPLIT_WAVES <= DSPLIT_MAXL) {
-      const size_t need = dsplit_layout(T_m, N, nullptr, nullptr);
-      if (ctx->dsplit_bytes < need) {
-        if (capturing(ctx))
-          return set_err(ctx, CSM_E_INVAL, "%s: the split decile workspace (%zu B) must grow to %zu B "
-                         "during stream capture; run the call once before capturing", who,
-                         ctx->dsplit_bytes, need);
-        if (ctx->dsplit) HIP_CHECK(ctx, hipFree(ctx->dsplit));
-        ctx->dsplit = nullptr;
-        ctx->dsplit_bytes = 0;
-        HIP_CHECK(ctx, hipMalloc(&ctx->dsplit, need));
-        ctx->dsplit_bytes = need;
-      }
-      DecSplit sp;
-      dsplit_layout(T_m, N, &sp, (char*)ctx->dsplit);
-      int64_t* tm = g_dec_timing;
-      switch (NR ? n_bins : 0) {
-#define DS_CASE(NBV) case NBV: launch_deciles_split<NBV>(T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, tm, ids, flg, sp); break;
-        DS_CASE(0) DS_CASE(2) DS_CASE(3) DS_CASE(4) DS_CASE(5) DS_CASE(10) DS_CASE(20)
-#undef DS_CASE
-        default:
-          return set_err(ctx, CSM_E_INVAL, "%s: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", who, n_bins);
-      }
-      LAUNCH_CHECK(ctx, who);
-      return CSM_OK;
-    }
   }
   if (!NR) {
     launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, pre, flg);

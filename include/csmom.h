@@ -44,9 +44,7 @@ int csm_abi_version(void);
  * drive the fallbacks on inputs that would not reach them): "signal_vec" (2 paired 16-B rows |
  * 1 one asset per lane, the odd-N path), "signal_bwf" (0 auto | 1 one-wave blocks | 4 the wide
  * panels' four barrier-free waves with buffer loads), "dec_merge" (1 the merged decile sweep on
- * ids, the general kernel for the rows it leaves | 0 the general kernel only), "dec_split" (1
- * wide rows on ids: the split pass -- plan, chunked sweep, finish | 0 the merged pass with one
- * workgroup per row; same labels and counts, means in another fixed order), "mj_reg"
+ * ids, the general kernel for the rows it leaves | 0 the general kernel only), "mj_reg"
  * (csm_momentum_multi: 2 register ring, two assets per lane | 1 one asset | 0 the LDS ring),
  * "dec_narrow_max" (widest row for the narrow-row decile kernels), "cohort_seg" / "cohort_lds"
  * (portfolio cohort-sum kernel: label-sorted segments (rows <= 7168) | per-wave LDS sums |
