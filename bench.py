@@ -76,6 +76,9 @@ def parse(argv=None):
                     help="C4 / C2: decile pass streams mom_J (k_deciles) instead of the bucket ids "
                          "the signal kernel (C4: csm_signal_ids) or the time-chunked scan (C2: "
                          "csm_momentum_chunked_ids) writes")
+    ap.add_argument("--no-fused-ls", action="store_true",
+                    help="C4 / C2 on ids: the long-short as its own launch (csm_long_short) "
+                         "instead of the decile pass's last workgroup (csm_deciles_ids_ls)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="C2: month chunks of the time-chunked scan (0 = Engine.default_chunks)")
     ap.add_argument("--match-dates", type=int, default=0,
@@ -355,10 +358,16 @@ def main(argv=None):
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     scan_name = (f"scan(k_momentum_chunked x{chunks}{' +ids' if narrow_ids else ''})" if chunks > 1
                  else "scan(k_momentum)")
-    stage_names = (["signal(k_signal+ids)", "deciles(k_deciles<ids>)", "long_short"] if use_ids else
+    # on ids the long-short is formed by the decile pass's last workgroup (csm_deciles_ids_ls)
+    fused_ls = (use_ids or narrow_ids) and not args.no_fused_ls
+    stage_names = (["signal(k_signal+ids)", "deciles+long_short(k_deciles<ids>)"] if use_ids and fused_ls else
+                   ["signal(k_signal+ids)", "deciles(k_deciles<ids>)", "long_short"] if use_ids else
                    ["signal(k_signal)", "deciles(k_deciles)", "long_short"] if fused else
                    ["month_end(k_month_end)", scan_name,
-                    "deciles(k_deciles<ids>)" if narrow_ids else "deciles(k_deciles)", "long_short"])
+                    "deciles+long_short(k_deciles<ids>)"] if narrow_ids and fused_ls else
+                   ["month_end(k_month_end)", scan_name, "deciles(k_deciles<ids>)", "long_short"]
+                   if narrow_ids else
+                   ["month_end(k_month_end)", scan_name, "deciles(k_deciles)", "long_short"])
     nst = len(stage_names) + 1
     step_events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst)]
                    for _ in range(args.steps)]
@@ -388,13 +397,18 @@ def main(argv=None):
                 eng.momentum(PM, J, skip, out=(None, M, NR))
         i += 1
         rec(ev[i])
-        if use_ids or narrow_ids:
+        if fused_ls:
+            eng.deciles_ids(M, NR, IDS, nb, out=(L, EW, CNT, None), LS=LS)
+        elif use_ids or narrow_ids:
             eng.deciles_ids(M, NR, IDS, nb, out=(L, EW, CNT, None))
+            i += 1
+            rec(ev[i])
+            eng.long_short(EW, CNT, LS)
         else:
             eng.deciles(M, NR, nb, out=(L, EW, CNT, None))
-        i += 1
-        rec(ev[i])
-        eng.long_short(EW, CNT, LS)
+            i += 1
+            rec(ev[i])
+            eng.long_short(EW, CNT, LS)
         rec(ev[i + 1])
         return LS
 
@@ -528,10 +542,11 @@ def main(argv=None):
             "hipgraph": graph is not None,
             "engine_path": (("speculative fused k_signal + k_shard_repair" if pipe.fused else
                              "k_month_end + carried k_momentum") if pipe is not None else
-                            "fused k_signal (+ bucket ids) -> k_deciles on ids" if use_ids else
+                            "fused k_signal (+ bucket ids) -> k_deciles on ids (+ long-short, one "
+                            "launch tail)" if use_ids else
                             "fused k_signal" if fused else
                             f"k_month_end + scan ({chunks} month chunks, + bucket ids) -> narrow "
-                            f"k_deciles on ids" if narrow_ids else
+                            f"k_deciles on ids (+ long-short in the same launch)" if narrow_ids else
                             f"k_month_end + scan ({chunks} month chunks)"),
             "config": {"workload": (cfg["name"] if args.assets is None and args.days is None
                                     else f"custom: {N} assets x {total_days} bdays") +

@@ -30,6 +30,8 @@ struct csm_ctx {
   int n_cu;               // compute units of the device (decile kernel choice)
   int32_t* dec_flg;       // [dec_flg_n] rows the merged decile pass left to the general kernel
   int32_t dec_flg_n;      // (allocated at create, so a captured pipeline never allocates)
+  int32_t* ticket;        // the fused long-short's arrival counter (zeroed at create; the last
+                          // workgroup of each decile launch resets it)
   void* comm;             // RCCL communicator of csm_allgather_init (collective.hip), or NULL
   int comm_rank, comm_size;
 };
@@ -129,15 +131,19 @@ void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, co
 
 // fused-pipeline decile launcher on the bucket ids of csm_signal_ids (deciles_pre.hip),
 // NB in {0,2,3,4,5,10,20}.  flg (T_m ints) non-NULL: the merged kernel first, then the general
-// kernel for the rows it left (flg[t] = 1); NULL: the general kernel only
+// kernel for the rows it left (flg[t] = 1); NULL: the general kernel only.  LS non-NULL (NB > 0,
+// with the context's ticket): the long-short by the general launch's last workgroup
 template <int NB>
 void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
-                        int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg);
+                        int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg, double* LS,
+                        int32_t* ticket);
 
-// the same on narrow rows (deciles_npre.hip: 2048 buckets = the fixed map's ids >> 2)
+// the same on narrow rows (deciles_npre.hip: 2048 buckets = the fixed map's ids >> 2); flg
+// non-NULL with decile sums: ONE launch, a row the merged pass gives up taking the general path
+// in the same workgroup
 template <int NB>
 void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                                int32_t* CNT, int32_t* NV, int64_t* tim, uint16_t* ids,
-                               int32_t* flg);
+                               int32_t* flg, double* LS, int32_t* ticket);

@@ -946,13 +946,23 @@ __global__ __launch_bounds__(256) void k_long_short(const double* __restrict__ E
   for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
     const double* e = EW + (int64_t)t * nb;
     const int32_t* c = CNT + (int64_t)t * nb;
+    int cv[MAXQ - 1];
+    double ev[MAXQ - 1];
+#pragma unroll
+    for (int d = 0; d < MAXQ - 1; ++d) {   // the row's counts and means, all loads in flight
+      cv[d] = d < nb ? c[d] : 0;
+      ev[d] = d < nb ? e[d] : 0.0;
+    }
     bool any = false;
-    double mx = -INFINITY, mn = INFINITY;
-    for (int d = 0; d < nb; ++d) {
-      if (c[d] > 0) { any = true; mx = fmax(mx, e[d]); mn = fmin(mn, e[d]); }
+    double mx = -INFINITY, mn = INFINITY, lo = 0.0, hi = 0.0;
+#pragma unroll
+    for (int d = 0; d < MAXQ - 1; ++d) {
+      if (cv[d] > 0) { any = true; mx = fmax(mx, ev[d]); mn = fmin(mn, ev[d]); }
+      if (d == 0) lo = ev[d];
+      if (d == nb - 1) hi = ev[d];
     }
     double v = qnan();
-    if (any) v = both ? (e[nb - 1] - e[0]) : (mx - mn);
+    if (any) v = both ? (hi - lo) : (mx - mn);
     LS[t] = v;
   }
 }
@@ -1453,16 +1463,30 @@ int csm_create(int device, csm_ctx** out) {
     free(c);
     return CSM_E_HIP;
   }
+  // the fused long-short's arrival counter: allocated and zeroed here, so a captured pipeline
+  // never allocates; each decile launch's last workgroup leaves it zero again
+  if (hipMalloc(&c->ticket, 256) != hipSuccess) {
+    (void)hipFree(c->dec_flg);
+    free(c);
+    return CSM_E_HIP;
+  }
+  if (hipMemset(c->ticket, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(c->ticket);
+    (void)hipFree(c->dec_flg);
+    free(c);
+    return CSM_E_HIP;
+  }
   *out = c;
   return CSM_OK;
 }
 
 int csm_destroy(csm_ctx* ctx) {
   if (ctx) (void)csm_allgather_free(ctx);
-  if (ctx && (ctx->scratch || ctx->dec_flg)) {
+  if (ctx && (ctx->scratch || ctx->dec_flg || ctx->ticket)) {
     (void)hipSetDevice(ctx->device);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->dec_flg) (void)hipFree(ctx->dec_flg);
+    if (ctx->ticket) (void)hipFree(ctx->ticket);
   }
   free(ctx);
   return CSM_OK;
@@ -1704,15 +1728,16 @@ template <int NB>
 static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
                            int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                            int32_t* CNT, int32_t* NV, uint16_t* ids, bool pre = false,
-                           int32_t* flg = nullptr) {
+                           int32_t* flg = nullptr, double* LS = nullptr,
+                           int32_t* ticket = nullptr) {
   int64_t* tm = g_dec_timing;
   if (pre) {   // ids written by csm_signal_ids / csm_momentum_multi_ids (fixed map): M is read only for a few cells
     if (N <= g_tune_dec_narrow_max)   // sweep rows: 2048 buckets (the fixed map's ids >> 2)
       launch_deciles_pre_narrow<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm, ids,
-                                    g_tune_dec_merge ? flg : nullptr);
+                                    g_tune_dec_merge ? flg : nullptr, LS, ticket);
     else
       launch_deciles_pre<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm, ids,
-                             g_tune_dec_merge ? flg : nullptr);
+                             g_tune_dec_merge ? flg : nullptr, LS, ticket);
     return;
   }
   if (N <= g_tune_dec_narrow_max) {   // rows of a few thousand assets (C2/C3/C5)
@@ -1773,7 +1798,13 @@ int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T
 static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
                             const double* M, const double* NR, int64_t N, int32_t n_bins,
                             const QTab& q, int8_t* L, double* EW, int32_t* CNT, int32_t* NV,
-                            uint16_t* ids, bool pre) {
+                            uint16_t* ids, bool pre, double* LS = nullptr) {
+  // LS (the ids path only): narrow rows form the long-short in the decile launch (its last
+  // workgroup); wide rows (C4) with k_long_short after it -- measured the same there
+  // (1.968 vs 1.971 ms/step), and the general kernel stays free of the per-workgroup fence
+  double* LSw = (LS && N > g_tune_dec_narrow_max) ? LS : nullptr;
+  if (LSw) LS = nullptr;
+  int32_t* tk = LS ? ctx->ticket : nullptr;
   int32_t* flg = nullptr;
   if (pre) {
     if (ctx->dec_flg_n < T_m) {   // beyond the create-time capacity
@@ -1793,17 +1824,21 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
     launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, pre, flg);
   } else {
     switch (n_bins) {
-      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
-      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
-      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
-      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
-      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
-      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg); break;
+      case 2: launch_deciles<2>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg, LS, tk); break;
+      case 3: launch_deciles<3>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg, LS, tk); break;
+      case 4: launch_deciles<4>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg, LS, tk); break;
+      case 5: launch_deciles<5>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg, LS, tk); break;
+      case 10: launch_deciles<10>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg, LS, tk); break;
+      case 20: launch_deciles<20>(v2, T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, ids, pre, flg, LS, tk); break;
       default:
         return set_err(ctx, CSM_E_INVAL, "%s: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", who, n_bins);
     }
   }
   LAUNCH_CHECK(ctx, who);
+  if (LSw) {
+    hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LSw);
+    LAUNCH_CHECK(ctx, "k_long_short");
+  }
   return CSM_OK;
 }
 
@@ -1830,6 +1865,25 @@ int csm_deciles_ids(csm_ctx* ctx, const double* M, const double* NR, const uint1
   for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
   return deciles_dispatch(ctx, "csm_deciles_ids", true, T_m, M, NR, N, n_bins, q, L, EW, CNT, NV,
                           const_cast<uint16_t*>(ids), true);
+}
+
+int csm_deciles_ids_ls(csm_ctx* ctx, const double* M, const double* NR, const uint16_t* ids,
+                       int32_t T_m, int64_t N, int32_t n_bins, const double* qtable, int8_t* L,
+                       double* EW, int32_t* CNT, int32_t* NV, double* LS) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!M || !NR || !EW || !CNT || !LS || !L || !qtable || N <= 0 || T_m < 0 || n_bins < 1 ||
+      n_bins > MAXQ - 1 || N > 0x7FFFFFFFLL)
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles_ids_ls: bad arguments (N=%lld T_m=%d n_bins=%d; "
+                   "NR, EW, CNT and LS required)", (long long)N, T_m, n_bins);
+  if (!ids_ok(N, M, NR, L, ids))
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles_ids_ls: needs N %% 4 == 0, 8-B aligned ids, 16-B "
+                   "aligned M / NR, 4-B aligned L (N=%lld)", (long long)N);
+  if (T_m == 0) return CSM_OK;
+  QTab q;
+  for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
+  return deciles_dispatch(ctx, "csm_deciles_ids_ls", true, T_m, M, NR, N, n_bins, q, L, EW, CNT,
+                          NV, const_cast<uint16_t*>(ids), true, LS);
 }
 
 int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const int64_t* month_start,
@@ -1871,9 +1925,10 @@ int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const in
   QTab q;
   for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
   const bool v2 = (N % 2 == 0) && aligned16(M) && aligned16(NR) && (((uintptr_t)L & 1u) == 0);
+  // the id path: labels, decile means and the long-short in one launch
   r = deciles_dispatch(ctx, "csm_pipeline", v2, T_m, M, NR, N, n_bins, q, L, EW, CNT, NV, ids,
-                       ids != nullptr);
-  if (r) return r;
+                       ids != nullptr, ids ? LS : nullptr);
+  if (r || ids) return r;
   hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
   LAUNCH_CHECK(ctx, "k_long_short");
   return CSM_OK;

@@ -21,21 +21,35 @@ template <int NB>
 void launch_deciles_pre_narrow(int T_m, hipStream_t st, const double* M, const double* NR,
                                int64_t N, int nbins, const QTab& q, int8_t* L, double* EW,
                                int32_t* CNT, int32_t* NV, int64_t* tim,
-                               uint16_t* ids, int32_t* flg) {
+                               uint16_t* ids, int32_t* flg, double* LS,
+                               int32_t* ticket) {
+  // with decile sums (C2): ONE launch -- a row the merged pass gives up takes the general path
+  // in the same workgroup, and LS (with the context's ticket) is formed by the last workgroup.
+  // Labels only (the sweeps, NB = 0): the merged kernel keeps its 8 workgroups per CU only
+  // without the general path beside it (64 VGPRs; with it the kernel spills), so the general
+  // kernel follows as its own launch for the rows the merged pass left (flg[t] = 1).
+  if constexpr (NB > 0) {
+    if (flg) {
+      hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, true, true>), dim3(T_m),
+                         dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
+                         ids, (int32_t*)nullptr, LS, ticket);
+      return;
+    }
+  }
   if (flg)
     hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, true>), dim3(T_m),
                        dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
-                       ids, flg);
+                       ids, flg, (double*)nullptr, (int32_t*)nullptr);
   hipLaunchKernelGGL((dec_npre::k_deciles<NB, true, true, false>), dim3(T_m),
                      dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
-                     ids, flg);
+                     ids, flg, LS, ticket);
 }
 
 #define INST(NB)                                                                              \
   template void launch_deciles_pre_narrow<NB>(int, hipStream_t, const double*, const double*,  \
                                               int64_t, int, const QTab&, int8_t*, double*,       \
                                               int32_t*, int32_t*, int64_t*, uint16_t*,       \
-                                              int32_t*);
+                                              int32_t*, double*, int32_t*);
 INST(0)
 INST(2)
 INST(3)

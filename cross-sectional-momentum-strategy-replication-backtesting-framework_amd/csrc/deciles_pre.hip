@@ -15,21 +15,26 @@ namespace dec_pre {
 template <int NB>
 void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
-                        int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg) {
-  if (flg)   // merged pass: one sweep of ids + next_ret per row (deciles.inc, MG)
+                        int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg, double* LS,
+                        int32_t* ticket) {
+  // merged pass first (flg): one sweep of ids + next_ret per row (deciles.inc, MG); then the
+  // general kernel takes the rows it left (all rows without flg) -- and, LS given, its last
+  // workgroup forms the long-short (csmom.hip launches k_long_short instead for these rows).
+  // (The merged pass with the general path as an in-workgroup fallback needs more than the 128
+  // VGPRs of two 512-thread workgroups per CU at this width.)
+  if (flg)
     hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, true>), dim3(T_m),
                        dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
-                       ids, flg);
-  // the general kernel: every row (flg NULL) or only the rows the merged pass left
+                       ids, flg, (double*)nullptr, (int32_t*)nullptr);
   hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, false>), dim3(T_m),
                      dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
-                     ids, flg);
+                     ids, flg, LS, ticket);
 }
 
 #define INST(NB)                                                                              \
   template void launch_deciles_pre<NB>(int, hipStream_t, const double*, const double*, int64_t, \
                                        int, const QTab&, int8_t*, double*, int32_t*, int32_t*,  \
-                                       int64_t*, uint16_t*, int32_t*);
+                                       int64_t*, uint16_t*, int32_t*, double*, int32_t*);
 INST(0)
 INST(2)
 INST(3)

@@ -301,10 +301,12 @@ class Engine:
                    _ptr(IDS))
         return PM, R, M, NR, IDS
 
-    def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False):
+    def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False, LS=None):
         """csm_deciles_ids: deciles() from the ids of signal_ids / momentum_multi(with_ids=True)
         (same labels / counts).  Rows of <= 16384 assets take the narrow kernel (2048 buckets:
-        the fixed map's ids >> 2), wider rows the 8192-bucket merged pass; needs N % 4 == 0."""
+        the fixed map's ids >> 2), wider rows the 8192-bucket merged pass; needs N % 4 == 0.
+        LS (float64 [T_m], needs NR): also the long-short of every date, in the same launch
+        (csm_deciles_ids_ls; equal to long_short(EW, CNT) bit for bit)."""
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)
         _need(IDS, "IDS", torch.int16, (T_m, N), self.device)
@@ -318,6 +320,14 @@ class Engine:
         else:
             L, EW, CNT, NV = out
         q = quantile_table(n_bins)
+        if LS is not None:
+            if NR is None:
+                raise ValueError("deciles_ids(LS=...) needs NR")
+            _need(LS, "LS", torch.float64, (T_m,), self.device)
+            self._call("csm_deciles_ids_ls", _ptr(M), _ptr(NR), _ptr(IDS), T_m, N, int(n_bins),
+                       q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV),
+                       _ptr(LS))
+            return L, EW, CNT, NV
         self._call("csm_deciles_ids", _ptr(M), _ptr(NR), _ptr(IDS), T_m, N, int(n_bins),
                    q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV))
         return L, EW, CNT, NV

@@ -206,6 +206,17 @@ int csm_deciles_ids(csm_ctx* ctx, const double* M, const double* NR, const uint1
                     double* EW, int32_t* CNT, int32_t* NV);
 
 /*
+ * csm_deciles_ids + csm_long_short in one call (run_demo.py:46-67).  Narrow rows (N <= 16384,
+ * C2): one launch, the decile pass's last workgroup forms LS[T_m] from every date's EW / CNT
+ * (the context's arrival counter; concurrent calls of one context on two streams are not
+ * supported).  Wider rows: the long-short kernel follows the decile pass.  NR, EW, CNT and LS
+ * are required; the same labels / EW / CNT / NV / LS bits as the two calls.
+ */
+int csm_deciles_ids_ls(csm_ctx* ctx, const double* M, const double* NR, const uint16_t* ids,
+                       int32_t T_m, int64_t N, int32_t n_bins, const double* qtable, int8_t* L,
+                       double* EW, int32_t* CNT, int32_t* NV, double* LS);
+
+/*
  * The whole K = 1 path of run_demo.py:31-67 in one call: fused month-end + scan (csm_signal,
  * with ids when N % 4 == 0 and the row is wide), per-date labels fused with the decile means
  * (csm_deciles / csm_deciles_ids), long-short (csm_long_short).  Arguments as in those calls

@@ -233,6 +233,46 @@ def test_deciles_ids_merged_equals_general(engine, tune_merge, case):
     assert max_rel(a, rEW) <= REL
 
 
+@pytest.mark.parametrize("N", [4_000, 20_000])   # narrow rows: one launch; wide: two
+@pytest.mark.parametrize("merge", [1, 0])
+def test_deciles_ids_fused_long_short(engine, tune_merge, N, merge):
+    """csm_deciles_ids_ls (run_demo.py:46-67 in one launch: the decile pass's last workgroup
+    forms the long-short) equals csm_deciles_ids + csm_long_short bit for bit, call after call
+    (the context's arrival counter resets itself), with the merged pass and without."""
+    pan = _panel(N=N, T=700, seed=N % 31 + merge)
+    ms_h = pan["month_start"]
+    P, ms = _up(pan["P"]), _up(ms_h)
+    _, _, M, NR, IDS = engine.signal_ids(P, ms, int(np.diff(ms_h).max()), 12, 1)
+    assert tune_merge(merge) == 0
+    L2, EW2, CNT2, NV2 = engine.deciles_ids(M, NR, IDS, 10, with_nv=True)
+    ref = engine.long_short(EW2, CNT2).cpu().numpy()
+    for _ in range(3):
+        LS = engine.empty((M.shape[0],))
+        L, EW, CNT, NV = engine.deciles_ids(M, NR, IDS, 10, with_nv=True, LS=LS)
+        assert torch.equal(L, L2) and torch.equal(CNT, CNT2) and torch.equal(NV, NV2)
+        assert bits_equal(EW.cpu().numpy(), EW2.cpu().numpy())
+        assert bits_equal(LS.cpu().numpy(), ref)
+    refL = O.assign_deciles(M.cpu().numpy(), 10)
+    _, _, LS_r = O.portfolio_ew(refL, NR.cpu().numpy(), 10)
+    assert np.array_equal(L.cpu().numpy(), refL) and max_rel(LS.cpu().numpy(), LS_r) <= REL
+
+
+@pytest.mark.parametrize("case", ["ties", "twoval", "wave_cluster", "lognormal_mild", "empty"])
+def test_narrow_fallback_rows_with_long_short(engine, case):
+    """Narrow rows the merged pass gives up (ties across edges, a list overflow) take the general
+    path in the same workgroup; the fused long-short still sees every row's means."""
+    rng = np.random.default_rng(5)
+    x = np.stack([_stress_row(case, n=8192), _stress_row("lognormal_mild", n=8192),
+                  _stress_row(case, n=8192)])
+    nr = rng.normal(0.01, 0.1, x.shape)
+    M, NR, IDS = _up(x), _up(nr), _ids_dev(x)
+    LS = engine.empty((3,))
+    L, EW, CNT, _ = engine.deciles_ids(M, NR, IDS, 10, LS=LS)
+    for r in range(3):
+        assert np.array_equal(L.cpu().numpy()[r], _oracle_labels(x[r])), (case, r)
+    assert bits_equal(LS.cpu().numpy(), engine.long_short(EW, CNT).cpu().numpy())
+
+
 def test_pipeline_deciles_repeatable(engine):
     """The wide-row decile pass on ids is deterministic (fixed summation order): two pipeline
     calls give the same bits; labels equal the oracle's on every date."""
