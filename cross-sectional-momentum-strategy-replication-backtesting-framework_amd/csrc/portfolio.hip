@@ -700,10 +700,14 @@ __device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INF
 // (bit 2q + leg: K non-empty cohorts in both windows).  TPv [rows][TP_STRIDE]: per leg
 // [inv_t, inv_{t-K_0..3}], then sk [q][leg].
 #define TP_STRIDE (2 * (TO_MAXQ + 1) + 2 * TO_MAXQ)
-__global__ __launch_bounds__(256) void k_turn_prep(const double* __restrict__ FWt, int T_m,
-                                                   int B, KSet ks, double* __restrict__ TPv,
-                                                   uint32_t* __restrict__ TPm) {
+#define TP_THREADS 64   // one thread per row: small grids, so 64-thread workgroups spread wide
+#define TP_U 16          // formation months' totals loaded together (all in flight)
+__global__ __launch_bounds__(TP_THREADS) void k_turn_prep(const double* __restrict__ FWt, int T_m,
+                                                          int B, KSet ks, double* __restrict__ TPv,
+                                                          uint32_t* __restrict__ TPm,
+                                                          int32_t* __restrict__ gen_count) {
   const int64_t tb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tb == 0 && gen_count) *gen_count = 0;   // the general-row work list, for the steady launch
   if (tb >= (int64_t)T_m * B) return;
   const int t = (int)(tb / B), b = (int)(tb - (int64_t)t * B);
   int kq = 0;
@@ -712,21 +716,32 @@ __global__ __launch_bounds__(256) void k_turn_prep(const double* __restrict__ FW
   double* tp = TPv + tb * TP_STRIDE;
 #pragma unroll
   for (int q = 0; q < TO_MAXQ; ++q) k1[q][0] = k1[q][1] = k0[q][0] = k0[q][1] = 0;
-  for (int j = 0; j <= kq; ++j) {
-    const int s = t - j;
+  for (int j0 = 0; j0 <= kq; j0 += TP_U) {
+    double fv[TP_U][2];
 #pragma unroll
-    for (int li = 0; li < 2; ++li) {
-      double tot = 0.0;
-      if (s >= 0) tot += FWt[((int64_t)s * B + b) * 2 + li];
-      const double v = tot > 0.0 ? 1.0 / tot : 0.0;
-      if (j == 0) tp[li * (TO_MAXQ + 1)] = v;
+    for (int u = 0; u < TP_U; ++u) {
+      const int s = t - (j0 + u);
+      const bool ok = j0 + u <= kq && s >= 0;
 #pragma unroll
-      for (int q = 0; q < TO_MAXQ; ++q) {
-        if (q >= ks.n) break;
-        const int K = ks.K[q];
-        if (j == K) tp[li * (TO_MAXQ + 1) + 1 + q] = v;
-        k1[q][li] += (j < K && v > 0.0) ? 1 : 0;
-        k0[q][li] += (j >= 1 && j <= K && t >= 1 && v > 0.0) ? 1 : 0;
+      for (int li = 0; li < 2; ++li) fv[u][li] = ok ? FWt[((int64_t)s * B + b) * 2 + li] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < TP_U; ++u) {
+      const int j = j0 + u;
+      if (j > kq) break;
+#pragma unroll
+      for (int li = 0; li < 2; ++li) {
+        const double tot = 0.0 + fv[u][li];
+        const double v = tot > 0.0 ? 1.0 / tot : 0.0;
+        if (j == 0) tp[li * (TO_MAXQ + 1)] = v;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {
+          if (q >= ks.n) break;
+          const int K = ks.K[q];
+          if (j == K) tp[li * (TO_MAXQ + 1) + 1 + q] = v;
+          k1[q][li] += (j < K && v > 0.0) ? 1 : 0;
+          k0[q][li] += (j >= 1 && j <= K && t >= 1 && v > 0.0) ? 1 : 0;
+        }
       }
     }
   }
@@ -1598,7 +1613,8 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   l.swr = 0;
   l.sw = cs;
   l.fw = 2 * cs;
-  l.fwt = l.fw + l.rows * l.p.C * 2;                       // [rows][2] folded totals
+  // [rows][2] folded totals; with one cohort chunk the partials ARE the totals (no fold launch)
+  l.fwt = l.p.C == 1 ? l.fw : l.fw + l.rows * l.p.C * 2;
   l.turn = l.fwt + l.rows * 2;                              // [TO_MAXQ][rows][Ct]
   l.cost = l.turn + (int64_t)TO_MAXQ * l.rows * l.p.Ct;
   l.bytes = (l.cost + (int64_t)TO_MAXQ * l.rows * l.p.Ct) * 8 + 256;
@@ -1683,9 +1699,11 @@ static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const do
       return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: n_bins=%d unsupported (2,3,4,5,10,20,30)", n_bins);
   }
   LAUNCH_CHECK(ctx, "k_cohort");
-  hipLaunchKernelGGL(k_fw_fold, dim3((unsigned)((2 * lay.rows + 255) / 256)), dim3(256), 0, st,
-                     (const double*)(ws + lay.fw), lay.rows, lay.p.C, ws + lay.fwt);
-  LAUNCH_CHECK(ctx, "k_fw_fold");
+  if (lay.p.C > 1) {
+    hipLaunchKernelGGL(k_fw_fold, dim3((unsigned)((2 * lay.rows + 255) / 256)), dim3(256), 0, st,
+                       (const double*)(ws + lay.fw), lay.rows, lay.p.C, ws + lay.fwt);
+    LAUNCH_CHECK(ctx, "k_fw_fold");
+  }
   return CSM_OK;
 }
 
@@ -1733,12 +1751,7 @@ int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const d
 #undef PJ_CASE
   }
   LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret)");
-  for (int q = 0; q < nJ; ++q) {
-    double* w = (double*)workspaces[q];
-    hipLaunchKernelGGL(k_fw_fold, dim3((unsigned)((2 * lay.rows + 255) / 256)), dim3(256), 0, st,
-                       (const double*)(w + lay.fw), lay.rows, lay.p.C, w + lay.fwt);
-  }
-  LAUNCH_CHECK(ctx, "k_fw_fold");
+  // (the shared path has one cohort chunk: each J's partials are its folded totals)
   return CSM_OK;
 }
 
@@ -1786,9 +1799,9 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
       // walks (C5 112.0 -> 108.9, C3 1.438 -> 1.405 ms/step against a second full grid)
       int32_t* gen_count = (int32_t*)((char*)workspace + lay.gen_b);
       int32_t* gen_list = gen_count + 1;
-      if (g_tune_gen_reset)
-        HIP_CHECK(ctx, zero_i32_async(gen_count, 1, st));
-      else
+      // the counter is reset by k_turn_prep's first thread (a kernel node, replay-safe), or --
+      // gen_reset 0, the diagnosis of tests/test_gpu_capture.py -- by hipMemsetAsync
+      if (!g_tune_gen_reset)
         HIP_CHECK(ctx, hipMemsetAsync(gen_count, 0, sizeof(int32_t), st));
       const unsigned gen_grid = (unsigned)std::min<int64_t>(nblk, g_tune_turn_gen_grid);
       // steady rows take their factors from k_turn_prep (no per-workgroup prologue: equal
@@ -1797,8 +1810,9 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
       double* TPv = prep ? (double*)((char*)workspace + lay.tp_b) : nullptr;
       uint32_t* TPm = prep ? (uint32_t*)((char*)workspace + lay.tpm_b) : nullptr;
       if (prep)
-        hipLaunchKernelGGL(k_turn_prep, dim3((unsigned)((lay.rows + 255) / 256)), dim3(256), 0, st,
-                           (const double*)(ws + lay.fwt), T_m, B, ks, TPv, TPm);
+        hipLaunchKernelGGL(k_turn_prep, dim3((unsigned)((lay.rows + TP_THREADS - 1) / TP_THREADS)),
+                           dim3(TP_THREADS), 0, st, (const double*)(ws + lay.fwt), T_m, B, ks, TPv,
+                           TPm, g_tune_gen_reset ? gen_count : (int32_t*)nullptr);
       for (int gen = 0; gen < 2; ++gen) {
         int kq = 0;
         for (int q = 0; q < ks.n; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;

@@ -204,6 +204,37 @@ def test_portfolio_multi_shares_cohort_pass(engine, vw):
             assert bits_equal(getattr(got, f).cpu().numpy(), getattr(one, f).cpu().numpy()), (K, f)
 
 
+@pytest.mark.parametrize("ncols", [500, 498, 497])
+@pytest.mark.parametrize("vw", [False, True])
+def test_turnover_cell_pairs_vs_oracle_and_per_k(engine, ncols, vw):
+    """Turnover / costs with square-root impact on rows of N % 4 == 0, 2 and odd N (the steady
+    rows' lanes take 4 or 1 cells and the general rows walk them the same way), through
+    k_turn_prep's factors: portfolio_multi over a K set equals per-K calls bit for bit (a row
+    switches between the steady and the general launch with the K set) and both match the
+    oracle."""
+    z = load_golden("c1")
+    PM, _ = engine.month_end(_up(np.ascontiguousarray(z["P"][:, :ncols])),
+                             _up(z["month_start"].astype(np.int64)))
+    _, M, NR = engine.momentum(PM, 12, 1)
+    L, _, _, _ = engine.deciles(M, None, 10)
+    rng = np.random.default_rng(ncols + vw)
+    T_m, N = L.shape
+    W = np.abs(PM.cpu().numpy()) * rng.uniform(1e5, 1e7, N) if vw else None
+    ADV = rng.uniform(1e5, 1e8, (T_m, N))
+    SIG = rng.uniform(0.005, 0.05, (T_m, N))
+    SIG[rng.random(SIG.shape) < 0.02] = np.nan
+    kw = dict(W=None if W is None else _up(W), aum=5e6, ADV=_up(ADV), SIG=_up(SIG))
+    multi = engine.portfolio_multi(L, NR, 10, Ks=(3, 6, 12), **kw)
+    for K in (3, 6, 12):
+        one = engine.portfolio(L, NR, 10, K=K, **kw)
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(multi[K], f).cpu().numpy(), getattr(one, f).cpu().numpy()), (K, f)
+        ref = PO.portfolio(L.cpu().numpy(), NR.cpu().numpy(), 10, K=K, W=W, aum=5e6, ADV=ADV,
+                           SIG=SIG)
+        for f in ("TURN", "COST", "NET", "LS"):
+            _close(getattr(one, f), ref[f], (K, f))
+
+
 _COHORT_MODES = {"seg": (1, 1), "lds": (0, 1), "reg": (0, 0)}   # (cohort_seg, cohort_lds)
 
 
