@@ -101,6 +101,9 @@ def parse(argv=None):
     ap.add_argument("--no-boot-scan", action="store_true",
                     help="C5: csm_bootstrap -> multi-J scan on materialised panels instead of "
                          "csm_boot_scan (the panel generated in registers, one shared next_ret)")
+    ap.add_argument("--no-grouped", action="store_true",
+                    help="C3 A/B: the joined look-backs' panels as side-by-side copies instead of "
+                         "the group-major portfolio calls (same bits)")
     ap.add_argument("--no-share-nr", action="store_true",
                     help="C5: each J's cohort pass reads the shared next_ret itself instead of one "
                          "pass staging each month's row for every J (csm_cohort_sums_js)")
@@ -607,10 +610,11 @@ class TimedStages:
         T_m, N = PM.shape
         return self._wrap("scan(k_momentum*)", 24.0 * N * T_m, self.eng.momentum, PM, J, skip, **k)
 
-    def momentum_multi(self, PM, Js, skip=1, with_ids=False, chunks=1):
+    def momentum_multi(self, PM, Js, skip=1, with_ids=False, chunks=1, stacked=False):
         T_m, N = PM.shape
         return self._wrap("scan(k_momentum*)", (8.0 + 16.0 * len(Js)) * N * T_m,
-                          self.eng.momentum_multi, PM, Js, skip, with_ids=with_ids, chunks=chunks)
+                          self.eng.momentum_multi, PM, Js, skip, with_ids=with_ids, chunks=chunks,
+                          stacked=stacked)
 
     def default_chunks(self, *a, **k):
         return self.eng.default_chunks(*a, **k)
@@ -637,6 +641,13 @@ class TimedStages:
             (8.0 if k.get("ADV") is not None else 0.0) + (8.0 if k.get("SIG") is not None else 0.0)
         return self._wrap("portfolio(k_cohort+k_turnover+k_overlap+k_ls)", per * T_m * BN,
                           self.eng.portfolio_multi, L, NR, n_bins, **k)
+
+    def portfolio_multi_grouped(self, Lg, NRg, n_bins=10, **k):
+        G, T_m, BgN = Lg.shape   # algorithmic: each group's labels + next_ret, the shared
+        per_w = sum(8.0 for x in ("W", "ADV", "SIG") if k.get(x) is not None)   # weights once
+        return self._wrap("portfolio(k_cohort+k_turnover+k_overlap+k_ls)",
+                          (9.0 * G + per_w) * T_m * BgN, self.eng.portfolio_multi_grouped, Lg,
+                          NRg, n_bins, **k)
 
     def portfolio_multi_js(self, Ls, NR, n_bins=10, **k):
         T_m, BN = NR.shape   # algorithmic: each J's labels, the shared next_ret once
@@ -723,7 +734,7 @@ def sweep_main(args):
     scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
                              multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids,
                              legs_only=not args.full_deciles, boot_scan=not args.no_boot_scan,
-                             share_nr=not args.no_share_nr)
+                             share_nr=not args.no_share_nr, grouped=not args.no_grouped)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":

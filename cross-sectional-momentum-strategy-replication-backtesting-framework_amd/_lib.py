@@ -77,6 +77,12 @@ SIGNATURES = {
     "csm_portfolio_from_cohorts_legs": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i64, _i32,
                                                        _i32, _i32, _p, _f64, _f64, _f64, _p,
                                                        _p, _p, _p, _p, _p, _p, _p, _p]),
+    "csm_cohort_sums_grouped": (ctypes.c_int, [_p, _i32, _p, _p, _p, _i32, _i32, _i64, _i32,
+                                               _i32, _i32, _p]),
+    "csm_portfolio_from_cohorts_grouped": (ctypes.c_int, [_p, _i32, _p, _p, _i32, _i32, _i64,
+                                                          _i32, _i32, _i32, _p, _f64, _f64, _f64,
+                                                          _p, _p, _p, _p, _p, _p, _p, _p, _i32,
+                                                          _p]),
     "csm_summary": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _f64, _p]),
     "csm_bootstrap": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i64, ctypes.c_uint64, _f64,
                                      _f64, _p, _p]),

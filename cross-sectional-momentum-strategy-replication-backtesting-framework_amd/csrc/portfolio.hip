@@ -51,6 +51,32 @@ __device__ __forceinline__ double member_w(int lab, int d, const double* W, int6
   return (w > 0.0 && w < INFINITY) ? w : 0.0;  // NaN fails w > 0
 }
 
+// Row addressing of a batch's input panels.  The B = G * Bg panels of a batch (row tb = t * B + b
+// of every workspace and output array) may hold their labels / next_ret group-major,
+// [G][T_m][Bg][N] -- G look-backs' label panels one block each, as the joined sweep's decile pass
+// writes them (no side-by-side copy) -- and their weights / ADV / vol once for all the groups,
+// [T_m][Bg][N] (no per-group copies).  The plain layout, [T_m][B][N] for both, is G = 1.
+struct PanAddr {
+  int B, Bg;        // panels of the batch, panels per group
+  int64_t N;
+  int64_t gl, ml;   // labels / next_ret: group stride, month stride (cells)
+  int64_t mw;       // weights / ADV / vol: month stride (one block for every group)
+  __host__ __device__ int64_t lrow(int t, int b) const {
+    const int g = b / Bg;
+    return (int64_t)g * gl + (int64_t)t * ml + (int64_t)(b - g * Bg) * N;
+  }
+  __host__ __device__ int64_t wrow(int t, int b) const {
+    const int g = b / Bg;
+    return (int64_t)t * mw + (int64_t)(b - g * Bg) * N;
+  }
+};
+static PanAddr pan_plain(int B, int64_t N) {
+  return PanAddr{B, B, N, 0, (int64_t)B * N, (int64_t)B * N};
+}
+static PanAddr pan_grouped(int G, int Bg, int T_m, int64_t N) {
+  return PanAddr{G * Bg, Bg, N, (int64_t)T_m * Bg * N, (int64_t)Bg * N, (int64_t)Bg * N};
+}
+
 // -------------------------------------------------------------------------------- E1
 // Cohort sums do not depend on the holding period: a pass with Kmax cohorts serves every
 // K <= Kmax (the sweep runs one pass per J for all its K).  Per-lane decile accumulators
@@ -60,7 +86,7 @@ template <int NB, bool VW>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort(
     const int8_t* __restrict__ L, const double* __restrict__ NR, const double* __restrict__ W,
     int T_m, int B, int64_t N, int K, int C, int64_t CH, int kpar, double* __restrict__ SWRp,
-    double* __restrict__ SWp, double* __restrict__ FWp) {
+    double* __restrict__ SWp, double* __restrict__ FWp, PanAddr pa) {
   __shared__ double red[PF_WAVES][2 * NB + 2];
   const int c = (int)(blockIdx.x % (unsigned)C);
   const int tb = (int)(blockIdx.x / (unsigned)C);
@@ -68,7 +94,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
-  const int64_t rt = ((int64_t)t * B + b) * N;
+  const int64_t rt = pa.lrow(t, b);
   const int k_lo = kpar ? (int)blockIdx.z : 0, k_hi = kpar ? k_lo + 1 : K;
   for (int k = k_lo; k < k_hi; ++k) {
     const int s = t - k;
@@ -77,7 +103,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
       if (tid < NB) { SWRp[ob + tid] = 0.0; SWp[ob + tid] = 0.0; }
       continue;
     }
-    const int64_t rs = ((int64_t)s * B + b) * N;
+    const int64_t rs = pa.lrow(s, b), rw = pa.wrow(s, b);
     double swr[NB], sw[NB];
     uint32_t cnt[NB];   // equal weight: the weight sum is a count
 #pragma unroll
@@ -95,7 +121,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
         const bool in = i < a1;
         lab[u] = in ? (int)L[rs + i] : -1;
         r[u] = in ? NR[rt + i] : 0.0;
-        if (VW) wx[u] = in ? W[rs + i] : 0.0;
+        if (VW) wx[u] = in ? W[rw + i] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < CU; ++u) {
@@ -156,7 +182,7 @@ template <int NB, bool VW>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
     const int8_t* __restrict__ L, const double* __restrict__ NR, const double* __restrict__ W,
     int T_m, int B, int64_t N, int K, int C, int64_t CH, double* __restrict__ SWRp,
-    double* __restrict__ SWp, double* __restrict__ FWp) {
+    double* __restrict__ SWp, double* __restrict__ FWp, PanAddr pa) {
   __shared__ double acc_r[PF_WAVES][AC_MAXKD];   // sum of w * r per (age, decile)
   __shared__ double acc_w[PF_WAVES][AC_MAXKD];   // sum of w (equal weight: the count)
   __shared__ double red[PF_WAVES][2];
@@ -168,13 +194,13 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
   for (int i = lane; i < KD; i += 64) { acc_r[wid][i] = 0.0; acc_w[wid][i] = 0.0; }
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
-  const int64_t rt = ((int64_t)t * B + b) * N;
+  const int64_t rt = pa.lrow(t, b), rtw = pa.wrow(t, b);
   const int kmax = t + 1 < K ? t + 1 : K;   // ages with a formation month s = t - k >= 0
   double ft = 0.0, fb = 0.0;
   double* ar = acc_r[wid];
   double* aw = acc_w[wid];
   __syncthreads();
-  const int64_t rowstep = (int64_t)B * N;   // one month back
+  const int64_t rowstep = pa.ml, rowstepw = pa.mw;   // one month back
   for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
     const double r = NR[rt + a];
     const bool rv = r == r;
@@ -188,7 +214,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
         const int k = k0 + u;
         const int64_t o = rt - (int64_t)k * rowstep + a;
         lab[u] = k < kmax ? (int)L[o] : -1;
-        if (VW) wx[u] = k < kmax ? W[o] : 0.0;
+        if (VW) wx[u] = k < kmax ? W[rtw - (int64_t)k * rowstepw + a] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
@@ -244,7 +270,7 @@ template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
     const int8_t* __restrict__ L, const double* __restrict__ W, int64_t N, int C,
     uint16_t* __restrict__ PERM, int32_t* __restrict__ OFF, double* __restrict__ WSRT,
-    double* __restrict__ FWp) {
+    double* __restrict__ FWp, PanAddr pa) {
   auto is_leg = [](int d) { return !LEGS || d == 0 || d == NB - 1; };
   const int64_t PS = seg_stride(N);
   // the row is staged in LDS first (all loads in flight at once), then both passes read LDS
@@ -254,8 +280,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
   __shared__ double red[PF_WAVES][2];
   const int64_t row = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int8_t* Lr = L + row * N;
-  const double* Wr = VW ? W + row * N : nullptr;
+  const int rt = (int)(row / pa.B), rb = (int)(row - (int64_t)rt * pa.B);
+  const int8_t* Lr = L + pa.lrow(rt, rb);
+  const double* Wr = VW ? W + pa.wrow(rt, rb) : nullptr;
   if (!VW && (N & 3) == 0) {   // 4-byte aligned rows: word loads
     const uint32_t* L4 = (const uint32_t*)Lr;
     uint32_t* l4 = (uint32_t*)ll;
@@ -388,12 +415,14 @@ __device__ __forceinline__ uint32_t byte_eq0(uint32_t z) {   // 0x80 in each byt
 template <int NB>
 __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
     const int8_t* __restrict__ L, int64_t N, int C, int64_t rows, uint16_t* __restrict__ PERM,
-    int32_t* __restrict__ OFF, double* __restrict__ FWp) {
+    int32_t* __restrict__ OFF, double* __restrict__ FWp, PanAddr pa) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * PF_WAVES + (threadIdx.x >> 6);
   if (row >= rows) return;   // no barriers below
   const int64_t PS = seg_stride(N);
-  const uint32_t* L4 = reinterpret_cast<const uint32_t*>(L + row * N);
+  const int rt0 = (int)(row / pa.B);
+  const uint32_t* L4 =
+      reinterpret_cast<const uint32_t*>(L + pa.lrow(rt0, (int)(row - (int64_t)rt0 * pa.B)));
   const int nw = (int)(N >> 2);
   const uint32_t topw = (uint32_t)(NB - 1) * 0x01010101u;
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -475,7 +504,7 @@ struct SegJ {
 template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const double* __restrict__ NR, SegJ sj, const double* __restrict__ WSRT, int T_m, int B,
-    int64_t N, int K, int C, int Cs, int xcd, int stage2) {
+    int64_t N, int K, int C, int Cs, int xcd, int stage2, PanAddr pa) {
   constexpr int ND = LEGS ? 2 : NB;   // segments per age
   auto dec_of = [](int e) { return LEGS ? (e ? NB - 1 : 0) : e; };
   // the return row of month t (N values), NaN at slot N
@@ -520,7 +549,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
       }
     return;
   }
-  const double* NRr = NR + tb * N;
+  const double* NRr = NR + pa.lrow(t, (int)(tb - (int64_t)t * B));
   for (int jq = 0; jq < sj.n; ++jq)
     for (int i = tid; i < kmax * OE; i += PF_THREADS) {
       const int k = i / OE, e = i - k * OE;
@@ -766,7 +795,8 @@ __device__ __forceinline__ void turnover_body(
     int Cf, int64_t CH, int Ct, double half_spread, double k_impact, double aum,
     const double* __restrict__ ADV, const double* __restrict__ SIG, double* __restrict__ TURNp,
     double* __restrict__ COSTp, int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count,
-    const double* __restrict__ TPv = nullptr, const uint32_t* __restrict__ TPm = nullptr) {
+    PanAddr pa, const double* __restrict__ TPv = nullptr,
+    const uint32_t* __restrict__ TPm = nullptr) {
   const int c = bid % Ct;
   const int tb = bid / Ct;
   const int rows = T_m * B;
@@ -804,8 +834,9 @@ __device__ __forceinline__ void turnover_body(
   }
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
-  const int64_t rt = ((int64_t)t * B + b) * N;
-  const int64_t rowstep = (int64_t)B * N;
+  // labels at rt (one month back: rowstep), weights / ADV / vol at rtw (rowstepw)
+  const int64_t rt = pa.lrow(t, b), rtw = pa.wrow(t, b);
+  const int64_t rowstep = pa.ml, rowstepw = pa.mw;
   const int nq = ks.n;
   const int dtop = n_bins - 1;
   // Equal weight (any cost model without impact): |w_t - w_{t-1}| of a cell in a full leg is
@@ -819,12 +850,16 @@ __device__ __forceinline__ void turnover_body(
   uint32_t s1 = 0, s0[TO_MAXQ], sb[TO_MAXQ];   // packed counts: leg 0 (top) low half, leg 1 high
 #pragma unroll
   for (int q = 0; q < TO_MAXQ; ++q) { turn[q] = 0.0; cost[q] = 0.0; s0[q] = 0; sb[q] = 0; }
-  auto charge = [&](int q, double dw, double adv, double unit_sig) {
+  // sra = sqrt(AUM / ADV) of the cell (< 0: no ADV, spread only), once per cell: the impact of
+  // a trade of dw is sqrt(dw) * sra, one square root per (q, leg) and no division (the same
+  // value as sqrt(dw * AUM / ADV) to a few ulps)
+  auto cell_sra = [&](double adv) { return (IMP && adv > 0.0) ? sqrt(aum / adv) : -1.0; };
+  auto charge = [&](int q, double dw, double sra, double unit_sig) {
     turn[q] += dw;
     if (IMP) {
       double unit = half_spread;
-      if (adv > 0.0) {
-        const double im = k_impact * unit_sig * sqrt(dw * aum / adv);
+      if (sra >= 0.0) {
+        const double im = k_impact * unit_sig * (sqrt(dw) * sra);
         unit = unit + ((im == im) ? im : 0.0);
       }
       cost[q] += dw * unit;
@@ -906,21 +941,22 @@ __device__ __forceinline__ void turnover_body(
         const int64_t a = i0 + (int64_t)u * PF_THREADS;
         const bool in = a < a1;
         l1[u] = in ? (int)L[rt + a] : -1;
-        x1[u] = (VW && in) ? W[rt + a] : 1.0;
+        x1[u] = (VW && in) ? W[rtw + a] : 1.0;
 #pragma unroll
         for (int q = 0; q < TO_MAXQ; ++q) {
           const bool use = in && q < nq;
-          const int64_t o = rt - (use ? (int64_t)ks.K[q] * rowstep : 0) + a;
-          l0[u][q] = use ? (int)L[o] : -1;
-          x0[u][q] = (VW && use) ? W[o] : 1.0;
+          const int64_t kq = use ? (int64_t)ks.K[q] : 0;
+          l0[u][q] = use ? (int)L[rt - kq * rowstep + a] : -1;
+          x0[u][q] = (VW && use) ? W[rtw - kq * rowstepw + a] : 1.0;
         }
-        adv[u] = (IMP && in) ? ADV[rt + a] : 0.0;
-        sg[u] = (IMP && SIG && in) ? SIG[rt + a] : 0.02;
+        adv[u] = (IMP && in) ? ADV[rtw + a] : 0.0;
+        sg[u] = (IMP && SIG && in) ? SIG[rtw + a] : 0.02;
       }
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
         const double vw1 = VW ? valid_w(x1[u]) : 1.0;
         const double unit_sig = sg[u] == sg[u] ? sg[u] : 0.02;
+        const double sra = cell_sra(adv[u]);
 #pragma unroll
         for (int q = 0; q < TO_MAXQ; ++q) {
           if (q >= nq) break;
@@ -930,7 +966,7 @@ __device__ __forceinline__ void turnover_body(
             const int d = li == 0 ? dtop : 0;
             const double w1 = (l1[u] == d ? vw1 : 0.0) * f1[li];
             const double w0 = (l0[u][q] == d ? vw0 : 0.0) * f0[q][li];
-            charge(q, fabs(w1 - w0) * fs[q][li], adv[u], unit_sig);
+            charge(q, fabs(w1 - w0) * fs[q][li], sra, unit_sig);
           }
         }
       }
@@ -1036,7 +1072,7 @@ __device__ __forceinline__ void turnover_body(
                   for (int q = 0; q < TO_MAXQ; ++q)
                     if ((cq >> (2 * q + li)) & 1u)
                       charge(q, fabs(sa[e][li] * sk[q][li][0] - (sz[e][li] + v) * sk[q][li][1]),
-                             0.0, 0.02);
+                             -1.0, 0.02);
                 }
                 sa[e][li] += v;
                 if (j >= 1) sz[e][li] += v;
@@ -1048,10 +1084,10 @@ __device__ __forceinline__ void turnover_body(
     } else if constexpr (!BM) {
     for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS)
     for (int64_t a = a4; a < a4 + cw && a < a1; ++a) {
-      double adv = 0.0, unit_sig = 0.02;
+      double sra = -1.0, unit_sig = 0.02;
       if (IMP) {
-        adv = ADV[rt + a];
-        if (SIG) { const double sg = SIG[rt + a]; unit_sig = (sg == sg) ? sg : 0.02; }
+        sra = cell_sra(ADV[rtw + a]);
+        if (SIG) { const double sg = SIG[rtw + a]; unit_sig = (sg == sg) ? sg : 0.02; }
       }
       double x1[TO_MAXQ][2], x0[TO_MAXQ][2], mK[TO_MAXQ][2], m0[2] = {0.0, 0.0};
       int lab0 = -1, labK[TO_MAXQ];
@@ -1068,9 +1104,9 @@ __device__ __forceinline__ void turnover_body(
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const bool ok = j0 + u <= jmax;
-        const int64_t o = rt - (int64_t)(ok ? j0 + u : 0) * rowstep + a;
-        labv[u] = ok ? (int)L[o] : -1;
-        wv[u] = (VW && ok) ? W[o] : 1.0;
+        const int64_t j = ok ? j0 + u : 0;
+        labv[u] = ok ? (int)L[rt - j * rowstep + a] : -1;
+        wv[u] = (VW && ok) ? W[rtw - j * rowstepw + a] : 1.0;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -1113,9 +1149,9 @@ __device__ __forceinline__ void turnover_body(
 #pragma unroll
         for (int li = 0; li < 2; ++li) {
           if (full[q][li]) {
-            if (!CNT) charge(q, fabs(m0[li] - mK[q][li]) * sk[q][li][0], adv, unit_sig);
+            if (!CNT) charge(q, fabs(m0[li] - mK[q][li]) * sk[q][li][0], sra, unit_sig);
           } else {
-            charge(q, fabs(x1[q][li] * sk[q][li][0] - x0[q][li] * sk[q][li][1]), adv,
+            charge(q, fabs(x1[q][li] * sk[q][li][0] - x0[q][li] * sk[q][li][1]), sra,
                    unit_sig);
           }
         }
@@ -1182,11 +1218,11 @@ __global__ __launch_bounds__(PF_THREADS, BM ? TO_MINB_BM : 1) void k_turnover(
     int Ct, double half_spread, double k_impact, double aum, const double* __restrict__ ADV,
     const double* __restrict__ SIG, double* __restrict__ TURNp, double* __restrict__ COSTp,
     int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count,
-    const double* __restrict__ TPv, const uint32_t* __restrict__ TPm) {
+    const double* __restrict__ TPv, const uint32_t* __restrict__ TPm, PanAddr pa) {
   if (!GEN) {
     turnover_body<VW, IMP, false>((int)blockIdx.x, L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH, Ct,
                                   half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp, gen_list,
-                                  gen_count, TPv, TPm);
+                                  gen_count, pa, TPv, TPm);
   } else {   // the general rows the steady launch put on the work list
     const int cap = T_m * B * Ct;                   // the list's capacity
     const int n0 = *(volatile int32_t*)gen_count;   // written by the previous launch
@@ -1194,7 +1230,7 @@ __global__ __launch_bounds__(PF_THREADS, BM ? TO_MINB_BM : 1) void k_turnover(
     for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
       turnover_body<VW, IMP, true, BM>(gen_list[i], L, W, FWp, T_m, B, N, ks, Kmax, n_bins, Cf, CH,
                                    Ct, half_spread, k_impact, aum, ADV, SIG, TURNp, COSTp,
-                                   gen_list, gen_count);
+                                   gen_list, gen_count, pa);
       __syncthreads();   // the shared tables are rebuilt for the next row
     }
   }
@@ -1490,7 +1526,7 @@ template <int NB>
 static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
                           const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
                           double* SWp, double* FWp, char* segws, int64_t perm_b, int64_t off_b,
-                          int64_t wsrt_b, bool legs = false) {
+                          int64_t wsrt_b, bool legs, const PanAddr& pa) {
   const dim3 g((unsigned)(pl.C * T_m * B), 1u, pl.kpar ? (unsigned)K : 1u);
   if (g_tune_cohort_seg && segws && !pl.kpar && K * (NB + 1) <= SEG_MAXKD) {
     uint16_t* PERM = (uint16_t*)(segws + perm_b);
@@ -1509,29 +1545,29 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     if (legs) {
       if (W) {
         hipLaunchKernelGGL((k_label_sort<NB, true, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N,
-                           pl.C, PERM, OFF, WSRT, FWp);
+                           pl.C, PERM, OFF, WSRT, FWp, pa);
         hipLaunchKernelGGL((k_cohort_seg<NB, true, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
+                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
       } else {
         if ((N & 3) == 0)   // one wave per row (C5's equal-weight legs)
           hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
-                             dim3(PF_THREADS), 0, st, L, N, pl.C, (int64_t)T_m * B, PERM, OFF, FWp);
+                             dim3(PF_THREADS), 0, st, L, N, pl.C, (int64_t)T_m * B, PERM, OFF, FWp, pa);
         else
           hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N,
-                             pl.C, PERM, OFF, WSRT, FWp);
+                             pl.C, PERM, OFF, WSRT, FWp, pa);
         hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
+                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
       }
     } else if (W) {
       hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
-                         PERM, OFF, WSRT, FWp);
+                         PERM, OFF, WSRT, FWp, pa);
       hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
+                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
     } else {
       hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N, pl.C,
-                         PERM, OFF, WSRT, FWp);
+                         PERM, OFF, WSRT, FWp, pa);
       hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1);
+                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
     }
     return;
   }
@@ -1539,18 +1575,18 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     const dim3 g2((unsigned)(pl.C * T_m * B));
     if (W)
       hipLaunchKernelGGL((k_cohort_lds<NB, true>), g2, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B,
-                         N, K, pl.C, pl.CH, SWRp, SWp, FWp);
+                         N, K, pl.C, pl.CH, SWRp, SWp, FWp, pa);
     else
       hipLaunchKernelGGL((k_cohort_lds<NB, false>), g2, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B,
-                         N, K, pl.C, pl.CH, SWRp, SWp, FWp);
+                         N, K, pl.C, pl.CH, SWRp, SWp, FWp, pa);
     return;
   }
   if (W)
     hipLaunchKernelGGL((k_cohort<NB, true>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
-                       pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp);
+                       pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp, pa);
   else
     hipLaunchKernelGGL((k_cohort<NB, false>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
-                       pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp);
+                       pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp, pa);
 }
 
 // Equal-weight cohort sums of nJ look-backs sharing one next_ret panel (segment path, one chunk
@@ -1565,6 +1601,7 @@ static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int
   const int xcd = B >= 8;
   const dim3 g1((unsigned)(T_m * B)),
       g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(T_m * B));
+  const PanAddr pa = pan_plain(B, N);
   SegJ sj;
   sj.n = nJ;
   for (int q = 0; q < nJ; ++q) {
@@ -1573,13 +1610,13 @@ static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int
     double* FWp = (double*)(ws[q] + fw_b);
     if (legs && (N & 3) == 0)
       hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
-                         dim3(PF_THREADS), 0, st, L[q], N, 1, (int64_t)T_m * B, PERM, OFF, FWp);
+                         dim3(PF_THREADS), 0, st, L[q], N, 1, (int64_t)T_m * B, PERM, OFF, FWp, pa);
     else if (legs)
       hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L[q],
-                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp);
+                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp, pa);
     else
       hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L[q],
-                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp);
+                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp, pa);
     sj.PERM[q] = PERM;
     sj.OFF[q] = OFF;
     sj.SWR[q] = (double*)(ws[q] + swr_b);
@@ -1589,10 +1626,10 @@ static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int
                      (legs ? (size_t)nJ * K * 4 * sizeof(uint16_t) : (size_t)nJ * K * (NB + 1) * sizeof(int32_t));
   if (legs)
     hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1);
+                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1, pa);
   else
     hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1);
+                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1, pa);
 }
 
 // Workspace layout of the cohort partials for (T_m, B, N, n_bins, Kmax): SWRp, SWp
@@ -1680,7 +1717,7 @@ int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bin
 
 static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,
                        int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
-                       void* workspace, bool legs) {
+                       void* workspace, bool legs, const PanAddr& pa) {
   int r = prep(ctx);
   if (r) return r;
   if (!L || !NR || !workspace || T_m < 0 || B < 1 || N <= 0 || Kmax < 1 || Kmax > TO_MAXK ||
@@ -1692,7 +1729,7 @@ static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const do
   double* ws = (double*)workspace;
   hipStream_t st = ctx->stream;
   switch (n_bins) {
-#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b, legs); break;
+#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b, legs, pa); break;
     PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20) PF_CASE(30)
 #undef PF_CASE
     default:
@@ -1709,7 +1746,7 @@ static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const do
 
 int csm_cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W, int32_t T_m,
                     int32_t B, int64_t N, int32_t n_bins, int32_t Kmax, void* workspace) {
-  return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, false);
+  return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, false, pan_plain(B, N));
 }
 
 int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const double* NR,
@@ -1737,7 +1774,8 @@ int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const d
                        n_bins == 20 || n_bins == 30);
   if (!shared) {
     for (int q = 0; q < nJ; ++q) {
-      r = cohort_sums(ctx, L[q], NR, nullptr, T_m, B, N, n_bins, Kmax, workspaces[q], legs != 0);
+      r = cohort_sums(ctx, L[q], NR, nullptr, T_m, B, N, n_bins, Kmax, workspaces[q], legs != 0,
+                      pan_plain(B, N));
       if (r) return r;
     }
     return CSM_OK;
@@ -1761,7 +1799,7 @@ int csm_cohort_sums_legs(csm_ctx* ctx, const int8_t* L, const double* NR, const 
   if (N > SEG_MAXN)
     return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_legs: rows of <= %d assets (N=%lld)", SEG_MAXN,
                    (long long)N);
-  return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, true);
+  return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, true, pan_plain(B, N));
 }
 
 static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W,
@@ -1770,7 +1808,7 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
                                   double half_spread, double k_impact, double aum,
                                   const double* ADV, const double* SIG, double* PR, double* LS,
                                   double* TURN, double* COST, double* NET, void* workspace,
-                                  bool legs, int32_t* need_full) {
+                                  bool legs, int32_t* need_full, const PanAddr& pa) {
   int r = prep(ctx);
   if (r) return r;
   bool ks_ok = Ks && nK >= 1;
@@ -1826,7 +1864,7 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
                            L, W, (const double*)(ws + lay.fwt), T_m, B, N, ks, Kmax, n_bins, 1,
                            lay.p.CHt, lay.p.Ct, half_spread, k_impact, aum, ADV, SIG,
                            ws + lay.turn, ws + lay.cost, gen_list, gen_count,
-                           (const double*)TPv, (const uint32_t*)TPm);
+                           (const double*)TPv, (const uint32_t*)TPm, pa);
       }
       LAUNCH_CHECK(ctx, "k_turnover");
       if (g_gen_probe) {
@@ -1868,7 +1906,8 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
                                      const double* ADV, const double* SIG, double* PR, double* LS,
                                      double* TURN, double* COST, double* NET, void* workspace) {
   return portfolio_from_cohorts(ctx, L, W, T_m, B, N, n_bins, Kmax, nK, Ks, half_spread, k_impact,
-                                aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace, false, nullptr);
+                                aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace, false, nullptr,
+                                pan_plain(B, N));
 }
 
 int csm_portfolio_from_cohorts_legs(csm_ctx* ctx, const int8_t* L, const double* W,
@@ -1881,7 +1920,33 @@ int csm_portfolio_from_cohorts_legs(csm_ctx* ctx, const int8_t* L, const double*
   if (!need_full)
     return set_err(ctx, CSM_E_INVAL, "csm_portfolio_from_cohorts_legs: need_full is required");
   return portfolio_from_cohorts(ctx, L, W, T_m, B, N, n_bins, Kmax, nK, Ks, half_spread, k_impact,
-                                aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace, true, need_full);
+                                aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace, true, need_full,
+                                pan_plain(B, N));
+}
+
+int csm_cohort_sums_grouped(csm_ctx* ctx, int32_t G, const int8_t* L, const double* NR,
+                            const double* W, int32_t T_m, int32_t Bg, int64_t N, int32_t n_bins,
+                            int32_t Kmax, int32_t legs, void* workspace) {
+  if (G < 1 || Bg < 1 || (int64_t)G * Bg > 0x7FFFFFFF || (legs && N > SEG_MAXN))
+    return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_grouped: bad arguments (G=%d Bg=%d N=%lld legs=%d;"
+                   " legs on rows of <= %d assets)", G, Bg, (long long)N, legs, SEG_MAXN);
+  return cohort_sums(ctx, L, NR, W, T_m, G * Bg, N, n_bins, Kmax, workspace, legs != 0,
+                     pan_grouped(G, Bg, T_m, N));
+}
+
+int csm_portfolio_from_cohorts_grouped(csm_ctx* ctx, int32_t G, const int8_t* L, const double* W,
+                                       int32_t T_m, int32_t Bg, int64_t N, int32_t n_bins,
+                                       int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                       double half_spread, double k_impact, double aum,
+                                       const double* ADV, const double* SIG, double* PR,
+                                       double* LS, double* TURN, double* COST, double* NET,
+                                       void* workspace, int32_t legs, int32_t* need_full) {
+  if (G < 1 || Bg < 1 || (int64_t)G * Bg > 0x7FFFFFFF || (legs && !need_full))
+    return set_err(ctx, CSM_E_INVAL, "csm_portfolio_from_cohorts_grouped: bad arguments (G=%d Bg=%d "
+                   "legs=%d; legs needs need_full)", G, Bg, legs);
+  return portfolio_from_cohorts(ctx, L, W, T_m, G * Bg, N, n_bins, Kmax, nK, Ks, half_spread,
+                                k_impact, aum, ADV, SIG, PR, LS, TURN, COST, NET, workspace,
+                                legs != 0, legs ? need_full : nullptr, pan_grouped(G, Bg, T_m, N));
 }
 
 int csm_portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W, int32_t T_m,

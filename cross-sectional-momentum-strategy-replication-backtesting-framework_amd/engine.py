@@ -177,26 +177,34 @@ class Engine:
                    _ptr(NR), _ptr(carry), _ptr(next_pm), _ptr(carry_out))
         return R, M, NR
 
-    def momentum_multi(self, PM, Js, skip=1, with_ids=False, chunks=1):
+    def momentum_multi(self, PM, Js, skip=1, with_ids=False, chunks=1, stacked=False):
         """csm_momentum_multi: one scan for several look-backs (up to 4 per launch).  Returns
         [(M, NR)] in the order of Js, each equal bit for bit to momentum(PM, J, skip).
         with_ids (csm_momentum_multi_ids): [(M, NR, IDS)], IDS the fixed-map bucket id of
         every mom_J (uint16 [T_m][N], read by deciles_ids on rows of any width).  chunks > 1
         (narrow panels; max(J) + skip <= 16, even N): the time-chunked multi-J scan
-        (csm_momentum_multi_chunked), the same bits."""
+        (csm_momentum_multi_chunked), the same bits.  stacked: each launch group's M / NR / IDS
+        are consecutive [T_m][N] blocks of one allocation (the joined sweep reads them as one
+        [nJ][T_m][N] tensor, no copy); otherwise one allocation per output, freed one by one."""
         T_m, N = PM.shape
         _need(PM, "PM", torch.float64, (T_m, N), self.device)
         Js = [int(J) for J in Js]
         outs = []
         for q0 in range(0, len(Js), 4):
             grp = Js[q0:q0 + 4]
-            Ms = [self.empty((T_m, N)) for _ in grp]
-            NRs = [self.empty((T_m, N)) for _ in grp]
+            if stacked:
+                Ms = list(self.empty((len(grp), T_m, N)))
+                NRs = list(self.empty((len(grp), T_m, N)))
+            else:
+                Ms = [self.empty((T_m, N)) for _ in grp]
+                NRs = [self.empty((T_m, N)) for _ in grp]
+            new_ids = ((lambda: list(self.empty((len(grp), T_m, N), torch.int16))) if stacked
+                       else (lambda: [self.empty((T_m, N), torch.int16) for _ in grp]))
             jarr = (ctypes.c_int32 * len(grp))(*grp)
             marr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in Ms])
             narr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in NRs])
             if chunks > 1:
-                IDs = [self.empty((T_m, N), torch.int16) for _ in grp] if with_ids else None
+                IDs = new_ids() if with_ids else None
                 iarr = ((ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in IDs])
                         if with_ids else None)
                 nbytes = int(self.lib.csm_momentum_multi_chunked_workspace(
@@ -206,7 +214,7 @@ class Engine:
                            int(skip), int(chunks), marr, narr, iarr, _ptr(ws))
                 outs.extend(zip(Ms, NRs, IDs) if with_ids else zip(Ms, NRs))
             elif with_ids:
-                IDs = [self.empty((T_m, N), torch.int16) for _ in grp]
+                IDs = new_ids()
                 iarr = (ctypes.c_void_p * len(grp))(*[t.data_ptr() for t in IDs])
                 self._call("csm_momentum_multi_ids", _ptr(PM), T_m, N, jarr, len(grp), int(skip),
                            marr, narr, iarr)
@@ -501,10 +509,55 @@ class Engine:
                                            with_costs, legs_only=False)
         return outs
 
+    def portfolio_multi_grouped(self, Lg, NRg, n_bins=10, Ks=(1,), W=None, Bg=1,
+                                half_spread=0.0005, k_impact=0.1, aum=0.0, ADV=None, SIG=None,
+                                with_costs=True, workspace=None, return_stacked=False,
+                                legs_only=False, need_full=None):
+        """portfolio_multi of B = G * Bg panels stored group-major (csm_cohort_sums_grouped ->
+        csm_portfolio_from_cohorts_grouped): Lg int8 / NRg f64 [G][T_m][Bg * N] (G blocks, e.g.
+        the look-backs' label panels as one stacked decile pass writes them) and W / ADV / SIG
+        [T_m][Bg * N] shared by the groups.  Outputs (panel g * Bg + p = group g's panel p) equal
+        portfolio_multi(cat(Lg, 1), cat(NRg, 1), ..., W.repeat(1, G), B=G * Bg) bit for bit,
+        without building those side-by-side copies."""
+        if Lg.dim() != 3:
+            raise ValueError("Lg must be [G][T_m][Bg * N]")
+        G, T_m, BgN = Lg.shape
+        if Bg < 1 or BgN % Bg:
+            raise ValueError(f"row width {BgN} is not Bg={Bg} panels")
+        N = BgN // Bg
+        B = G * Bg
+        _need(Lg, "Lg", torch.int8, (G, T_m, BgN), self.device)
+        _need(NRg, "NRg", torch.float64, (G, T_m, BgN), self.device)
+        for t, nm in ((W, "W"), (ADV, "ADV"), (SIG, "SIG")):
+            if t is not None:
+                _need(t, nm, torch.float64, (T_m, BgN), self.device)
+        Ks = [int(k) for k in Ks]
+        Kmax = max(Ks)
+        legs_only = bool(legs_only) and N <= LEGS_MAX_N
+        nbytes = int(self.lib.csm_portfolio_workspace(T_m, B, N, int(n_bins), Kmax))
+        if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
+            workspace = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
+        self._call("csm_cohort_sums_grouped", G, _ptr(Lg), _ptr(NRg), _ptr(W), T_m, int(Bg), N,
+                   int(n_bins), Kmax, 1 if legs_only else 0, _ptr(workspace))
+        flag = need_full
+        if legs_only and need_full is None:
+            flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        res, stacked = self._from_cohorts(Lg, W, T_m, B, N, n_bins, Ks, half_spread, k_impact,
+                                          aum, ADV, SIG, with_costs, workspace, legs_only, flag,
+                                          groups=(G, Bg))
+        if legs_only and need_full is None and int(flag.item()):   # a panel lacks a leg's column
+            return self.portfolio_multi_grouped(Lg, NRg, n_bins, Ks, W, Bg, half_spread, k_impact,
+                                                aum, ADV, SIG, with_costs, workspace,
+                                                return_stacked)
+        if return_stacked:
+            return res, stacked
+        return res
+
     def _from_cohorts(self, L, W, T_m, B, N, n_bins, Ks, half_spread, k_impact, aum, ADV, SIG,
-                      with_costs, workspace, legs_only, need_full):
+                      with_costs, workspace, legs_only, need_full, groups=None):
         """The accounting half of portfolio_multi on a workspace holding the cohort sums ->
-        (res {K: PortfolioOut}, stacked PortfolioOut)."""
+        (res {K: PortfolioOut}, stacked PortfolioOut).  groups=(G, Bg): the group-major layout
+        of portfolio_multi_grouped."""
         nK = len(Ks)
         Kmax = max(Ks)
         PR, LS = self.empty((nK, T_m, B, n_bins)), self.empty((nK, T_m, B))
@@ -516,7 +569,12 @@ class Engine:
                 ctypes.cast(ks, ctypes.c_void_p), float(half_spread), float(k_impact), float(aum),
                 _ptr(ADV), _ptr(SIG), _ptr(PR), _ptr(LS), _ptr(TURN), _ptr(COST), _ptr(NET),
                 _ptr(workspace))
-        if legs_only:
+        if groups is not None:
+            G, Bg = groups
+            gargs = (_ptr(L), _ptr(W), T_m, int(Bg)) + args[4:]
+            self._call("csm_portfolio_from_cohorts_grouped", int(G), *gargs,
+                       1 if legs_only else 0, _ptr(need_full) if legs_only else None)
+        elif legs_only:
             self._call("csm_portfolio_from_cohorts_legs", *args, _ptr(need_full))
         else:
             self._call("csm_portfolio_from_cohorts_multi", *args)

@@ -129,11 +129,28 @@ class SweepConfig:
     # bootstrap batches: the Js' cohort sums in one pass over the shared next_ret
     # (csm_cohort_sums_js: each month's return row read once for every J; same table bit for bit)
     share_nr: bool = True
+    # joined batches: the Js' labels / next_ret read group-major where the stacked scan and
+    # decile pass wrote them and the weights / ADV / vol once for every J
+    # (portfolio_multi_grouped); False: side-by-side copies (torch.cat / repeat) -- same bits
+    grouped: bool = True
     extra: dict = field(default_factory=dict)
 
     @property
     def strategies(self):
         return strategy_grid(self.Js, self.Ks)
+
+
+def _stacked(ts):
+    """The equal-shape tensors `ts` as one [len(ts)][...] tensor: a view when they already lie
+    back to back in one allocation (momentum_multi(stacked=True), slices of one stacked decile
+    pass), else a stacked copy."""
+    t0 = ts[0]
+    n = t0.numel() * t0.element_size()
+    if all(t.is_contiguous() and t.shape == t0.shape and t.dtype == t0.dtype
+           and t.device == t0.device and t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr()
+           and t.data_ptr() == t0.data_ptr() + i * n for i, t in enumerate(ts)):
+        return t0.as_strided((len(ts),) + tuple(t0.shape), (t0.numel(),) + tuple(t0.stride()))
+    return torch.stack(list(ts))
 
 
 class _JoinedSeries(Mapping):
@@ -256,14 +273,18 @@ class SweepRunner:
             if (c.multi_j_scan and hasattr(st, "momentum_multi") and len(c.Js) <= 4 and Cm > 1
                     and max(c.Js) + c.skip <= 16 and BN % 2 == 0):
                 ids = c.decile_ids and hasattr(st, "deciles_ids") and N % 4 == 0
-                MN = st.momentum_multi(PMb, c.Js, c.skip, with_ids=ids, chunks=Cm)
+                # (stacked: the Js' mom / next_ret / ids panels back to back, read below as one
+                # tensor each -- no concatenation copies)
+                MN = st.momentum_multi(PMb, c.Js, c.skip, with_ids=ids, chunks=Cm,
+                                       stacked=c.grouped)
             else:
                 ids = False
                 MN = [st.momentum(PMb, J, c.skip)[1:] for J in c.Js]
-            Mcat = torch.cat([mo[0].reshape(T_m * B, N) for mo in MN], 0)
+            Mcat = _stacked([mo[0] for mo in MN]).view(len(MN) * T_m * B, N)
             if ids:
-                Lcat, _, _, _ = st.deciles_ids(Mcat, None, torch.cat(
-                    [mo[2].reshape(T_m * B, N) for mo in MN], 0), c.n_bins)
+                Lcat, _, _, _ = st.deciles_ids(
+                    Mcat, None, _stacked([mo[2] for mo in MN]).view(len(MN) * T_m * B, N),
+                    c.n_bins)
             else:
                 Lcat, _, _, _ = st.deciles(Mcat, None, c.n_bins)
             R = T_m * B
@@ -346,15 +367,29 @@ class SweepRunner:
         per-J calls (one chunk plan for batches of up to four panels)."""
         c, st = self.cfg, self.st
         nJ = len(items)
-        rep = lambda X: None if X is None else X.repeat(1, nJ)
-        L = torch.cat([it[1] for it in items], dim=1)
-        NR = torch.cat([it[2] for it in items], dim=1)
-        kw = dict(W=rep(W), B=nJ * B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum,
-                  ADV=rep(ADV), SIG=rep(SIG), with_costs=c.costs)
-        if flag is not None:
-            kw.update(legs_only=True, need_full=flag)
-        outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)
-        del L, NR
+        if c.grouped and hasattr(st, "portfolio_multi_grouped"):
+            # the Js' label / next_ret panels group-major as the stacked decile pass and scan
+            # wrote them, weights / ADV / vol once for every J (csm_*_grouped: the same bits as
+            # the side-by-side copies below, without making them)
+            Lg = _stacked([it[1] for it in items])
+            NRg = _stacked([it[2] for it in items])
+            kw = dict(W=W, Bg=B, half_spread=c.half_spread, k_impact=c.k_impact, aum=c.aum,
+                      ADV=ADV, SIG=SIG, with_costs=c.costs)
+            if flag is not None:
+                kw.update(legs_only=True, need_full=flag)
+            outs, stk = st.portfolio_multi_grouped(Lg, NRg, c.n_bins, Ks=c.Ks, return_stacked=True,
+                                                   **kw)
+            del Lg, NRg
+        else:
+            rep = lambda X: None if X is None else X.repeat(1, nJ)
+            L = torch.cat([it[1] for it in items], dim=1)
+            NR = torch.cat([it[2] for it in items], dim=1)
+            kw = dict(W=rep(W), B=nJ * B, half_spread=c.half_spread, k_impact=c.k_impact,
+                      aum=c.aum, ADV=rep(ADV), SIG=rep(SIG), with_costs=c.costs)
+            if flag is not None:
+                kw.update(legs_only=True, need_full=flag)
+            outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)
+            del L, NR
         summ_all = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # [nK][nJ * B][F]
         Js = [it[0] for it in items]
         # per-(J, K) series: strided views of the joined outputs, built when read (C3's step is

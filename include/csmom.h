@@ -368,6 +368,28 @@ int csm_portfolio_from_cohorts_legs(csm_ctx* ctx, const int8_t* L, const double*
                                     int32_t* need_full);
 
 /*
+ * The cohort sums and accounting of B = G * Bg panels whose labels / next_ret are stored
+ * group-major -- L, NR [G][T_m][Bg][N]: G blocks, e.g. G look-backs' label panels as one decile
+ * pass over the stacked rows writes them -- and whose weights / ADV / vol are shared by the G
+ * groups -- W, ADV, SIG [T_m][Bg][N] (nullable as above).  Each call equals its plain-layout
+ * counterpart (csm_cohort_sums(_legs), csm_portfolio_from_cohorts_multi / _legs) on the
+ * side-by-side panels ([T_m][G * Bg][N], panel g * Bg + p = group g's panel p, weights repeated
+ * per group) bit for bit, outputs and workspace included (csm_portfolio_workspace(T_m, G * Bg,
+ * N, n_bins, Kmax) bytes; outputs [nK][T_m][G * Bg]), without those copies.  legs: 1 = the
+ * legs-only forms (rows of <= 7168 assets; need_full as csm_portfolio_from_cohorts_legs).
+ */
+int csm_cohort_sums_grouped(csm_ctx* ctx, int32_t G, const int8_t* L, const double* NR,
+                            const double* W, int32_t T_m, int32_t Bg, int64_t N, int32_t n_bins,
+                            int32_t Kmax, int32_t legs, void* workspace);
+int csm_portfolio_from_cohorts_grouped(csm_ctx* ctx, int32_t G, const int8_t* L, const double* W,
+                                       int32_t T_m, int32_t Bg, int64_t N, int32_t n_bins,
+                                       int32_t Kmax, int32_t nK, const int32_t* Ks,
+                                       double half_spread, double k_impact, double aum,
+                                       const double* ADV, const double* SIG, double* PR,
+                                       double* LS, double* TURN, double* COST, double* NET,
+                                       void* workspace, int32_t legs, int32_t* need_full);
+
+/*
  * Performance summary per (strategy, panel) of stacked long-short series (LS, and the
  * nullable-together TURN / COST / NET, each [nS][T_m][B]): out [nS][B][7] = months, mean,
  * Sharpe (src/utils.py:8-16 at `freq` periods a year, ddof = 1), mean turnover, mean cost,

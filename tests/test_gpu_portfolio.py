@@ -454,3 +454,44 @@ def test_overlap_rows_bit_identical(engine, B, legs, vw, Ks):
     for K in set(Ks):
         for f in ("PR", "LS", "TURN", "COST", "NET"):
             assert bits_equal(getattr(got[1][K], f).cpu().numpy(), getattr(got[0][K], f).cpu().numpy()), (K, f)
+
+
+@pytest.mark.parametrize("G,Bg,vw,legs,mode,ncols", [
+    (4, 1, True, True, "seg", 500), (4, 1, False, True, "seg", 500), (3, 2, True, False, "seg", 497),
+    (2, 3, False, False, "lds", 498), (4, 1, True, False, "reg", 500), (2, 2, True, True, "seg", 498)])
+def test_grouped_equals_side_by_side(engine, G, Bg, vw, legs, mode, ncols):
+    """csm_cohort_sums_grouped / csm_portfolio_from_cohorts_grouped (labels / next_ret
+    group-major [G][T_m][Bg * N], weights / ADV shared by the groups) give the plain-layout
+    accounting of the side-by-side panels (weights repeated per group) bit for bit: PR / LS /
+    TURN / COST / NET, every cohort kernel, legs-only and full, equal and value weights with
+    impact costs, row widths that are not a multiple of 4."""
+    z = load_golden("c1")
+    PM, _ = engine.month_end(_up(np.ascontiguousarray(z["P"][:, :ncols])),
+                             _up(z["month_start"].astype(np.int64)))
+    T_m, N = PM.shape
+    Lgs, NRgs = [], []
+    for g in range(G):   # group g: look-back 3 + 3g on Bg rolled copies of the panel
+        _, M, NR = engine.momentum(PM, 3 + 3 * g, 1)
+        L, _, _, _ = engine.deciles(M, None, 10)
+        roll = lambda x: np.stack([np.roll(x.cpu().numpy(), 5 * p, axis=1) for p in range(Bg)],
+                                  axis=1).reshape(T_m, Bg * N)
+        Lgs.append(roll(L))
+        NRgs.append(roll(NR))
+    rng = np.random.default_rng(G * 10 + Bg)
+    Wh = np.abs(np.stack([np.roll(PM.cpu().numpy(), 5 * p, axis=1) for p in range(Bg)], axis=1)
+                ).reshape(T_m, Bg * N) * rng.uniform(1e5, 1e7, Bg * N)
+    Wh[rng.random(Wh.shape) < 0.01] = np.nan
+    ADVh = rng.uniform(1e5, 1e8, (T_m, Bg * N))
+    W = _up(Wh) if vw else None
+    ADV = _up(ADVh)
+    kw = dict(Ks=(3, 6, 12), half_spread=0.0005, k_impact=0.1, aum=5e6, legs_only=legs)
+    grp = _with_cohort_mode(engine, mode, lambda: engine.portfolio_multi_grouped(
+        _up(np.stack(Lgs)), _up(np.stack(NRgs)), 10, W=W, Bg=Bg, ADV=ADV, **kw))
+    side = lambda xs: _up(np.concatenate(xs, axis=1))
+    plain = _with_cohort_mode(engine, mode, lambda: engine.portfolio_multi(
+        side(Lgs), side(NRgs), 10, W=None if W is None else _up(np.tile(Wh, (1, G))), B=G * Bg,
+        ADV=_up(np.tile(ADVh, (1, G))), **kw))
+    for K in (3, 6, 12):
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            a, b = getattr(grp[K], f).cpu().numpy(), getattr(plain[K], f).cpu().numpy()
+            assert a.shape == b.shape and bits_equal(a, b), (K, f)

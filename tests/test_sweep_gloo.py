@@ -191,3 +191,20 @@ def test_strategy_shards_single_process_is_run_batch():
     assert np.array_equal(np.isnan(a.numpy()), np.isnan(b.numpy()))
     m = ~np.isnan(b.numpy())
     assert np.array_equal(a.numpy()[m], b.numpy()[m])
+
+
+def test_stacked_view_or_copy():
+    """sweep._stacked: tensors lying back to back in one allocation come back as a view of it
+    (the joined sweep's group-major panels, no copy); any other list is stacked into a copy."""
+    from csmom.sweep import _stacked
+    base = torch.arange(24, dtype=torch.float64).reshape(3, 2, 4)
+    v = _stacked(list(base))
+    assert v.data_ptr() == base.data_ptr() and torch.equal(v, base)
+    parts = [torch.full((2, 4), float(i)) for i in range(3)]
+    c = _stacked(parts)
+    assert c.shape == (3, 2, 4) and all(torch.equal(c[i], parts[i]) for i in range(3))
+    out_of_order = _stacked([base[1], base[0]])
+    assert torch.equal(out_of_order, torch.stack([base[1], base[0]]))
+    assert out_of_order.data_ptr() != base.data_ptr()
+    flat = base.view(6, 4)   # slices of one stacked [rows][N] pass, reshaped
+    assert _stacked([flat[0:2], flat[2:4], flat[4:6]]).data_ptr() == base.data_ptr()
