@@ -1082,77 +1082,125 @@ __device__ __forceinline__ void turnover_body(
         }
       }
     } else if constexpr (!BM) {
-    for (int64_t a4 = a0 + cw * tid; a4 < a1; a4 += cw * PF_THREADS)
-    for (int64_t a = a4; a < a4 + cw && a < a1; ++a) {
-      double sra = -1.0, unit_sig = 0.02;
-      if (IMP) {
-        sra = cell_sra(ADV[rtw + a]);
-        if (SIG) { const double sg = SIG[rtw + a]; unit_sig = (sg == sg) ? sg : 0.02; }
-      }
-      double x1[TO_MAXQ][2], x0[TO_MAXQ][2], mK[TO_MAXQ][2], m0[2] = {0.0, 0.0};
-      int lab0 = -1, labK[TO_MAXQ];
+    // ages whose cohort is empty on both legs add 0.0 to every sum (inv 0.0) and make neither
+    // leg full, so their loads are skipped; a row with no cohort formed yet (a panel's first
+    // months) has all sums zero and skips its cells (exact: every skipped term is +0.0)
+    uint64_t amask = ~0ull;
+    if (jmax < 64) {
+      amask = 0;
+      for (int j = 0; j <= jmax; ++j)
+        amask |= (inv[0][j] != 0.0 || inv[1][j] != 0.0) ? 1ull << j : 0ull;
+    }
+    auto live = [&](int j) { return j >= 64 || ((amask >> j) & 1ull); };
+    // cell k of this lane, in the steady paths' order
+    auto cell = [&](int k) -> int64_t {
+      return cw == 1 ? a0 + tid + (int64_t)k * PF_THREADS
+                     : a0 + 4 * tid + (int64_t)(k >> 2) * 4 * PF_THREADS + (k & 3);
+    };
+    // CC cells of the lane at a time, all their age loads in flight together.  Each age's
+    // member weights go into running sums over ages >= 0 (sa) and >= 1 (sz): x1 of pair q is sa
+    // before age K_q and x0 is sz after it -- the same ascending-age additions as one
+    // accumulator per q -- so q is charged at age K_q (after the last age when K_q > jmax),
+    // cell by cell: every turn[q] / cost[q] receives its terms in the same order as before.
+    constexpr int CC = 2;
+    for (int k = 0; amask && cell(k) < a1; k += CC) {
+      int64_t ac[CC];
+      bool on[CC];
+      double sra[CC], usig[CC], sa[CC][2], sz[CC][2], m0[CC][2];
+      int lab0[CC], labK[CC][TO_MAXQ];
 #pragma unroll
-      for (int q = 0; q < TO_MAXQ; ++q) {
-        labK[q] = -1;
+      for (int c = 0; c < CC; ++c) {
+        ac[c] = cell(k + c);
+        on[c] = ac[c] < a1;
+        sra[c] = -1.0;
+        usig[c] = 0.02;
+        if (IMP && on[c]) {
+          sra[c] = cell_sra(ADV[rtw + ac[c]]);
+          if (SIG) { const double sg = SIG[rtw + ac[c]]; usig[c] = (sg == sg) ? sg : 0.02; }
+        }
+        lab0[c] = -1;
 #pragma unroll
-        for (int li = 0; li < 2; ++li) { x1[q][li] = 0.0; x0[q][li] = 0.0; mK[q][li] = 0.0; }
+        for (int li = 0; li < 2; ++li) { sa[c][li] = 0.0; sz[c][li] = 0.0; m0[c][li] = 0.0; }
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) labK[c][q] = -1;
       }
-      // ages in trips of 8: the trip's label and weight loads are all in flight before use
       for (int j0 = 0; j0 <= jmax; j0 += 8) {
-      int labv[8];
-      double wv[8];
+        int labv[CC][8];
+        double wv[CC][8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const bool ok = j0 + u <= jmax;
-        const int64_t j = ok ? j0 + u : 0;
-        labv[u] = ok ? (int)L[rt - j * rowstep + a] : -1;
-        wv[u] = (VW && ok) ? W[rtw - j * rowstepw + a] : 1.0;
-      }
+        for (int c = 0; c < CC; ++c)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = j0 + u;
-        if (j > jmax) break;
-        const double i0 = inv[0][j], i1 = inv[1][j];
-        if (i0 == 0.0 && i1 == 0.0) continue;
-        const int lab = labv[u];
-        const double w = VW ? valid_w(wv[u]) : 1.0;
-        const double m[2] = {lab == dtop ? w * i0 : 0.0, lab == 0 ? w * i1 : 0.0};
-        if (j == 0) { m0[0] = m[0]; m0[1] = m[1]; lab0 = lab; }
+          for (int u = 0; u < 8; ++u) {
+            const bool ok = on[c] && j0 + u <= jmax && live(j0 + u);
+            const int64_t j = ok ? j0 + u : 0;
+            labv[c][u] = ok ? (int)L[rt - j * rowstep + ac[c]] : -1;
+            wv[c][u] = (VW && ok) ? W[rtw - j * rowstepw + ac[c]] : 1.0;
+          }
 #pragma unroll
-        for (int q = 0; q < TO_MAXQ; ++q) {
-          if (q >= nq) break;
-          const int K = ks.K[q];
-          if (j == K) labK[q] = lab;
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + u;
+          if (j > jmax) break;
+          const double i0 = inv[0][j], i1 = inv[1][j];
+          uint32_t cq = 0;   // pairs charged at this age
 #pragma unroll
-          for (int li = 0; li < 2; ++li) {
-            if (j < K) x1[q][li] += m[li];
-            if (j >= 1 && j <= K) x0[q][li] += m[li];
-            if (j == K) mK[q][li] = m[li];
+          for (int q = 0; q < TO_MAXQ; ++q) cq |= (q < nq && ks.K[q] == j) ? 1u << q : 0u;
+#pragma unroll
+          for (int c = 0; c < CC; ++c) {
+            const int lab = labv[c][u];   // -1 for a dead age: m = 0, as if skipped
+            const double w = VW ? valid_w(wv[c][u]) : 1.0;
+            const double m[2] = {lab == dtop ? w * i0 : 0.0, lab == 0 ? w * i1 : 0.0};
+            if (j == 0) { m0[c][0] = m[0]; m0[c][1] = m[1]; lab0[c] = lab; }
+            if (cq) {
+#pragma unroll
+              for (int q = 0; q < TO_MAXQ; ++q) {
+                if (!((cq >> q) & 1u)) continue;
+                if (CNT) labK[c][q] = lab;
+                if (!on[c]) continue;
+#pragma unroll
+                for (int li = 0; li < 2; ++li) {
+                  if (full[q][li]) {
+                    if (!CNT) charge(q, fabs(m0[c][li] - m[li]) * sk[q][li][0], sra[c], usig[c]);
+                  } else {
+                    charge(q, fabs(sa[c][li] * sk[q][li][0] - (sz[c][li] + m[li]) * sk[q][li][1]),
+                           sra[c], usig[c]);
+                  }
+                }
+              }
+            }
+#pragma unroll
+            for (int li = 0; li < 2; ++li) {
+              sa[c][li] += m[li];
+              if (j >= 1) sz[c][li] += m[li];
+            }
           }
         }
       }
-      }
-      if (CNT) {
-        const uint32_t e1 = (lab0 == dtop ? 1u : 0u) | (lab0 == 0 ? 0x10000u : 0u);
-        s1 += e1;
 #pragma unroll
-        for (int q = 0; q < TO_MAXQ; ++q) {
+      for (int c = 0; c < CC; ++c) {
+        if (!on[c]) continue;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q) {   // windows reaching past the first month
           if (q >= nq) break;
-          const uint32_t e0 = (labK[q] == dtop ? 1u : 0u) | (labK[q] == 0 ? 0x10000u : 0u);
-          s0[q] += e0;
-          sb[q] += e1 & e0;
+          if (ks.K[q] <= jmax) continue;
+#pragma unroll
+          for (int li = 0; li < 2; ++li) {
+            if (full[q][li]) {
+              if (!CNT) charge(q, fabs(m0[c][li] - 0.0) * sk[q][li][0], sra[c], usig[c]);
+            } else {
+              charge(q, fabs(sa[c][li] * sk[q][li][0] - sz[c][li] * sk[q][li][1]), sra[c],
+                     usig[c]);
+            }
+          }
         }
-      }
+        if (CNT) {
+          const uint32_t e1 = (lab0[c] == dtop ? 1u : 0u) | (lab0[c] == 0 ? 0x10000u : 0u);
+          s1 += e1;
 #pragma unroll
-      for (int q = 0; q < TO_MAXQ; ++q) {
-        if (q >= nq) break;
-#pragma unroll
-        for (int li = 0; li < 2; ++li) {
-          if (full[q][li]) {
-            if (!CNT) charge(q, fabs(m0[li] - mK[q][li]) * sk[q][li][0], sra, unit_sig);
-          } else {
-            charge(q, fabs(x1[q][li] * sk[q][li][0] - x0[q][li] * sk[q][li][1]), sra,
-                   unit_sig);
+          for (int q = 0; q < TO_MAXQ; ++q) {
+            if (q >= nq) break;
+            const uint32_t e0 = (labK[c][q] == dtop ? 1u : 0u) | (labK[c][q] == 0 ? 0x10000u : 0u);
+            s0[q] += e0;
+            sb[q] += e1 & e0;
           }
         }
       }
