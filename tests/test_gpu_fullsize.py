@@ -228,15 +228,19 @@ def test_c5_shape_and_finite(c5):
     assert np.isfinite(summ[..., :3]).all()
 
 
-@pytest.mark.parametrize("b", [0, 57, 99])
+@pytest.mark.parametrize("b", [0, 7, 13, 29, 42, 57, 64, 86, 93, 99])
 def test_c5_sampled_panels_vs_oracle(c5, b):
+    """Ten of the batch's 100 bootstrap panels: every (J, K) summary row against the oracle
+    stages within north_star's 1e-10 relative (fp64 sums in another order; months exact)."""
     cfg, R0, summ = c5
     ref = _oracle_panel_summary(cfg, R0.cpu().numpy(), b)
     got = summ[b]
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     assert np.array_equal(got[:, 0], ref[:, 0])                 # months per strategy
     m = ~np.isnan(ref)
-    assert np.allclose(got[m], ref[m], rtol=1e-9, atol=1e-13), b
+    scale = np.maximum(np.abs(ref[m]), 1e-12)
+    err = np.abs(got[m] - ref[m]) / scale
+    assert err.max() <= 1e-10, (b, float(err.max()))
 
 
 def test_c5_boot_scan_equals_materialised(engine, c5):
