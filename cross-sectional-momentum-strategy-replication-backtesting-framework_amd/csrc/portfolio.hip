@@ -1254,6 +1254,130 @@ __device__ __forceinline__ void turnover_body(
   }
 }
 
+// Steady value-weight rows of the G = B / Bg panels that share one weight row (the grouped
+// layout: G look-backs of one panel, TO_MAXG at most): one workgroup per (month t, weight panel
+// p, chunk c) serves the G rows (t, g * Bg + p).  A cell's weights of months t and t - K_q and
+// its ADV / vol are loaded once for all G rows, its labels per row; each row's charges go to
+// its own accumulators in exactly the per-row launch's order (a lane's cells in order, then q,
+// then leg), and each row is reduced by the per-row launch's tree -- its TURN / COST partials
+// are the same bits.  Rows that are not all-full go onto the general launch's work list as the
+// per-row launch's ids (tb * Ct + c).
+#define TO_MAXG 4
+template <bool IMP>
+__global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
+    const int8_t* __restrict__ L, const double* __restrict__ W, int T_m, int B, int64_t N,
+    KSet ks, int n_bins, int64_t CH, int Ct, double half_spread, double k_impact, double aum,
+    const double* __restrict__ ADV, const double* __restrict__ SIG, double* __restrict__ TURNp,
+    double* __restrict__ COSTp, int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count,
+    const double* __restrict__ TPv, const uint32_t* __restrict__ TPm, PanAddr pa) {
+  const int Bg = pa.Bg, G = B / Bg;
+  const int c = (int)(blockIdx.x % (unsigned)Ct);
+  const int tp = (int)(blockIdx.x / (unsigned)Ct);
+  const int t = tp / Bg, p = tp - t * Bg;
+  const int rows = T_m * B;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nq = ks.n;
+  const uint32_t need = (1u << (2 * nq)) - 1u;   // bit 2q + leg
+  uint32_t act = 0;                              // this workgroup's steady rows (bit g)
+#pragma unroll
+  for (int g = 0; g < TO_MAXG; ++g) {
+    if (g >= G) break;
+    const int tb = t * B + g * Bg + p;
+    if ((TPm[tb] & need) == need) act |= 1u << g;
+    else if (gen_list && tid == 0) {   // the general launch's row (bounded like the per-row launch)
+      const int slot = atomicAdd(gen_count, 1);
+      if (slot < rows * Ct) gen_list[slot] = tb * Ct + c;
+    }
+  }
+  if (!act) return;
+  const int64_t a0 = (int64_t)c * CH;
+  const int64_t a1 = a0 + CH < N ? a0 + CH : N;
+  const int64_t rtw = (int64_t)t * pa.mw + (int64_t)p * N;   // pa.wrow(t, g * Bg + p), every g
+  const int dtop = n_bins - 1;
+  double turn[TO_MAXG][TO_MAXQ], cost[TO_MAXG][TO_MAXQ];
+#pragma unroll
+  for (int g = 0; g < TO_MAXG; ++g)
+#pragma unroll
+    for (int q = 0; q < TO_MAXQ; ++q) { turn[g][q] = 0.0; cost[g][q] = 0.0; }
+  for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
+    // every load of the cell first: weights / ADV / vol once, then each row's labels
+    double x1, x0[TO_MAXQ], adv = 0.0, sg = 0.02;
+    int l1[TO_MAXG], l0[TO_MAXG][TO_MAXQ];
+    x1 = W[rtw + a];
+#pragma unroll
+    for (int q = 0; q < TO_MAXQ; ++q)
+      x0[q] = q < nq ? W[rtw - (int64_t)ks.K[q] * pa.mw + a] : 1.0;
+    if (IMP) {
+      adv = ADV[rtw + a];
+      if (SIG) sg = SIG[rtw + a];
+    }
+#pragma unroll
+    for (int g = 0; g < TO_MAXG; ++g) {
+      const bool on = g < G && ((act >> g) & 1u);
+      const int64_t rt = pa.lrow(t, g * Bg + p);
+      l1[g] = on ? (int)L[rt + a] : -1;
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q)
+        l0[g][q] = (on && q < nq) ? (int)L[rt - (int64_t)ks.K[q] * pa.ml + a] : -1;
+    }
+    const double vw1 = valid_w(x1);
+    const double unit_sig = sg == sg ? sg : 0.02;
+    const double sra = (IMP && adv > 0.0) ? sqrt(aum / adv) : -1.0;
+#pragma unroll
+    for (int g = 0; g < TO_MAXG; ++g) {
+      if (g >= G || !((act >> g) & 1u)) continue;
+      const double* tpv = TPv + (int64_t)(t * B + g * Bg + p) * TP_STRIDE;
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q) {
+        if (q >= nq) break;
+        const double vw0 = valid_w(x0[q]);
+#pragma unroll
+        for (int li = 0; li < 2; ++li) {
+          const int d = li == 0 ? dtop : 0;
+          const double f1 = tpv[li * (TO_MAXQ + 1)];
+          const double f0 = tpv[li * (TO_MAXQ + 1) + 1 + q];
+          const double fs = tpv[2 * (TO_MAXQ + 1) + 2 * q + li];
+          const double w1 = (l1[g] == d ? vw1 : 0.0) * f1;
+          const double w0 = (l0[g][q] == d ? vw0 : 0.0) * f0;
+          const double dw = fabs(w1 - w0) * fs;
+          turn[g][q] += dw;
+          if (IMP) {   // turnover_body's charge, term for term
+            double unit = half_spread;
+            if (sra >= 0.0) {
+              const double im = k_impact * unit_sig * (sqrt(dw) * sra);
+              unit = unit + ((im == im) ? im : 0.0);
+            }
+            cost[g][q] += dw * unit;
+          }
+        }
+      }
+    }
+  }
+  __shared__ double red[TO_MAXG][PF_WAVES][2 * TO_MAXQ];
+#pragma unroll
+  for (int g = 0; g < TO_MAXG; ++g) {
+    if (g >= G || !((act >> g) & 1u)) continue;
+#pragma unroll
+    for (int q = 0; q < TO_MAXQ; ++q) {
+      if (q >= nq) break;
+      const double x1 = wave_sum(turn[g][q]);
+      const double y1 = IMP ? wave_sum(cost[g][q]) : 0.0;
+      if (lane == 0) { red[g][wid][2 * q] = x1; red[g][wid][2 * q + 1] = y1; }
+    }
+  }
+  __syncthreads();
+  if (tid < TO_MAXG * TO_MAXQ) {
+    const int g = tid / TO_MAXQ, q = tid - g * TO_MAXQ;
+    if (g < G && ((act >> g) & 1u) && q < nq) {
+      const int tb = t * B + g * Bg + p;
+      double x = 0.0, y = 0.0;
+      for (int w2 = 0; w2 < PF_WAVES; ++w2) { x += red[g][w2][2 * q]; y += red[g][w2][2 * q + 1]; }
+      TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.5 * x;
+      COSTp[((int64_t)q * rows + tb) * Ct + c] = IMP ? y : x * half_spread;
+    }
+  }
+}
+
 // BM (general launch, equal weight, every K <= 31): only the bit-mask path is compiled, so the
 // kernel keeps the registers of that path (the dense path's arrays would double them).
 template <bool VW, bool IMP, bool GEN, bool BM = false>
@@ -1507,6 +1631,9 @@ static int g_tune_overlap_rows = 1;
 // hipMemsetAsync, round 3's form), and an optional device int32 that receives the counter the
 // general launch read (csm_tune_ptr("gen_probe")).  Neither changes a result.
 static int g_tune_gen_reset = 1;
+// 1: grouped batches' steady value-weight rows by k_turnover_vwg (a weight panel's groups in one
+// workgroup) | 0 by the per-row launch (A/B; the same bits)
+static int g_tune_turn_vwg = 1;
 static int32_t* g_gen_probe = nullptr;
 
 __global__ void k_copy_i32(const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
@@ -1747,6 +1874,10 @@ int csm_tune_portfolio(const char* key, int value) {
     g_tune_gen_reset = value;
     return CSM_OK;
   }
+  if (key && !strcmp(key, "turn_vwg") && (value == 0 || value == 1)) {
+    g_tune_turn_vwg = value;
+    return CSM_OK;
+  }
   return CSM_E_INVAL;
 }
 
@@ -1908,6 +2039,16 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
                                                                 : k_turnover<false, false, true>)))
                         : (W ? (imp ? k_turnover<true, true, false> : k_turnover<true, false, false>)
                              : (imp ? k_turnover<false, true, false> : k_turnover<false, false, false>));
+        // value weights shared by the groups of a grouped batch: the steady rows of a weight
+        // panel's G groups in one workgroup (weights / ADV loaded once for them)
+        if (!gen && W && g_tune_turn_vwg && pa.Bg < pa.B && pa.B / pa.Bg <= TO_MAXG) {
+          hipLaunchKernelGGL(imp ? k_turnover_vwg<true> : k_turnover_vwg<false>,
+                             dim3((unsigned)((int64_t)T_m * pa.Bg * lay.p.Ct)), dim3(PF_THREADS), 0,
+                             st, L, W, T_m, B, N, ks, n_bins, lay.p.CHt, lay.p.Ct, half_spread,
+                             k_impact, aum, ADV, SIG, ws + lay.turn, ws + lay.cost, gen_list,
+                             gen_count, (const double*)TPv, (const uint32_t*)TPm, pa);
+          continue;
+        }
         hipLaunchKernelGGL(kern, dim3(gen ? gen_grid : (unsigned)nblk), dim3(PF_THREADS), 0, st,
                            L, W, (const double*)(ws + lay.fwt), T_m, B, N, ks, Kmax, n_bins, 1,
                            lay.p.CHt, lay.p.Ct, half_spread, k_impact, aum, ADV, SIG,

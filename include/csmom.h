@@ -53,7 +53,9 @@ int csm_abi_version(void);
  * default 8192), "overlap_rows" (1 one thread per (month, panel, decile) for single-chunk
  * plans | 0 one per (K, month, panel, decile)), "gen_reset" (1 the turnover work-list counter
  * reset by a kernel | 0 by hipMemsetAsync, round 3's form, kept for the graph-replay diagnosis
- * of tests/test_gpu_capture.py).  Returns CSM_E_INVAL for an unknown key or value. */
+ * of tests/test_gpu_capture.py), "turn_vwg" (1 a grouped batch's steady value-weight turnover
+ * rows by one workgroup per weight panel | 0 one per row).  Returns CSM_E_INVAL for an unknown
+ * key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aids: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
  * wall-clock ticks (100 MHz) at its phase boundaries; "gen_probe" = device int32 that receives

@@ -75,7 +75,7 @@ def test_tune_keys_documented_in_header_are_accepted():
              b"dec_merge": ([0, 1], 1), b"dec_narrow_max": ([0, 16384], 16384),
              b"mj_reg": ([0, 1, 2], 2), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
-             b"turn_gen_grid": ([1, 2048], 8192), b"gen_reset": ([0, 1], 1)}
+             b"turn_gen_grid": ([1, 2048], 8192), b"gen_reset": ([0, 1], 1), b"turn_vwg": ([0, 1], 1)}
     for key, (vals, default) in cases.items():
         for v in vals:
             assert lib.csm_tune(key, v) == 0, (key, v)
