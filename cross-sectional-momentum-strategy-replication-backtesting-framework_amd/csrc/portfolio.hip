@@ -731,10 +731,16 @@ __device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INF
 #define TP_STRIDE (2 * (TO_MAXQ + 1) + 2 * TO_MAXQ)
 #define TP_THREADS 64   // one thread per row: small grids, so 64-thread workgroups spread wide
 #define TP_U 16          // formation months' totals loaded together (all in flight)
+// TPm bit: no cohort of the row's windows has a member (a panel's first months).  Every charge
+// of such a row is +0.0, so k_turn_prep writes its TURN / COST partials (0.0, the bits the
+// general launch would write) and neither turnover launch takes the row.
+#define TP_EMPTY 0x80000000u
 __global__ __launch_bounds__(TP_THREADS) void k_turn_prep(const double* __restrict__ FWt, int T_m,
                                                           int B, KSet ks, double* __restrict__ TPv,
                                                           uint32_t* __restrict__ TPm,
-                                                          int32_t* __restrict__ gen_count) {
+                                                          int32_t* __restrict__ gen_count,
+                                                          int Ct, double* __restrict__ TURNp,
+                                                          double* __restrict__ COSTp) {
   const int64_t tb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (tb == 0 && gen_count) *gen_count = 0;   // the general-row work list, for the steady launch
   if (tb >= (int64_t)T_m * B) return;
@@ -784,6 +790,21 @@ __global__ __launch_bounds__(TP_THREADS) void k_turn_prep(const double* __restri
       tp[2 * (TO_MAXQ + 1) + 2 * q + li] = k1[q][li] > 0 ? 1.0 / (double)k1[q][li] : 0.0;
       m |= (k1[q][li] == K && k0[q][li] == K) ? (1u << (2 * q + li)) : 0u;
     }
+  }
+  // a member in some formation month of the windows: the windows of the longest K cover every
+  // age 0..kq (month t's ages 0..K-1, month t-1's 1..K)
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < TO_MAXQ; ++q)
+    if (q < ks.n) any = any || k1[q][0] > 0 || k1[q][1] > 0 || k0[q][0] > 0 || k0[q][1] > 0;
+  if (!any && TURNp) {
+    m = TP_EMPTY;
+    const int64_t rows = (int64_t)T_m * B;
+    for (int q = 0; q < ks.n; ++q)
+      for (int c = 0; c < Ct; ++c) {
+        TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.0;
+        COSTp[((int64_t)q * rows + tb) * Ct + c] = 0.0;
+      }
   }
   TPm[tb] = m;
 }
@@ -868,6 +889,7 @@ __device__ __forceinline__ void turnover_body(
   bool all_full = true;
   if (pre) {
     const uint32_t need = (1u << (2 * nq)) - 1u;   // bit 2q + leg
+    if (TPm[tb] & TP_EMPTY) return;   // k_turn_prep wrote its partials
     all_full = (TPm[tb] & need) == need;
   } else {
     for (int q = 0; q < nq; ++q) all_full = all_full && full[q][0] && full[q][1];
@@ -1283,7 +1305,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
   for (int g = 0; g < TO_MAXG; ++g) {
     if (g >= G) break;
     const int tb = t * B + g * Bg + p;
-    if ((TPm[tb] & need) == need) act |= 1u << g;
+    const uint32_t m = TPm[tb];
+    if (m & TP_EMPTY) continue;   // k_turn_prep wrote its partials
+    if ((m & need) == need) act |= 1u << g;
     else if (gen_list && tid == 0) {   // the general launch's row (bounded like the per-row launch)
       const int slot = atomicAdd(gen_count, 1);
       if (slot < rows * Ct) gen_list[slot] = tb * Ct + c;
@@ -2029,7 +2053,8 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
       if (prep)
         hipLaunchKernelGGL(k_turn_prep, dim3((unsigned)((lay.rows + TP_THREADS - 1) / TP_THREADS)),
                            dim3(TP_THREADS), 0, st, (const double*)(ws + lay.fwt), T_m, B, ks, TPv,
-                           TPm, g_tune_gen_reset ? gen_count : (int32_t*)nullptr);
+                           TPm, g_tune_gen_reset ? gen_count : (int32_t*)nullptr, lay.p.Ct,
+                           ws + lay.turn, ws + lay.cost);
       for (int gen = 0; gen < 2; ++gen) {
         int kq = 0;
         for (int q = 0; q < ks.n; ++q) kq = ks.K[q] > kq ? ks.K[q] : kq;
