@@ -80,7 +80,7 @@ def parse(argv=None):
                     help="C4 / C2 on ids: the long-short as its own launch (csm_long_short) "
                          "instead of the decile pass's last workgroup (csm_deciles_ids_ls)")
     ap.add_argument("--chunks", type=int, default=0,
-                    help="C2: month chunks of the time-chunked scan (0 = Engine.default_chunks)")
+                    help="C2 / C3: month chunks of the time-chunked scan (0 = Engine.default_chunks)")
     ap.add_argument("--match-dates", type=int, default=0,
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -734,7 +734,8 @@ def sweep_main(args):
     scfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8,
                              multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids,
                              legs_only=not args.full_deciles, boot_scan=not args.no_boot_scan,
-                             share_nr=not args.no_share_nr, grouped=not args.no_grouped)
+                             share_nr=not args.no_share_nr, grouped=not args.no_grouped,
+                             scan_chunks=args.chunks or 0)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)
     if args.config == "c3":

@@ -133,6 +133,9 @@ class SweepConfig:
     # decile pass wrote them and the weights / ADV / vol once for every J
     # (portfolio_multi_grouped); False: side-by-side copies (torch.cat / repeat) -- same bits
     grouped: bool = True
+    # joined batches: month chunks of the time-chunked multi-J scan (0: Engine.default_chunks;
+    # any count gives the same bits -- the fold chains through every earlier chunk)
+    scan_chunks: int = 0
     extra: dict = field(default_factory=dict)
 
     @property
@@ -269,7 +272,8 @@ class SweepRunner:
         if self._joined(T_m, B):
             # every J from one time-chunked scan where it applies (csm_momentum_multi_chunked:
             # C3 scan 0.245 ms for four chunked scans), with the bucket ids for the decile pass
-            Cm = st.default_chunks(T_m, BN, max(c.Js), c.skip) if hasattr(st, "default_chunks") else 1
+            Cm = (c.scan_chunks or st.default_chunks(T_m, BN, max(c.Js), c.skip)
+                  if hasattr(st, "default_chunks") else 1)
             if (c.multi_j_scan and hasattr(st, "momentum_multi") and len(c.Js) <= 4 and Cm > 1
                     and max(c.Js) + c.skip <= 16 and BN % 2 == 0):
                 ids = c.decile_ids and hasattr(st, "deciles_ids") and N % 4 == 0
