@@ -725,9 +725,12 @@ __device__ __forceinline__ double valid_w(double x) { return (x > 0.0 && x < INF
 // Per-row turnover factors for the steady equal-weight launch, computed once per row instead
 // of in every workgroup's prologue (two barriers and a dependent load round each): one thread
 // per row (t, b) forms, with the prologue's own arithmetic, inv_s = 1 / (leg total of the
-// cohort formed at s) for s = t and s = t - K_q, sk = 1 / K_u of month t, and the full-leg mask
-// (bit 2q + leg: K non-empty cohorts in both windows).  TPv [rows][TP_STRIDE]: per leg
-// [inv_t, inv_{t-K_0..3}], then sk [q][leg].
+// cohort formed at s) for s = t and s = t - K_q, sk = 1 / K_u of month t, and the telescoping
+// mask (bit 2q + leg: the windows of months t and t - 1 hold as many non-empty cohorts, K_t ==
+// K_{t-1} -- both full, or an empty formation month inside both -- so w_t - w_{t-1} =
+// (omega_t - omega_{t-K}) / K_t: the common cohorts cancel, and only the month-t and month t-K
+// labels enter, as in every steady row; month t - K must exist, t >= K).
+// TPv [rows][TP_STRIDE]: per leg [inv_t, inv_{t-K_0..3}], then sk [q][leg].
 #define TP_STRIDE (2 * (TO_MAXQ + 1) + 2 * TO_MAXQ)
 #define TP_THREADS 64   // one thread per row: small grids, so 64-thread workgroups spread wide
 #define TP_U 16          // formation months' totals loaded together (all in flight)
@@ -784,11 +787,11 @@ __global__ __launch_bounds__(TP_THREADS) void k_turn_prep(const double* __restri
 #pragma unroll
   for (int q = 0; q < TO_MAXQ; ++q) {
     if (q >= ks.n) break;
-    const int K = ks.K[q];
+    const bool has_tk = t >= ks.K[q];   // month t - K exists: the steady rows read its labels
 #pragma unroll
     for (int li = 0; li < 2; ++li) {
       tp[2 * (TO_MAXQ + 1) + 2 * q + li] = k1[q][li] > 0 ? 1.0 / (double)k1[q][li] : 0.0;
-      m |= (k1[q][li] == K && k0[q][li] == K) ? (1u << (2 * q + li)) : 0u;
+      m |= (has_tk && k1[q][li] == k0[q][li]) ? (1u << (2 * q + li)) : 0u;
     }
   }
   // a member in some formation month of the windows: the windows of the longest K cover every
@@ -849,7 +852,7 @@ __device__ __forceinline__ void turnover_body(
     for (int j = 1; j <= K; ++j) k0 += (t >= 1 && inv[li][j] > 0.0) ? 1 : 0;        // month t-1
     sk[q][li][0] = k1 > 0 ? 1.0 / (double)k1 : 0.0;
     sk[q][li][1] = k0 > 0 ? 1.0 / (double)k0 : 0.0;
-    full[q][li] = (k1 == K && k0 == K) ? 1 : 0;
+    full[q][li] = (t >= K && k1 == k0) ? 1 : 0;   // telescoping (k_turn_prep's mask bit)
   }
   __syncthreads();
   }
