@@ -104,6 +104,9 @@ def parse(argv=None):
     ap.add_argument("--no-grouped", action="store_true",
                     help="C3 A/B: the joined look-backs' panels as side-by-side copies instead of "
                          "the group-major portfolio calls (same bits)")
+    ap.add_argument("--no-legs-labels", action="store_true",
+                    help="C3/C5 A/B: exact interior deciles in the decile pass instead of the legs "
+                         "mode before legs-only accounting (same table bit for bit)")
     ap.add_argument("--no-share-nr", action="store_true",
                     help="C5: each J's cohort pass reads the shared next_ret itself instead of one "
                          "pass staging each month's row for every J (csm_cohort_sums_js)")
@@ -735,6 +738,7 @@ def sweep_main(args):
                              multi_j_scan=not args.per_j_scan, decile_ids=not args.no_decile_ids,
                              legs_only=not args.full_deciles, boot_scan=not args.no_boot_scan,
                              share_nr=not args.no_share_nr, grouped=not args.no_grouped,
+                             legs_labels=not args.no_legs_labels,
                              scan_chunks=args.chunks or 0)
     S = len(scfg.strategies)
     runner = csmom.SweepRunner(ts, scfg)

@@ -115,6 +115,7 @@ SIGNATURES = {
     "csm_deciles_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),
     "csm_deciles_ids_ls": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p,
                                           _p]),
+    "csm_deciles_ids_legs": (ctypes.c_int, [_p, _p, _p, _i32, _i64, _i32, _p, _p, _p]),
     "csm_pipeline": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _i32,
                                     _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "csm_comm_unique_id": (ctypes.c_int, [_p]),

@@ -98,6 +98,9 @@ __device__ __forceinline__ void dec_mark(int64_t* tim, int t, int ph) {
 }
 struct QTab {
   double q[MAXQ];
+  // legs mode (csm_deciles_ids_legs; labels-only merged pass, n_bins >= 4): only the first and
+  // last decile are exact -- every other ranked cell gets some label in [1, n_bins - 2]
+  int legs = 0;
 };
 
 // Fixed bucket map of the fused pipeline (csm_signal_ids writes one u16 id per asset-month,

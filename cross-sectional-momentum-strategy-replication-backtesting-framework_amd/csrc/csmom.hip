@@ -1868,6 +1868,24 @@ int csm_deciles_ids(csm_ctx* ctx, const double* M, const double* NR, const uint1
                           const_cast<uint16_t*>(ids), true);
 }
 
+int csm_deciles_ids_legs(csm_ctx* ctx, const double* M, const uint16_t* ids, int32_t T_m,
+                         int64_t N, int32_t n_bins, const double* qtable, int8_t* L, int32_t* NV) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!M || !L || !qtable || N <= 0 || T_m < 0 || n_bins < 1 || n_bins > MAXQ - 1 || N > 0x7FFFFFFFLL)
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles_ids_legs: bad arguments (N=%lld T_m=%d n_bins=%d)",
+                   (long long)N, T_m, n_bins);
+  if (!ids_ok(N, M, nullptr, L, ids))
+    return set_err(ctx, CSM_E_INVAL, "csm_deciles_ids_legs: needs N %% 4 == 0, 8-B aligned ids, "
+                   "16-B aligned M, 4-B aligned L (N=%lld)", (long long)N);
+  if (T_m == 0) return CSM_OK;
+  QTab q;
+  for (int i = 0; i < MAXQ; ++i) q.q[i] = i <= n_bins ? qtable[i] : 1.0;
+  q.legs = 1;
+  return deciles_dispatch(ctx, "csm_deciles_ids_legs", true, T_m, M, nullptr, N, n_bins, q, L,
+                          nullptr, nullptr, NV, const_cast<uint16_t*>(ids), true);
+}
+
 int csm_deciles_ids_ls(csm_ctx* ctx, const double* M, const double* NR, const uint16_t* ids,
                        int32_t T_m, int64_t N, int32_t n_bins, const double* qtable, int8_t* L,
                        double* EW, int32_t* CNT, int32_t* NV, double* LS) {

@@ -309,12 +309,14 @@ class Engine:
                    _ptr(IDS))
         return PM, R, M, NR, IDS
 
-    def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False, LS=None):
+    def deciles_ids(self, M, NR, IDS, n_bins=10, out=None, with_nv=False, LS=None, legs=False):
         """csm_deciles_ids: deciles() from the ids of signal_ids / momentum_multi(with_ids=True)
         (same labels / counts).  Rows of <= 16384 assets take the narrow kernel (2048 buckets:
         the fixed map's ids >> 2), wider rows the 8192-bucket merged pass; needs N % 4 == 0.
         LS (float64 [T_m], needs NR): also the long-short of every date, in the same launch
-        (csm_deciles_ids_ls; equal to long_short(EW, CNT) bit for bit)."""
+        (csm_deciles_ids_ls; equal to long_short(EW, CNT) bit for bit).
+        legs=True (NR None; for legs-only accounting): csm_deciles_ids_legs -- labels 0,
+        n_bins - 1 and NaN exact, every other ranked cell SOME label in [1, n_bins - 2]."""
         T_m, N = M.shape
         _need(M, "M", torch.float64, (T_m, N), self.device)
         _need(IDS, "IDS", torch.int16, (T_m, N), self.device)
@@ -335,6 +337,12 @@ class Engine:
             self._call("csm_deciles_ids_ls", _ptr(M), _ptr(NR), _ptr(IDS), T_m, N, int(n_bins),
                        q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV),
                        _ptr(LS))
+            return L, EW, CNT, NV
+        if legs:
+            if NR is not None:
+                raise ValueError("deciles_ids(legs=True) takes no NR (labels only)")
+            self._call("csm_deciles_ids_legs", _ptr(M), _ptr(IDS), T_m, N, int(n_bins),
+                       q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(NV))
             return L, EW, CNT, NV
         self._call("csm_deciles_ids", _ptr(M), _ptr(NR), _ptr(IDS), T_m, N, int(n_bins),
                    q.ctypes.data_as(ctypes.c_void_p), _ptr(L), _ptr(EW), _ptr(CNT), _ptr(NV))

@@ -32,6 +32,7 @@ import torch
 import torch.distributed as dist
 
 from .distributed import all_gather_stack
+from .engine import LEGS_MAX_N
 
 JOIN_ROWS = 4096   # SweepConfig.join_js: batches below this many (month, panel) rows
 SUMMARY_FIELDS = ("months", "mean", "sharpe", "turnover", "cost", "net_mean", "net_sharpe")
@@ -117,6 +118,10 @@ class SweepConfig:
     # series has -- wider rows always get every decile).  False: every decile's overlapped
     # return
     legs_only: bool = True
+    # with legs_only: the decile pass selects only the legs' edges (csm_deciles_ids_legs --
+    # labels 0 / n_bins - 1 exact, the interior ones arbitrary in [1, n_bins - 2]); the same
+    # summary table bit for bit
+    legs_labels: bool = True
     # bootstrap sweeps (run_bootstrap): csm_boot_scan -- the panel generated in registers and
     # scanned for every J at once, one next_ret panel for every J -- instead of csm_bootstrap ->
     # multi-J scan (same labels and summary table, bit for bit)
@@ -141,6 +146,13 @@ class SweepConfig:
     @property
     def strategies(self):
         return strategy_grid(self.Js, self.Ks)
+
+
+def _legs_labels(c, legs, N):
+    """Whether a batch's ids decile pass may label legs only (csm_deciles_ids_legs): the
+    legs-only accounting follows (it reads deciles 0 and n_bins - 1 only; a rerun for a panel
+    lacking a leg ranks every decile again) and takes rows this wide (LEGS_MAX_N)."""
+    return bool(legs) and c.legs_labels and c.n_bins >= 4 and N <= LEGS_MAX_N
 
 
 def _stacked(ts):
@@ -253,7 +265,7 @@ class SweepRunner:
         return (table, series, flag) if defer else (table, series)
 
     def _run_batch(self, PMb, B, W, ADV, SIG, flag):
-        return self._account(self._ranked(PMb, B), B, W, ADV, SIG, flag)
+        return self._account(self._ranked(PMb, B, legs=flag is not None), B, W, ADV, SIG, flag)
 
     def _joined(self, T_m, B):
         """Whether a batch this small runs its Js' decile passes and accounting as one launch
@@ -262,13 +274,15 @@ class SweepRunner:
         return (c.join_js and hasattr(self.st, "summary") and len(c.Js) > 1
                 and T_m * B < JOIN_ROWS)
 
-    def _ranked(self, PMb, B):
+    def _ranked(self, PMb, B, legs=False):
         """(J, L, NR) per J of the grid from the month prices of a batch: one J's ranking
         panels live at a time (small joined batches: every J's scan, then one decile pass over
-        the Js' rows stacked)."""
+        the Js' rows stacked).  legs (legs-only accounting follows): the ids decile pass may
+        leave the interior deciles inexact (deciles_ids(legs=True))."""
         c, st = self.cfg, self.st
         T_m, BN = PMb.shape
         N = BN // B
+        lg = {"legs": True} if _legs_labels(c, legs, N) else {}
         if self._joined(T_m, B):
             # every J from one time-chunked scan where it applies (csm_momentum_multi_chunked:
             # C3 scan 0.245 ms for four chunked scans), with the bucket ids for the decile pass
@@ -288,7 +302,7 @@ class SweepRunner:
             if ids:
                 Lcat, _, _, _ = st.deciles_ids(
                     Mcat, None, _stacked([mo[2] for mo in MN]).view(len(MN) * T_m * B, N),
-                    c.n_bins)
+                    c.n_bins, **lg)
             else:
                 Lcat, _, _, _ = st.deciles(Mcat, None, c.n_bins)
             R = T_m * B
@@ -319,7 +333,7 @@ class SweepRunner:
                 _, M, NR = st.momentum(PMb, J, c.skip)
             if IDS is not None:
                 L, _, _, _ = st.deciles_ids(M.reshape(T_m * B, N), None,
-                                            IDS.reshape(T_m * B, N), c.n_bins)
+                                            IDS.reshape(T_m * B, N), c.n_bins, **lg)
             else:
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS
@@ -445,12 +459,13 @@ class SweepRunner:
                                         mean_block=mean_block, with_ids=ids)
         legs = legs and c.legs_only and hasattr(st, "summary")
         flag = torch.zeros(1, dtype=torch.int32, device=NR.device) if legs else None
+        lg = {"legs": True} if _legs_labels(c, legs, N) else {}
         labels = []
         for q, J in enumerate(c.Js):
             (M, IDS), outs[q] = outs[q], None
             if IDS is not None:
                 L, _, _, _ = st.deciles_ids(M.reshape(T_m * B, N), None, IDS.reshape(T_m * B, N),
-                                            c.n_bins)
+                                            c.n_bins, **lg)
             else:
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS

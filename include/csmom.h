@@ -219,6 +219,16 @@ int csm_deciles_ids_ls(csm_ctx* ctx, const double* M, const double* NR, const ui
                        double* EW, int32_t* CNT, int32_t* NV, double* LS);
 
 /*
+ * csm_deciles_ids without decile sums, for legs-only accounting (csm_cohort_sums_legs /
+ * csm_portfolio_from_cohorts_legs, sweep.SweepConfig.legs_only): with n_bins >= 4 the labels
+ * 0 and n_bins - 1 and the NaN label (-1) are exactly csm_deciles_ids's, every other ranked
+ * cell gets SOME label in [1, n_bins - 2] (the interior edges' order statistics are not
+ * selected).  n_bins < 4: exactly csm_deciles_ids.  NV as there (nullable).
+ */
+int csm_deciles_ids_legs(csm_ctx* ctx, const double* M, const uint16_t* ids, int32_t T_m,
+                         int64_t N, int32_t n_bins, const double* qtable, int8_t* L, int32_t* NV);
+
+/*
  * The whole K = 1 path of run_demo.py:31-67 in one call: fused month-end + scan (csm_signal,
  * with ids when N % 4 == 0 and the row is wide), per-date labels fused with the decile means
  * (csm_deciles / csm_deciles_ids), long-short (csm_long_short).  Arguments as in those calls

@@ -26,15 +26,19 @@ _, outs, NR, bad = eng.boot_scan(R, B, Js, 1, b0=0, with_ids=True)
 for J, (M, IDS) in zip(Js, outs):
     L, _, _, _ = eng.deciles_ids(M.reshape(T_m * B, N), None, IDS.reshape(T_m * B, N), 10)
     L = L.reshape(T_m, B, N)
-    ne = torch.stack([(L == 9).any(2), (L == 0).any(2)], 0)   # [leg][t][b] cohort non-empty
+    ne = torch.stack([(L == 9).any(2), (L == 0).any(2)], 0).int()   # [leg][t][b] non-empty cohort
+    cs = torch.cat([torch.zeros_like(ne[:, :1]), ne.cumsum(1)], 1)   # cs[:, t] = months < t
     gen = torch.zeros(T_m, B, dtype=torch.bool, device=L.device)
-    for K in Ks:
-        for t in range(T_m):
-            w1 = ne[:, max(0, t - K + 1):t + 1].all(1) & (t - K + 1 >= 0)
-            w0 = ne[:, max(0, t - K):t].all(1) & (t - K >= 0)
-            gen[t] |= ~(w1 & w0).all(0)
+    empty = torch.ones(T_m, B, dtype=torch.bool, device=L.device)
+    Kmax = max(Ks)
+    for t in range(T_m):
+        lo = max(0, t - Kmax)
+        empty[t] = (cs[:, t + 1] - cs[:, lo]).sum(0) == 0
+        for K in Ks:   # steady (telescoping): t >= K and as many non-empty cohorts in both windows
+            k1 = cs[:, t + 1] - cs[:, max(0, t - K + 1)]
+            k0 = cs[:, t] - cs[:, max(0, t - K)]
+            gen[t] |= ~((k1 == k0) & (t >= K)).all(0)
+    gen &= ~empty
     g = gen.sum(1).cpu()
-    first = [int(t) for t in torch.nonzero(g < B).flatten()[:1]]
     print(f"J={J}: general rows {int(g.sum())} of {T_m * B} ({100 * g.sum() / (T_m * B):.1f} %), "
-          f"all-general months {int((g == B).sum())}, first month with a steady row {first}, "
-          f"general rows after month 40: {int(g[40:].sum())}")
+          f"empty rows {int(empty.sum())}, general rows after month 40: {int(g[40:].sum())}")

@@ -359,6 +359,59 @@ def test_deciles_ids_narrow_rows(engine, tune_merge, width):
     assert torch.equal(Lz, L1)
 
 
+def _legs_consistent(full, legs, n_bins):
+    """legs-mode labels against exact ones: deciles 0 / n_bins - 1 and NaN cells identical, every
+    other ranked cell inside [1, n_bins - 2]."""
+    top = n_bins - 1
+    assert np.array_equal(full == 0, legs == 0) and np.array_equal(full == top, legs == top)
+    assert np.array_equal(full == -1, legs == -1)
+    mid = (full > 0) & (full < top)
+    assert ((legs[mid] >= 1) & (legs[mid] <= top - 1)).all()
+
+
+@pytest.mark.parametrize("width", [4_000, 5_000, 16_384, 36_000])
+@pytest.mark.parametrize("n_bins", [2, 3, 4, 5, 10, 20])
+def test_deciles_ids_legs(engine, width, n_bins):
+    """csm_deciles_ids_legs (the sweeps' labels before legs-only accounting): on every stress
+    case and momentum-like rows the legs and NaN labels equal csm_deciles_ids's and the oracle's
+    qcut, the interior ones lie in [1, n_bins - 2], NV is equal; n_bins < 4: identical labels.
+    Narrow rows (merged pass of the 2048-bucket kernel) and a wide one (8192 buckets)."""
+    cases = MERGE_CASES + ["lognormal_mild"] * 4
+    x = np.stack([_stress_row(c, n=width) for c in cases])
+    M, IDS = _up(x), _ids_dev(x)
+    Lf, _, _, Nf = engine.deciles_ids(M, None, IDS, n_bins, with_nv=True)
+    Ll, _, _, Nl = engine.deciles_ids(M, None, IDS, n_bins, with_nv=True, legs=True)
+    assert torch.equal(Nf, Nl)
+    if n_bins < 4:
+        assert torch.equal(Lf, Ll)
+        return
+    lf, ll = Lf.cpu().numpy(), Ll.cpu().numpy()
+    _legs_consistent(lf, ll, n_bins)
+    _legs_consistent(O.assign_deciles(x, n_bins), ll, n_bins)
+    if n_bins == 10:   # the legs mode ran: interior labels differ somewhere
+        assert (lf != ll).any()
+
+
+@pytest.mark.parametrize("boot", [False, True])
+def test_sweep_legs_labels_same_table(engine, boot):
+    """SweepConfig.legs_labels (the decile pass selects only the legs' edges before legs-only
+    accounting): the summary table equals legs_labels=False bit for bit -- a month-price batch
+    with gaps, and a bootstrap batch (csm_boot_scan)."""
+    from csmom.sweep import SweepConfig, SweepRunner
+    pm = _month_panel(2_000, 240, 11)
+    runs = {}
+    for ll in (True, False):
+        sr = SweepRunner(engine, SweepConfig(legs_labels=ll))
+        if boot:
+            R, _, _ = engine.momentum(_up(pm), 12, 1, with_ret=True)
+            runs[ll] = sr.run_boot_batch(R.contiguous(), 3, 0)[0]
+        else:
+            B = 3
+            PMb = _up(np.concatenate([pm, pm[:, ::-1], pm * 1.5], axis=1))
+            runs[ll] = sr.run_batch(PMb, B)[0]
+    assert bits_equal(runs[True].cpu().numpy(), runs[False].cpu().numpy())
+
+
 def test_sweep_batch_ids_equal_streaming(engine):
     """SweepRunner.run_batch with the id path (default) equals decile_ids=False: the summary
     table bit for bit (the labels are identical, so every later stage is)."""
