@@ -658,6 +658,15 @@ class TimedStages:
                           (1.0 * len(Ls) + 8.0) * T_m * BN, self.eng.portfolio_multi_js, Ls, NR,
                           n_bins, **k)
 
+    def portfolio_multi_js_grouped(self, Lg, NR, n_bins=10, **k):
+        T_m, BN = NR.shape   # algorithmic: each J's labels, the shared next_ret once
+        return self._wrap("portfolio(k_cohort+k_turnover+k_overlap+k_ls)",
+                          (1.0 * Lg.shape[0] + 8.0) * T_m * BN, self.eng.portfolio_multi_js_grouped,
+                          Lg, NR, n_bins, **k)
+
+    def portfolio_plan(self, *a, **k):
+        return self.eng.portfolio_plan(*a, **k)
+
     def summary(self, LS, TURN=None, COST=None, NET=None, **k):
         return self._wrap("summary(k_summary)", 8.0 * LS.numel() * (4 if TURN is not None else 1),
                           self.eng.summary, LS, TURN, COST, NET, **k)

@@ -79,6 +79,9 @@ SIGNATURES = {
                                                        _p, _p, _p, _p, _p, _p, _p, _p]),
     "csm_cohort_sums_grouped": (ctypes.c_int, [_p, _i32, _p, _p, _p, _i32, _i32, _i64, _i32,
                                                _i32, _i32, _p]),
+    "csm_cohort_sums_js_grouped": (ctypes.c_int, [_p, _i32, _p, _p, _i32, _i32, _i64, _i32,
+                                                  _i32, _i32, _p]),
+    "csm_portfolio_plan": (ctypes.c_int64, [_i32, _i32, _i64, _i32, _i32]),
     "csm_portfolio_from_cohorts_grouped": (ctypes.c_int, [_p, _i32, _p, _p, _i32, _i32, _i64,
                                                           _i32, _i32, _i32, _p, _f64, _f64, _f64,
                                                           _p, _p, _p, _p, _p, _p, _p, _p, _i32,

@@ -61,9 +61,14 @@ struct PanAddr {
   int64_t N;
   int64_t gl, ml;   // labels / next_ret: group stride, month stride (cells)
   int64_t mw;       // weights / ADV / vol: month stride (one block for every group)
+  int64_t ngl;      // next_ret: group stride (gl, or 0: one next_ret block for every group)
   __host__ __device__ int64_t lrow(int t, int b) const {
     const int g = b / Bg;
     return (int64_t)g * gl + (int64_t)t * ml + (int64_t)(b - g * Bg) * N;
+  }
+  __host__ __device__ int64_t nrow(int t, int b) const {
+    const int g = b / Bg;
+    return (int64_t)g * ngl + (int64_t)t * ml + (int64_t)(b - g * Bg) * N;
   }
   __host__ __device__ int64_t wrow(int t, int b) const {
     const int g = b / Bg;
@@ -71,10 +76,11 @@ struct PanAddr {
   }
 };
 static PanAddr pan_plain(int B, int64_t N) {
-  return PanAddr{B, B, N, 0, (int64_t)B * N, (int64_t)B * N};
+  return PanAddr{B, B, N, 0, (int64_t)B * N, (int64_t)B * N, 0};
 }
-static PanAddr pan_grouped(int G, int Bg, int T_m, int64_t N) {
-  return PanAddr{G * Bg, Bg, N, (int64_t)T_m * Bg * N, (int64_t)Bg * N, (int64_t)Bg * N};
+static PanAddr pan_grouped(int G, int Bg, int T_m, int64_t N, bool shared_nr = false) {
+  const int64_t gl = (int64_t)T_m * Bg * N;
+  return PanAddr{G * Bg, Bg, N, gl, (int64_t)Bg * N, (int64_t)Bg * N, shared_nr ? 0 : gl};
 }
 
 // -------------------------------------------------------------------------------- E1
@@ -94,7 +100,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
-  const int64_t rt = pa.lrow(t, b);
+  const int64_t rt = pa.nrow(t, b);   // next_ret row of month t
   const int k_lo = kpar ? (int)blockIdx.z : 0, k_hi = kpar ? k_lo + 1 : K;
   for (int k = k_lo; k < k_hi; ++k) {
     const int s = t - k;
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
   for (int i = lane; i < KD; i += 64) { acc_r[wid][i] = 0.0; acc_w[wid][i] = 0.0; }
   const int64_t a0 = (int64_t)c * CH;
   const int64_t a1 = a0 + CH < N ? a0 + CH : N;
-  const int64_t rt = pa.lrow(t, b), rtw = pa.wrow(t, b);
+  const int64_t rt = pa.lrow(t, b), rtw = pa.wrow(t, b), rtn = pa.nrow(t, b);
   const int kmax = t + 1 < K ? t + 1 : K;   // ages with a formation month s = t - k >= 0
   double ft = 0.0, fb = 0.0;
   double* ar = acc_r[wid];
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_lds(
   __syncthreads();
   const int64_t rowstep = pa.ml, rowstepw = pa.mw;   // one month back
   for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
-    const double r = NR[rt + a];
+    const double r = NR[rtn + a];
     const bool rv = r == r;
     // ages in groups of KU: the group's label (and weight) loads are issued before use
     constexpr int KU = 4;
@@ -504,7 +510,7 @@ struct SegJ {
 template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const double* __restrict__ NR, SegJ sj, const double* __restrict__ WSRT, int T_m, int B,
-    int64_t N, int K, int C, int Cs, int xcd, int stage2, PanAddr pa) {
+    int64_t N, int K, int C, int Cs, int xcd, int stage2, PanAddr pa, int Bo) {
   constexpr int ND = LEGS ? 2 : NB;   // segments per age
   auto dec_of = [](int e) { return LEGS ? (e ? NB - 1 : 0) : e; };
   // the return row of month t (N values), NaN at slot N
@@ -538,23 +544,26 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   const int tid = threadIdx.x;
   const int grp = tid / SEG_G, sl = tid % SEG_G;
   const int kmax = t + 1 < K ? t + 1 : K;
+  // the segment rows and cohort partials of panel b: row t * Bo + b of the workspace (Bo = B;
+  // the shared-return grouped pass: Bo = nJ * B, J q's panels at rows q * B + b via sj's bases)
+  const int64_t tbo = (int64_t)t * Bo + (tb - (int64_t)t * B);
   const int KD = K * OE;
   if (c >= Cs) {   // chunks beyond the Cs working ones only hold zeros
     for (int jq = 0; jq < sj.n; ++jq)
       for (int g = tid; g < K * ND; g += PF_THREADS) {
         const int k = g / ND, d = dec_of(g - k * ND);
-        const int64_t ob = ((tb * K + k) * C + c) * NB + d;
+        const int64_t ob = ((tbo * K + k) * C + c) * NB + d;
         sj.SWR[jq][ob] = 0.0;
         sj.SW[jq][ob] = 0.0;
       }
     return;
   }
-  const double* NRr = NR + pa.lrow(t, (int)(tb - (int64_t)t * B));
+  const double* NRr = NR + pa.nrow(t, (int)(tb - (int64_t)t * B));
   for (int jq = 0; jq < sj.n; ++jq)
     for (int i = tid; i < kmax * OE; i += PF_THREADS) {
       const int k = i / OE, e = i - k * OE;
       const int es = LEGS ? (e < 2 ? e : NB - 3 + e) : e;   // legs: bounds 0, 1, NB - 1, NB
-      offs_all[jq * KD + i] = (OffT)sj.OFF[jq][(tb - (int64_t)k * B) * (NB + 1) + es];
+      offs_all[jq * KD + i] = (OffT)sj.OFF[jq][(tbo - (int64_t)k * Bo) * (NB + 1) + es];
     }
   if ((N & 1) == 0 && stage2) {
     // 16-B loads, up to SEG_STAGE_U per lane issued before any LDS store: a 6144-value row
@@ -592,7 +601,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   for (int g = tid; g < K * ND && Cs > 1; g += PF_THREADS) {
     if (g % Cs == c) continue;
     const int k = g / ND, d = dec_of(g - k * ND);
-    const int64_t ob = ((tb * K + k) * C + c) * NB + d;
+    const int64_t ob = ((tbo * K + k) * C + c) * NB + d;
     SWRp[ob] = 0.0;
     SWp[ob] = 0.0;
   }
@@ -610,9 +619,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   auto seg_at = [&](int g) {
     Seg q;
     const int k = g / ND, d = dec_of(g - k * ND);
-    q.ob = ((tb * K + k) * C + c) * NB + d;
+    q.ob = ((tbo * K + k) * C + c) * NB + d;
     q.live = k < kmax;
-    const int64_t srow = tb - (int64_t)(q.live ? k : 0) * B;
+    const int64_t srow = tbo - (int64_t)(q.live ? k : 0) * Bo;
     const int oi = LEGS ? k * 4 + (d == 0 ? 0 : 2) : k * (NB + 1) + d;
     q.w0 = q.live ? (int64_t)offs[oi] >> 2 : 0;
     q.w1 = q.live ? (int64_t)offs[oi + 1] >> 2 : 0;
@@ -1749,7 +1758,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
         hipLaunchKernelGGL((k_label_sort<NB, true, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N,
                            pl.C, PERM, OFF, WSRT, FWp, pa);
         hipLaunchKernelGGL((k_cohort_seg<NB, true, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
+                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa, B);
       } else {
         if ((N & 3) == 0)   // one wave per row (C5's equal-weight legs)
           hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
@@ -1758,18 +1767,18 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
           hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N,
                              pl.C, PERM, OFF, WSRT, FWp, pa);
         hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
+                           (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa, B);
       }
     } else if (W) {
       hipLaunchKernelGGL((k_label_sort<NB, true>), g1, dim3(PF_THREADS), (size_t)N * 9, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp, pa);
       hipLaunchKernelGGL((k_cohort_seg<NB, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
+                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa, B);
     } else {
       hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N, pl.C,
                          PERM, OFF, WSRT, FWp, pa);
       hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa);
+                         (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa, B);
     }
     return;
   }
@@ -1795,43 +1804,54 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
 // per row): each J's label sort, then ONE k_cohort_seg launch staging each month's return row
 // once for every J.  ws[q]: J q's workspace base; the partials land where launch_cohort puts
 // them, bit for bit the same values.
+// grouped: L[0] holds the Js' label panels group-major ([nJ][T_m][B * N]) and ws[0] is ONE
+// workspace laid out for nJ * B panels (J q's panel b = panel q * B + b, as csm_cohort_sums_grouped
+// lays them out): one label-sort launch for every J, and the same partials at those rows.
 template <int NB>
 static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int8_t* const* L,
                              const double* NR, int T_m, int B, int64_t N, int K, char* const* ws,
                              int64_t swr_b, int64_t sw_b, int64_t fw_b, int64_t perm_b,
-                             int64_t off_b, bool legs) {
+                             int64_t off_b, bool legs, bool grouped = false) {
   const int xcd = B >= 8;
-  const dim3 g1((unsigned)(T_m * B)),
-      g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(T_m * B));
+  const dim3 g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(T_m * B));
   const PanAddr pa = pan_plain(B, N);
+  const int Bo = grouped ? nJ * B : B;   // panels per month of the workspace rows
+  auto label_sort = [&](const int8_t* Lq, char* w, int nrow_b, const PanAddr& pl_a) {
+    uint16_t* PERM = (uint16_t*)(w + perm_b);
+    int32_t* OFF = (int32_t*)(w + off_b);
+    double* FWp = (double*)(w + fw_b);
+    const int64_t rows = (int64_t)T_m * nrow_b;
+    if (legs && (N & 3) == 0)
+      hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((rows + PF_WAVES - 1) / PF_WAVES)),
+                         dim3(PF_THREADS), 0, st, Lq, N, 1, rows, PERM, OFF, FWp, pl_a);
+    else if (legs)
+      hipLaunchKernelGGL((k_label_sort<NB, false, true>), dim3((unsigned)rows), dim3(PF_THREADS), (size_t)N,
+                         st, Lq, (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp, pl_a);
+    else
+      hipLaunchKernelGGL((k_label_sort<NB, false>), dim3((unsigned)rows), dim3(PF_THREADS), (size_t)N, st,
+                         Lq, (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp, pl_a);
+  };
+  if (grouped) label_sort(L[0], ws[0], nJ * B, pan_grouped(nJ, B, T_m, N));
+  const int64_t PS = seg_stride(N);
   SegJ sj;
   sj.n = nJ;
   for (int q = 0; q < nJ; ++q) {
-    uint16_t* PERM = (uint16_t*)(ws[q] + perm_b);
-    int32_t* OFF = (int32_t*)(ws[q] + off_b);
-    double* FWp = (double*)(ws[q] + fw_b);
-    if (legs && (N & 3) == 0)
-      hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
-                         dim3(PF_THREADS), 0, st, L[q], N, 1, (int64_t)T_m * B, PERM, OFF, FWp, pa);
-    else if (legs)
-      hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L[q],
-                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp, pa);
-    else
-      hipLaunchKernelGGL((k_label_sort<NB, false>), g1, dim3(PF_THREADS), (size_t)N, st, L[q],
-                         (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp, pa);
-    sj.PERM[q] = PERM;
-    sj.OFF[q] = OFF;
-    sj.SWR[q] = (double*)(ws[q] + swr_b);
-    sj.SW[q] = (double*)(ws[q] + sw_b);
+    char* w = grouped ? ws[0] : ws[q];
+    if (!grouped) label_sort(L[q], w, B, pa);
+    const int64_t r0 = grouped ? (int64_t)q * B : 0;   // J q's first workspace row of a month
+    sj.PERM[q] = (uint16_t*)(w + perm_b) + r0 * PS;
+    sj.OFF[q] = (int32_t*)(w + off_b) + r0 * (NB + 1);
+    sj.SWR[q] = (double*)(w + swr_b) + r0 * K * NB;   // (one cohort chunk)
+    sj.SW[q] = (double*)(w + sw_b) + r0 * K * NB;
   }
   const size_t lds = (size_t)(N + 1) * sizeof(double) +
                      (legs ? (size_t)nJ * K * 4 * sizeof(uint16_t) : (size_t)nJ * K * (NB + 1) * sizeof(int32_t));
   if (legs)
     hipLaunchKernelGGL((k_cohort_seg<NB, false, true>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1, pa);
+                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1, pa, Bo);
   else
     hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR, sj,
-                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1, pa);
+                       (const double*)nullptr, T_m, B, N, K, 1, 1, xcd, 1, pa, Bo);
 }
 
 // Workspace layout of the cohort partials for (T_m, B, N, n_bins, Kmax): SWRp, SWp
@@ -1997,6 +2017,44 @@ int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const d
   LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret)");
   // (the shared path has one cohort chunk: each J's partials are its folded totals)
   return CSM_OK;
+}
+
+int csm_cohort_sums_js_grouped(csm_ctx* ctx, int32_t nJ, const int8_t* L, const double* NR,
+                               int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
+                               int32_t legs, void* workspace) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!L || !NR || !workspace || nJ < 1 || nJ > SEG_MAXJ || T_m < 0 || B < 1 || N <= 0 ||
+      Kmax < 1 || Kmax > TO_MAXK || (int64_t)T_m * nJ * B > 0x7FFFFFFF)
+    return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_js_grouped: bad arguments (nJ=%d T_m=%d B=%d "
+                   "N=%lld Kmax=%d; 1 <= nJ <= %d)", nJ, T_m, B, (long long)N, Kmax, SEG_MAXJ);
+  if (legs && N > SEG_MAXN)
+    return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_js_grouped: legs on rows of <= %d assets "
+                   "(N=%lld)", SEG_MAXN, (long long)N);
+  if (T_m == 0) return CSM_OK;
+  const PfLayout lay = pf_layout(T_m, nJ * B, N, n_bins, Kmax);
+  const bool shared = g_tune_cohort_seg && lay.seg && lay.p.C == 1 && !lay.p.kpar &&
+                      (legs ? nJ * Kmax * 4 : nJ * Kmax * (n_bins + 1)) <= SEG_MAXKD &&
+                      (n_bins == 2 || n_bins == 3 || n_bins == 4 || n_bins == 5 || n_bins == 10 ||
+                       n_bins == 20 || n_bins == 30);
+  if (!shared)   // the grouped pass with every group reading the one next_ret block
+    return cohort_sums(ctx, L, NR, nullptr, T_m, nJ * B, N, n_bins, Kmax, workspace, legs != 0,
+                       pan_grouped(nJ, B, T_m, N, true));
+  hipStream_t st = ctx->stream;
+  char* ws = (char*)workspace;
+  switch (n_bins) {
+#define PJ_CASE(NBV) case NBV: launch_cohort_js<NBV>(st, lay.p, nJ, &L, NR, T_m, B, N, Kmax, &ws, lay.swr * 8, lay.sw * 8, lay.fw * 8, lay.perm_b, lay.off_b, legs != 0, true); break;
+    PJ_CASE(2) PJ_CASE(3) PJ_CASE(4) PJ_CASE(5) PJ_CASE(10) PJ_CASE(20) PJ_CASE(30)
+#undef PJ_CASE
+  }
+  LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret, grouped)");
+  return CSM_OK;
+}
+
+int64_t csm_portfolio_plan(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t K) {
+  if (T_m < 0 || B < 1 || N <= 0 || n_bins < 1 || K < 1) return -1;
+  const PfPlan p = pf_plan(T_m, B, N, K, n_bins);
+  return (int64_t)p.C | ((int64_t)p.Ct << 32);
 }
 
 int csm_cohort_sums_legs(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,

@@ -517,6 +517,49 @@ class Engine:
                                            with_costs, legs_only=False)
         return outs
 
+    def portfolio_plan(self, T_m, B, N, n_bins=10, K=1):
+        """csm_portfolio_plan: (cohort chunks, turnover chunks) of a portfolio call; calls with
+        the same plan give each panel the same bits."""
+        v = int(self.lib.csm_portfolio_plan(int(T_m), int(B), int(N), int(n_bins), int(K)))
+        if v < 0:
+            raise ValueError("csm_portfolio_plan: bad arguments")
+        return v & 0xFFFFFFFF, v >> 32
+
+    def portfolio_multi_js_grouped(self, Lg, NR, n_bins=10, Ks=(1,), B=1, half_spread=0.0005,
+                                   k_impact=0.1, aum=0.0, with_costs=True, legs_only=False,
+                                   need_full=None, return_stacked=False):
+        """portfolio_multi_js with the look-backs' label panels stored group-major, Lg int8
+        [nJ][T_m][B * N] (as one stacked decile pass writes them): one cohort pass over the shared
+        next_ret NR [T_m][B * N] into one workspace of nJ * B panels (csm_cohort_sums_js_grouped),
+        then ONE accounting launch set for every J (csm_portfolio_from_cohorts_grouped: panel
+        q * B + b = J q's panel b).  Where portfolio_plan(T_m, B) == portfolio_plan(T_m, nJ * B),
+        each J's outputs equal portfolio_multi_js's bit for bit."""
+        if Lg.dim() != 3:
+            raise ValueError("Lg must be [nJ][T_m][B * N]")
+        nJ, T_m, BN = Lg.shape
+        if B < 1 or BN % B:
+            raise ValueError(f"row width {BN} is not B={B} panels")
+        N = BN // B
+        _need(Lg, "Lg", torch.int8, (nJ, T_m, BN), self.device)
+        _need(NR, "NR", torch.float64, (T_m, BN), self.device)
+        Ks = [int(k) for k in Ks]
+        Kmax = max(Ks)
+        legs_only = bool(legs_only) and N <= LEGS_MAX_N
+        nbytes = int(self.lib.csm_portfolio_workspace(T_m, nJ * B, N, int(n_bins), Kmax))
+        ws = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=self.device)
+        self._call("csm_cohort_sums_js_grouped", nJ, _ptr(Lg), _ptr(NR), T_m, int(B), N,
+                   int(n_bins), Kmax, 1 if legs_only else 0, _ptr(ws))
+        flag = need_full
+        if legs_only and need_full is None:
+            flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        res, stacked = self._from_cohorts(Lg, None, T_m, nJ * B, N, n_bins, Ks, half_spread,
+                                          k_impact, aum, None, None, with_costs, ws, legs_only,
+                                          flag, groups=(nJ, B))
+        if legs_only and need_full is None and int(flag.item()):   # a panel lacks a leg's column
+            return self.portfolio_multi_js_grouped(Lg, NR, n_bins, Ks, B, half_spread, k_impact,
+                                                   aum, with_costs, False, None, return_stacked)
+        return (res, stacked) if return_stacked else res
+
     def portfolio_multi_grouped(self, Lg, NRg, n_bins=10, Ks=(1,), W=None, Bg=1,
                                 half_spread=0.0005, k_impact=0.1, aum=0.0, ADV=None, SIG=None,
                                 with_costs=True, workspace=None, return_stacked=False,

@@ -409,7 +409,12 @@ class SweepRunner:
             outs, stk = st.portfolio_multi(L, NR, c.n_bins, Ks=c.Ks, return_stacked=True, **kw)
             del L, NR
         summ_all = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # [nK][nJ * B][F]
-        Js = [it[0] for it in items]
+        return self._joined_table(summ_all, outs, [it[0] for it in items], B)
+
+    def _joined_table(self, summ_all, outs, Js, B):
+        """(summary [B][S][F], series) of a joined accounting (panel q * B + b = J q's panel b)
+        from its [nK][nJ * B][F] summaries and {K: PortfolioOut}."""
+        c = self.cfg
         # per-(J, K) series: strided views of the joined outputs, built when read (C3's step is
         # host-bound: 16 strategies x 5 views a step cost more than the GPU work they describe)
         series = _JoinedSeries(outs, Js, B)
@@ -460,21 +465,34 @@ class SweepRunner:
         legs = legs and c.legs_only and hasattr(st, "summary")
         flag = torch.zeros(1, dtype=torch.int32, device=NR.device) if legs else None
         lg = {"legs": True} if _legs_labels(c, legs, N) else {}
+        # grouped shared-return accounting: the Js' labels written group-major by their decile
+        # passes, one cohort pass and ONE accounting launch set for every J -- where the batch's
+        # chunk plan is that of the Js' panels side by side, so every table entry keeps its bits
+        nJ, Km = len(c.Js), max(c.Ks)
+        jsg = (ids and c.share_nr and c.grouped and nJ > 1 and not self._joined(T_m, B)
+               and hasattr(st, "portfolio_multi_js_grouped") and hasattr(st, "portfolio_plan")
+               and st.portfolio_plan(T_m, B, N, c.n_bins, Km)
+               == st.portfolio_plan(T_m, nJ * B, N, c.n_bins, Km))
+        Lg = torch.empty((nJ, T_m * B, N), dtype=torch.int8, device=NR.device) if jsg else None
         labels = []
         for q, J in enumerate(c.Js):
             (M, IDS), outs[q] = outs[q], None
             if IDS is not None:
                 L, _, _, _ = st.deciles_ids(M.reshape(T_m * B, N), None, IDS.reshape(T_m * B, N),
-                                            c.n_bins, **lg)
+                                            c.n_bins, out=(Lg[q], None, None, None) if jsg else None,
+                                            **lg)
             else:
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS
             labels.append((J, L.reshape(T_m, B * N), NR))
-        shared = (c.share_nr and hasattr(st, "portfolio_multi_js") and len(labels) > 1
-                  and not self._joined(T_m, B))
-        acc = self._account_shared if shared else self._account
-        out = acc(labels, B, None, None, None, flag)
-        del labels, NR
+        if jsg:
+            out = self._account_js_grouped(Lg.view(nJ, T_m, B * N), NR, B, flag)
+        else:
+            shared = (c.share_nr and hasattr(st, "portfolio_multi_js") and len(labels) > 1
+                      and not self._joined(T_m, B))
+            acc = self._account_shared if shared else self._account
+            out = acc(labels, B, None, None, None, flag)
+        del labels, NR, Lg
         state = bad * 2 + (flag if legs else 0)
 
         def redo(v):   # holds no panel: a flagged batch is recomputed from its seed
@@ -488,6 +506,18 @@ class SweepRunner:
                 return o
             return None
         return out, state, redo
+
+    def _account_js_grouped(self, Lg, NR, B, flag):
+        """_account_shared with the Js' labels group-major (Lg [nJ][T_m][B * N]): one cohort
+        pass over the shared next_ret and one accounting launch set for every J
+        (portfolio_multi_js_grouped), then one summary launch -- the same table and series."""
+        c, st = self.cfg, self.st
+        outs, stk = st.portfolio_multi_js_grouped(
+            Lg, NR, c.n_bins, Ks=c.Ks, B=B, half_spread=c.half_spread, k_impact=c.k_impact,
+            aum=c.aum, with_costs=c.costs, legs_only=flag is not None, need_full=flag,
+            return_stacked=True)
+        summ_all = st.summary(stk.LS, stk.TURN, stk.COST, stk.NET)   # [nK][nJ * B][F]
+        return self._joined_table(summ_all, outs, [int(J) for J in c.Js], B)
 
     def _account_shared(self, labels, B, W, ADV, SIG, flag):
         """_account for Js that share one next_ret panel (bootstrap batches, no weights / ADV /

@@ -393,6 +393,26 @@ int csm_portfolio_from_cohorts_legs(csm_ctx* ctx, const int8_t* L, const double*
 int csm_cohort_sums_grouped(csm_ctx* ctx, int32_t G, const int8_t* L, const double* NR,
                             const double* W, int32_t T_m, int32_t Bg, int64_t N, int32_t n_bins,
                             int32_t Kmax, int32_t legs, void* workspace);
+
+/*
+ * csm_cohort_sums_js for label panels stored group-major, L int8 [nJ][T_m][B * N] (the look-backs'
+ * panels as one stacked decile pass writes them), into ONE workspace laid out for nJ * B panels
+ * (csm_portfolio_workspace(T_m, nJ * B, ...); J q's panel b is panel q * B + b, as
+ * csm_cohort_sums_grouped lays it out): one label-sort launch for every J and each month's
+ * return row staged once for every J.  csm_portfolio_from_cohorts_grouped(G = nJ, Bg = B) then
+ * accounts every J in one launch set.  Where csm_portfolio_plan(T_m, B, ...) equals
+ * csm_portfolio_plan(T_m, nJ * B, ...), every J's results are csm_cohort_sums_js's bit for bit.
+ */
+int csm_cohort_sums_js_grouped(csm_ctx* ctx, int32_t nJ, const int8_t* L, const double* NR,
+                               int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
+                               int32_t legs, void* workspace);
+
+/*
+ * The chunk plan of a portfolio call on (T_m, B, N, n_bins, K): cohort chunks C in the low 32
+ * bits, turnover chunks Ct in the high ones (-1 on bad arguments).  Two calls with the same plan
+ * give each panel the same partial sums, so their per-panel results are the same bits.
+ */
+int64_t csm_portfolio_plan(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t K);
 int csm_portfolio_from_cohorts_grouped(csm_ctx* ctx, int32_t G, const int8_t* L, const double* W,
                                        int32_t T_m, int32_t Bg, int64_t N, int32_t n_bins,
                                        int32_t Kmax, int32_t nK, const int32_t* Ks,

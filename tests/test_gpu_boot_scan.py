@@ -115,6 +115,47 @@ def test_cohort_sums_js_equal_per_j(engine, N, B, Js, Ks, n_bins, legs):
         assert stk.legs_only == rstk.legs_only
 
 
+@pytest.mark.parametrize("N,B,Js,Ks,n_bins,legs", [
+    (256, 36, (3, 6, 9, 12), (3, 6, 9, 12), 10, True),    # C5's grid: one shared grouped pass
+    (256, 36, (3, 6, 9, 12), (1, 3), 10, False),          # every decile, shared
+    (256, 36, (3, 6, 9, 12), (3, 6, 9, 12), 10, False),   # offsets too many: the grouped pass
+    (202, 40, (3, 12), (2, 5), 5, True),                  # N % 4 != 0: the general label sort
+    (1024, 6, (3, 6, 9, 12), (3, 6, 9, 12), 10, True),    # plans differ: TURN / COST within 1e-12
+])
+def test_cohort_sums_js_grouped_equal_js(engine, N, B, Js, Ks, n_bins, legs):
+    """csm_cohort_sums_js_grouped + csm_portfolio_from_cohorts_grouped (the Js' labels
+    group-major, one workspace of nJ * B panels, one accounting launch set) give every J's
+    outputs bit for bit as portfolio_multi_js where the chunk plans agree (portfolio_plan); with
+    different plans the cohort sums (PR / LS) keep their bits and TURN / COST their values."""
+    R = _base_returns(engine, N, seed=15)
+    T_m = R.shape[0]
+    _, outs, NR, bad = engine.boot_scan(R, B, Js, 1, b0=3, with_ids=False)
+    assert int(bad.item()) == 0
+    nJ = len(Js)
+    Lg = torch.empty((nJ, T_m * B, N), dtype=torch.int8, device="cuda:0")
+    for q, (M, _) in enumerate(outs):
+        Lg[q].copy_(engine.deciles(M.reshape(T_m * B, N), None, n_bins)[0])
+    Lg = Lg.view(nJ, T_m, B * N)
+    same = engine.portfolio_plan(T_m, B, N, n_bins, max(Ks)) == \
+        engine.portfolio_plan(T_m, nJ * B, N, n_bins, max(Ks))
+    assert same == (B > 6)   # (714 rows per J: chunked plans; 2856 side by side: one chunk)
+    res, stk = engine.portfolio_multi_js_grouped(Lg, NR, n_bins, Ks=Ks, B=B, legs_only=legs,
+                                                 return_stacked=True)
+    ref = engine.portfolio_multi_js([Lg[q] for q in range(nJ)], NR, n_bins, Ks=Ks, B=B,
+                                    legs_only=legs)
+    assert stk.legs_only == ref[0][1].legs_only
+    for q, (_, rstk) in enumerate(ref):
+        for f in ("PR", "LS", "TURN", "COST", "NET"):
+            a = getattr(stk, f)[:, :, q * B:(q + 1) * B].cpu().numpy()
+            b = getattr(rstk, f).cpu().numpy()
+            if same or f in ("PR", "LS"):
+                assert bits_equal(a, b), (q, f)
+            else:
+                assert np.array_equal(np.isnan(a), np.isnan(b)), (q, f)
+                assert np.nanmax(np.abs(a - b) / np.maximum(np.abs(b), 1e-300),
+                                 initial=0.0) <= 1e-12, (q, f)
+
+
 @pytest.mark.parametrize("legs", [True, False])
 def test_sweep_runner_share_nr_bit_identical(engine, legs):
     """A bootstrap batch above JOIN_ROWS rows takes the shared cohort pass (share_nr): the table
