@@ -707,8 +707,9 @@ class Engine:
         nJ = len(Js)
         BN = B * N
         src = self.empty((B, T_m), torch.int32)
-        Ms = [self.empty((T_m, BN)) for _ in Js]
-        IDS = [self.empty((T_m, BN), torch.int16) for _ in Js] if with_ids else None
+        # (the Js' panels back to back: a caller may rank them as one stacked decile pass)
+        Ms = list(self.empty((len(Js), T_m, BN)))
+        IDS = list(self.empty((len(Js), T_m, BN), torch.int16)) if with_ids else None
         NR = self.empty((T_m, BN))
         bad = torch.empty(1, dtype=torch.int32, device=self.device)
         arr = lambda ts: (ctypes.c_void_p * nJ)(*[t.data_ptr() for t in ts])

@@ -475,12 +475,19 @@ class SweepRunner:
                == st.portfolio_plan(T_m, nJ * B, N, c.n_bins, Km))
         Lg = torch.empty((nJ, T_m * B, N), dtype=torch.int8, device=NR.device) if jsg else None
         labels = []
+        if jsg:   # every J's rows in one decile pass (boot_scan wrote the panels back to back)
+            Ms, Is = _stacked([o[0] for o in outs]), _stacked([o[1] for o in outs])
+            outs = None
+            st.deciles_ids(Ms.view(nJ * T_m * B, N), None, Is.view(nJ * T_m * B, N), c.n_bins,
+                           out=(Lg.view(nJ * T_m * B, N), None, None, None), **lg)
+            del Ms, Is
         for q, J in enumerate(c.Js):
+            if jsg:
+                break
             (M, IDS), outs[q] = outs[q], None
             if IDS is not None:
                 L, _, _, _ = st.deciles_ids(M.reshape(T_m * B, N), None, IDS.reshape(T_m * B, N),
-                                            c.n_bins, out=(Lg[q], None, None, None) if jsg else None,
-                                            **lg)
+                                            c.n_bins, **lg)
             else:
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS
