@@ -60,7 +60,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS) + sorted(SWEEP_CONFIGS))
     ap.add_argument("--panels", type=int, default=None, help="C5: bootstrap panels (total)")
-    ap.add_argument("--batch", type=int, default=100, help="C5: panels per device batch")
+    ap.add_argument("--batch", type=int, default=200, help="C5: panels per device batch (200: 56.2-57.1 vs 59.1-59.4 ms/step at 100, 60.4 at 250, same box; profiles/r04/experiments/batch/)")
     ap.add_argument("--assets", type=int, default=None)
     ap.add_argument("--days", type=int, default=None)
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
