@@ -822,6 +822,9 @@ def sweep_main(args):
     # step (its all-gather is a host-staged gloo call or an RCCL call outside the graph).
     graph = None
     if defer and world == 1 and args.graph == "on":
+        if args.per_j_scan or args.no_decile_ids:   # never captured (sweep._refuse_capture)
+            raise SystemExit("--graph on takes the default scan and decile paths only "
+                             "(not --per-j-scan / --no-decile-ids; DESIGN.md 4.3)")
         s_cap = torch.cuda.Stream()
         s_cap.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s_cap):      # warm-up on a side stream (torch's capture recipe)

@@ -1740,8 +1740,11 @@ static PfPlan pf_plan(int32_t T_m, int32_t B, int64_t N, int32_t K, int32_t n_bi
   const int64_t rows = (int64_t)T_m * (B < PF_PLAN_MIN_B ? PF_PLAN_MIN_B : B);
   const int64_t want = 4096;
   const int64_t cmax = (N + PF_CHUNK_MIN - 1) / PF_CHUNK_MIN;
-  // the chunking depends on (rows, N) only, so a cohort pass gives the same partial sums
-  // whatever Kmax it was planned for (portfolio_multi == per-K portfolio, bit for bit)
+  // the turnover chunking depends on (rows, N) only; the cohort chunk count also on whether the
+  // segment path takes this (N, Kmax, n_bins) -- the same for every K of a portfolio_multi call,
+  // so a cohort pass gives the same partial sums as the per-K calls (bit for bit).  The plan
+  // reads the "cohort_seg" and "turn_want" tune knobs: set them BEFORE sizing a workspace
+  // (csm_portfolio_workspace), never between sizing and the call
   // (cohort-parallel grids, kpar = 1, made tens of thousands of tiny workgroups at C3 and
   // ran slower than one workgroup walking its K cohorts over a chunk.)
   (void)K;

@@ -128,8 +128,8 @@ class SweepConfig:
     boot_scan: bool = True
     # batches of fewer than JOIN_ROWS (month, panel) rows (C3's single panel): the Js' decile
     # passes and accounting as one launch set over the Js side by side (_account_joined); the
-    # same table and series bit for bit (batches of up to four panels share one chunk plan,
-    # portfolio.hip pf_plan; tests/test_gpu_fullsize.py::test_c3_joined_js_equal_per_j)
+    # same table and series bit for bit (taken only where the side-by-side batch has the chunk
+    # plan of one J's batch, _joined; tests/test_gpu_fullsize.py::test_c3_joined_js_equal_per_j)
     join_js: bool = True
     # bootstrap batches: the Js' cohort sums in one pass over the shared next_ret
     # (csm_cohort_sums_js: each month's return row read once for every J; same table bit for bit)
@@ -146,6 +146,17 @@ class SweepConfig:
     @property
     def strategies(self):
         return strategy_grid(self.Js, self.Ks)
+
+
+def _refuse_capture(what):
+    """The round-3 hipGraph replay fault came from a capture of the joined C3
+    step on the per-J chunked scans and the streaming narrow decile pass; its cause was never
+    named.  Those launches stay available eagerly (configs outside the multi-J kernels' domain,
+    A/B knobs) but are never captured: a joined step that would take them under stream capture
+    is refused before it records anything."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(f"SweepRunner: {what} are not captured into a hipGraph (DESIGN.md 4.3); "
+                           "run this configuration eagerly")
 
 
 def _legs_labels(c, legs, N):
@@ -204,6 +215,10 @@ class SweepRunner:
         self.group = group
         self.G = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # accounting branch of each bootstrap batch run_bootstrap ran, in order: "jsg" (the
+        # grouped shared-return launch set), "shared" (one cohort pass, per-J accounting),
+        # "per_j" or "materialised" (csm_bootstrap -> run_batch)
+        self.boot_paths = []
 
     def run_batch(self, PMb: torch.Tensor, B: int, W=None, ADV=None, SIG=None, defer=False):
         """PMb [T_m][B*N] month prices of B panels -> summary [B][S][F] and the per-strategy
@@ -267,12 +282,22 @@ class SweepRunner:
     def _run_batch(self, PMb, B, W, ADV, SIG, flag):
         return self._account(self._ranked(PMb, B, legs=flag is not None), B, W, ADV, SIG, flag)
 
-    def _joined(self, T_m, B):
+    def _joined(self, T_m, B, N):
         """Whether a batch this small runs its Js' decile passes and accounting as one launch
-        set over the Js side by side (join_js; every J's panels then live at once)."""
-        c = self.cfg
-        return (c.join_js and hasattr(self.st, "summary") and len(c.Js) > 1
-                and T_m * B < JOIN_ROWS)
+        set over the Js side by side (join_js; every J's panels then live at once).  Only where
+        the portfolio chunk plan of the nJ * B side-by-side panels is the plan of B panels, so a
+        joined batch -- and a strategy-sharded rank joining fewer Js (the plan is monotone in
+        the panel count) -- keeps the per-J launches' TURN / COST bits (pf_plan treats batches
+        below four panels as four, not wider ones: T_m = 300, B = 2 plans two turnover chunks
+        joined against four per J)."""
+        c, st = self.cfg, self.st
+        if not (c.join_js and hasattr(st, "summary") and len(c.Js) > 1 and T_m * B < JOIN_ROWS):
+            return False
+        if hasattr(st, "portfolio_plan"):
+            Km = max(c.Ks)
+            return (st.portfolio_plan(T_m, B, N, c.n_bins, Km)
+                    == st.portfolio_plan(T_m, len(c.Js) * B, N, c.n_bins, Km))
+        return True
 
     def _ranked(self, PMb, B, legs=False):
         """(J, L, NR) per J of the grid from the month prices of a batch: one J's ranking
@@ -283,7 +308,7 @@ class SweepRunner:
         T_m, BN = PMb.shape
         N = BN // B
         lg = {"legs": True} if _legs_labels(c, legs, N) else {}
-        if self._joined(T_m, B):
+        if self._joined(T_m, B, N):
             # every J from one time-chunked scan where it applies (csm_momentum_multi_chunked:
             # C3 scan 0.245 ms for four chunked scans), with the bucket ids for the decile pass
             Cm = (c.scan_chunks or st.default_chunks(T_m, BN, max(c.Js), c.skip)
@@ -296,8 +321,11 @@ class SweepRunner:
                 MN = st.momentum_multi(PMb, c.Js, c.skip, with_ids=ids, chunks=Cm,
                                        stacked=c.grouped)
             else:
+                _refuse_capture("the per-J time-chunked scans")
                 ids = False
                 MN = [st.momentum(PMb, J, c.skip)[1:] for J in c.Js]
+            if not ids:
+                _refuse_capture("the streaming narrow decile pass")
             Mcat = _stacked([mo[0] for mo in MN]).view(len(MN) * T_m * B, N)
             if ids:
                 Lcat, _, _, _ = st.deciles_ids(
@@ -335,6 +363,7 @@ class SweepRunner:
                 L, _, _, _ = st.deciles_ids(M.reshape(T_m * B, N), None,
                                             IDS.reshape(T_m * B, N), c.n_bins, **lg)
             else:
+                _refuse_capture("the streaming narrow decile pass")
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS
             yield J, L.reshape(T_m, BN), NR
@@ -346,7 +375,7 @@ class SweepRunner:
         c, st = self.cfg, self.st
         ranked = iter(ranked)
         first = next(ranked)
-        if self._joined(first[1].shape[0], B):
+        if self._joined(first[1].shape[0], B, first[1].shape[1] // B):
             return self._account_joined([first] + list(ranked), B, W, ADV, SIG, flag)
         ranked = itertools.chain([first], ranked)
         rows, series, summ = [], {}, {}
@@ -469,7 +498,7 @@ class SweepRunner:
         # passes, one cohort pass and ONE accounting launch set for every J -- where the batch's
         # chunk plan is that of the Js' panels side by side, so every table entry keeps its bits
         nJ, Km = len(c.Js), max(c.Ks)
-        jsg = (ids and c.share_nr and c.grouped and nJ > 1 and not self._joined(T_m, B)
+        jsg = (ids and c.share_nr and c.grouped and nJ > 1 and not self._joined(T_m, B, N)
                and hasattr(st, "portfolio_multi_js_grouped") and hasattr(st, "portfolio_plan")
                and st.portfolio_plan(T_m, B, N, c.n_bins, Km)
                == st.portfolio_plan(T_m, nJ * B, N, c.n_bins, Km))
@@ -492,14 +521,16 @@ class SweepRunner:
                 L, _, _, _ = st.deciles(M.reshape(T_m * B, N), None, c.n_bins)
             del M, IDS
             labels.append((J, L.reshape(T_m, B * N), NR))
+        shared = False
         if jsg:
             out = self._account_js_grouped(Lg.view(nJ, T_m, B * N), NR, B, flag)
         else:
             shared = (c.share_nr and hasattr(st, "portfolio_multi_js") and len(labels) > 1
-                      and not self._joined(T_m, B))
+                      and not self._joined(T_m, B, N))
             acc = self._account_shared if shared else self._account
             out = acc(labels, B, None, None, None, flag)
         del labels, NR, Lg
+        self.boot_paths.append("jsg" if jsg else ("shared" if shared else "per_j"))
         state = bad * 2 + (flag if legs else 0)
 
         def redo(v):   # holds no panel: a flagged batch is recomputed from its seed
@@ -564,6 +595,7 @@ class SweepRunner:
             else:
                 _, PMb = self.st.bootstrap(R_base, B, b0=b0, seed=seed, mean_block=mean_block)
                 summ, _ = self.run_batch(PMb, B)
+                self.boot_paths.append("materialised")
             mine.append(summ)
         if pend:
             states = torch.cat([s for _, s, _ in pend]).tolist()   # one sync for every batch

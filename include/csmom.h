@@ -48,7 +48,8 @@ int csm_abi_version(void);
  * (csm_momentum_multi: 2 register ring, two assets per lane | 1 one asset | 0 the LDS ring),
  * "dec_narrow_max" (widest row for the narrow-row decile kernels), "cohort_seg" / "cohort_lds"
  * (portfolio cohort-sum kernel: label-sorted segments (rows <= 7168) | per-wave LDS sums |
- * register sums), "turn_want" (turnover workgroups per launch, default 4096; set before sizing
+ * register sums; "cohort_seg" changes the chunk plan, so set it before sizing the portfolio
+ * workspace), "turn_want" (turnover workgroups per launch, default 4096; set before sizing
  * the portfolio workspace), "turn_gen_grid" (workgroups of the general-row turnover launch,
  * default 8192), "overlap_rows" (1 one thread per (month, panel, decile) for single-chunk
  * plans | 0 one per (K, month, panel, decile)), "gen_reset" (1 the turnover work-list counter

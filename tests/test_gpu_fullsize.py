@@ -8,8 +8,9 @@ is exact for those columns: month prices, mom_J and next_ret bit for bit on all 
 mom_J; counts exact and decile means / long-short within 1e-10 of the oracle's portfolio.
 C3: the 5,000 x 6,522-day value-weighted 16-strategy grid with square-root-impact costs, every
 (J, K), against the portfolio oracle (rules E1-E5).  C5: SweepRunner.run_bootstrap at the
-bench's layout (5,000 assets, 300 months, one batch of 100 panels, 16 strategies, turnover +
-spread costs); sampled panels' summary rows against the oracle stages.
+bench's layout (5,000 assets, 300 months, 16 strategies, turnover + spread costs) in each batch
+geometry the bench runs (200 panels on one GPU, 125 per rank on 8, and 100); sampled panels'
+summary rows against the oracle stages, and the accounting branch each batch took.
 """
 import numpy as np
 import pytest
@@ -185,20 +186,40 @@ def test_c3_sweep_runner_summary(engine, c3):
 
 
 # ------------------------------------------------------------------------------------ C5
+# Geometries of the C5 bench (bench.py --config c5): 1000 panels in device batches of 200 on one
+# GPU (the default), 125 panels per rank on 8 ranks (one batch of 125), and batches of 100 (the
+# round-4 default).  Whether a batch takes the grouped shared-return accounting (sweep.py
+# _boot_batch, "jsg") depends on the portfolio chunk plan at that width, so each geometry is
+# checked against the oracle on its own and the branch it took is asserted.
+C5_GEOMETRIES = {100: [0, 7, 13, 29, 42, 57, 64, 86, 93, 99],
+                 200: [0, 13, 57, 99, 100, 128, 150, 177, 198, 199],
+                 125: [0, 7, 31, 62, 63, 64, 88, 100, 117, 124]}
+
+
 @pytest.fixture(scope="module")
-def c5(engine):
-    import csmom
+def c5_base(engine):
     from csmom.synth import bday_calendar, make_device_panel
     N, T_d = 5_000, 6_522
     days, ms_h, _ = bday_calendar("2000-01-03", T_d)
     pan = make_device_panel(N, days, ms_h, seed=4 * 1000 + 5, device="cuda:0")
     PM0, _ = engine.month_end(pan.P, pan.month_start)
     R0, _, _ = engine.momentum(PM0, 12, 1, with_ret=True)
-    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
-    summ = csmom.SweepRunner(engine, cfg).run_bootstrap(R0, 100, seed=5000, mean_block=6.0,
-                                                         batch=100)
     torch.cuda.synchronize()
-    return cfg, R0, summ.cpu().numpy()
+    return R0, R0.cpu().numpy()
+
+
+@pytest.fixture(scope="module", params=sorted(C5_GEOMETRIES))
+def c5(engine, c5_base, request):
+    """One device batch of `batch` panels through SweepRunner.run_bootstrap, as the bench runs
+    it; also the accounting branch the batch took."""
+    import csmom
+    R0, _ = c5_base
+    batch = request.param
+    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    runner = csmom.SweepRunner(engine, cfg)
+    summ = runner.run_bootstrap(R0, batch, seed=5000, mean_block=6.0, batch=batch)
+    torch.cuda.synchronize()
+    return cfg, R0, summ.cpu().numpy(), batch, list(runner.boot_paths)
 
 
 def _oracle_panel_summary(cfg, R_h, b):
@@ -222,25 +243,33 @@ def _summary_rows(LS, TURN, COST, NET, freq=12.0):
     return _summary_ref(LS, TURN, COST, NET, freq)
 
 
-def test_c5_shape_and_finite(c5):
-    cfg, R0, summ = c5
-    assert summ.shape == (100, 16, 7)
+def test_c5_shape_and_branch(engine, c5):
+    """Every bench geometry runs one batch, through the grouped shared-return accounting: its
+    chunk plan at the batch width equals the plan of the four look-backs side by side (C5: one
+    cohort chunk and one turnover chunk either way)."""
+    cfg, R0, summ, batch, paths = c5
+    assert summ.shape == (batch, 16, 7)
     assert np.isfinite(summ[..., :3]).all()
+    assert paths == ["jsg"], paths
+    T_m, N = R0.shape
+    assert (engine.portfolio_plan(T_m, batch, N, 10, 12)
+            == engine.portfolio_plan(T_m, 4 * batch, N, 10, 12))
 
 
-@pytest.mark.parametrize("b", [0, 7, 13, 29, 42, 57, 64, 86, 93, 99])
-def test_c5_sampled_panels_vs_oracle(c5, b):
-    """Ten of the batch's 100 bootstrap panels: every (J, K) summary row against the oracle
-    stages within north_star's 1e-10 relative (fp64 sums in another order; months exact)."""
-    cfg, R0, summ = c5
-    ref = _oracle_panel_summary(cfg, R0.cpu().numpy(), b)
+@pytest.mark.parametrize("k", range(10))
+def test_c5_sampled_panels_vs_oracle(c5, c5_base, k):
+    """Ten of each batch's bootstrap panels: every (J, K) summary row against the oracle stages
+    within north_star's 1e-10 relative (fp64 sums in another order; months exact)."""
+    cfg, R0, summ, batch, _ = c5
+    b = C5_GEOMETRIES[batch][k]
+    ref = _oracle_panel_summary(cfg, c5_base[1], b)
     got = summ[b]
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     assert np.array_equal(got[:, 0], ref[:, 0])                 # months per strategy
     m = ~np.isnan(ref)
     scale = np.maximum(np.abs(ref[m]), 1e-12)
     err = np.abs(got[m] - ref[m]) / scale
-    assert err.max() <= 1e-10, (b, float(err.max()))
+    assert err.max() <= 1e-10, (batch, b, float(err.max()))
 
 
 def test_c5_boot_scan_equals_materialised(engine, c5):
@@ -248,9 +277,9 @@ def test_c5_boot_scan_equals_materialised(engine, c5):
     multi-J scan -> decile pass on the whole C5 batch: the summary table bit for bit."""
     import csmom
     from dataclasses import replace
-    cfg, R0, summ = c5
+    cfg, R0, summ, batch, _ = c5
     off = csmom.SweepRunner(engine, replace(cfg, boot_scan=False)).run_bootstrap(
-        R0, 100, seed=5000, mean_block=6.0, batch=100).cpu().numpy()
+        R0, batch, seed=5000, mean_block=6.0, batch=batch).cpu().numpy()
     assert bits_equal(summ, off)
 
 
@@ -271,3 +300,25 @@ def test_c3_joined_js_equal_per_j(engine, c3):
             x, y = getattr(sa[key], f), getattr(sb[key], f)
             assert x.shape == y.shape, (key, f)
             assert bits_equal(x.cpu().numpy(), y.cpu().numpy()), (key, f)
+
+
+def test_c3_two_panel_batch_joins_only_on_equal_plans(engine, c3):
+    """A 2-panel C3 batch (T_m * B < JOIN_ROWS): the four look-backs side by side would plan
+    two turnover chunks against four per J (pf_plan treats batches below four panels as four),
+    so the batch is NOT joined and its table equals the per-J launches' bit for bit; the
+    single-panel batch (plans equal) is joined."""
+    import csmom
+    from dataclasses import replace
+    PM, W, ADV = c3
+    T_m, N = PM.shape
+    PM2 = torch.cat([PM, PM * 1.5], 1).contiguous()
+    W2 = torch.cat([W, W * 0.5], 1).contiguous()
+    ADV2 = torch.cat([ADV, ADV * 0.5], 1).contiguous()
+    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    run = csmom.SweepRunner(engine, cfg)
+    assert run._joined(T_m, 1, N)
+    assert not run._joined(T_m, 2, N)
+    assert engine.portfolio_plan(T_m, 2, N, 10, 12) != engine.portfolio_plan(T_m, 8, N, 10, 12)
+    a, _ = run.run_batch(PM2, 2, W=W2, ADV=ADV2)
+    b, _ = csmom.SweepRunner(engine, replace(cfg, join_js=False)).run_batch(PM2, 2, W=W2, ADV=ADV2)
+    assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
