@@ -30,8 +30,10 @@ struct csm_ctx {
   int n_cu;               // compute units of the device (decile kernel choice)
   int32_t* dec_flg;       // [dec_flg_n] rows the merged decile pass left to the general kernel
   int32_t dec_flg_n;      // (allocated at create, so a captured pipeline never allocates)
-  int32_t* ticket;        // the fused long-short's arrival counter (zeroed at create; the last
-                          // workgroup of each decile launch resets it)
+  int32_t* ticket;        // the fused long-short's arrival counter (zeroed at create; it wraps
+                          // back to 0 on each decile launch's last increment)
+  void* dsplit;           // the split decile pass's workspace (DecSplit), grown lazily
+  size_t dsplit_bytes;
   void* comm;             // RCCL communicator of csm_allgather_init (collective.hip), or NULL
   int comm_rank, comm_size;
 };
@@ -126,6 +128,25 @@ __device__ __forceinline__ uint32_t csm_fid(double x) {
   return x == x ? (uint32_t)csm_fbucket(x) : CSM_FB_NAN;
 }
 
+// The split decile pass on ids (deciles.inc, wide rows): device workspace of the plan / sweep /
+// finish launches, carved from the context's split buffer (csmom.hip dsplit_layout).
+#define SPLIT_CELLS 16384   // cells per sweep chunk (fixed: chunking depends on N only)
+#define SPLIT_THREADS 256
+#define SPLIT_WAVES (SPLIT_THREADS / 64)
+#define SPLIT_FL 1024       // uncertain cells a sweep wave can list per chunk
+#define DSPLAN_BYTES 4096   // one row's DsPlan
+#define DSPLIT_MAXL 512     // (chunk, wave) lists per row the finish launch merges
+struct DecSplit {
+  char* plan;        // [T_m] DsPlan (slots, targets, ranked count)
+  int8_t* tab;       // [T_m][8192] bucket -> label (-1 NaN, >= 0 certain, <= -2 uncertain)
+  double* ph;        // [T_m][C][NB] the certain cells' next_ret sums per label (two-sum high,
+  double* pl;        //   low) and counts, per chunk
+  int32_t* pc;
+  int32_t* ucnt;     // [T_m][C][SPLIT_WAVES] uncertain cells listed per (chunk, wave)
+  uint32_t* ulist;   // [T_m][C][SPLIT_WAVES][SPLIT_FL] their cell indices
+  int C;             // chunks per row: ceil(N / SPLIT_CELLS)
+};
+
 // narrow-row decile launcher (deciles_narrow.hip), NB in {0,2,3,4,5,10,20}
 template <int NB>
 void launch_deciles_narrow(bool v2, int T_m, hipStream_t st, const double* M, const double* NR,
@@ -141,6 +162,14 @@ void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* 
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
                         int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg, double* LS,
                         int32_t* ticket);
+
+// the split pass (plan, chunked sweep, finish + the general path for the rows it leaves) on
+// wide rows of short date shards; flg (T_m ints) required
+template <int NB>
+void launch_deciles_split(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
+                          int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
+                          int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg,
+                          const DecSplit& sp, double* LS, int32_t* ticket);
 
 // the same on narrow rows (deciles_npre.hip: 2048 buckets = the fixed map's ids >> 2); flg
 // non-NULL with decile sums: ONE launch, a row the merged pass gives up taking the general path

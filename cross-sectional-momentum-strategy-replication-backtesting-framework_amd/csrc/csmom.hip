@@ -1245,37 +1245,47 @@ __device__ __forceinline__ double shard_pm_at(const double* __restrict__ PM,
 
 // Same record as k_shard_summary (n, fv, lvi, lv, head, first; tail of the last T present
 // month prices, ABSENT-padded at the front) from the SH state's n / first / last month.
+// idx (the halo pass's fallback columns): output column j < ncol is asset idx[j] (record rows
+// ncol apart); columns past the list's length *cnt get the record of an asset with no present
+// month (a neutral column for k_fold_carry).
 __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __restrict__ PM,
                                                              const double* __restrict__ P,
                                                              const int64_t* __restrict__ ms,
                                                              int T_m, int64_t N, int T,
                                                              const double* __restrict__ st,
-                                                             double* __restrict__ out) {
+                                                             double* __restrict__ out,
+                                                             const int32_t* __restrict__ idx,
+                                                             const int32_t* __restrict__ cnt,
+                                                             int64_t ncol) {
   const int W = T - 1;
-  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= N) return;
-  const int64_t n = (int64_t)st[a];
-  const int fm = (int)st[3 * N + a], lm = (int)st[4 * N + a];
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (idx ? ncol : N)) return;
+  const int64_t os = idx ? ncol : N;   // output row stride
+  out += j;
+  const bool listed = !idx || j < (int64_t)*cnt;
+  const int64_t a = idx ? (listed ? (int64_t)idx[j] : 0) : j;
+  const int64_t n = listed ? (int64_t)st[a] : 0;
+  const int fm = listed ? (int)st[3 * N + a] : -1, lm = listed ? (int)st[4 * N + a] : -1;
   int64_t fv = -1, lvi = -1;
   double lv = qnan(), head = qnan(), first = absent_val();
   const int k = (int)(n < T ? n : T);
-  for (int j = 0; j < T - k; ++j) out[(int64_t)(SUM_SCALARS + j) * N + a] = absent_val();
+  for (int q = 0; q < T - k; ++q) out[(int64_t)(SUM_SCALARS + q) * os] = absent_val();
   if (n > 0) {
     // forward from the first present month: first price, index of the first valid row
     first = shard_pm_at(PM, P, ms, fm, T_m, W, N, a);
-    int64_t idx = 0;
+    int64_t ix = 0;
     bool found = false;
     for (int m0 = fm; m0 <= lm && !found; m0 += WALK_CHUNK) {
       double buf[WALK_CHUNK];
 #pragma unroll
-      for (int j = 0; j < WALK_CHUNK; ++j)
-        buf[j] = (m0 + j <= lm) ? shard_pm_at(PM, P, ms, m0 + j, T_m, W, N, a) : absent_val();
+      for (int q = 0; q < WALK_CHUNK; ++q)
+        buf[q] = (m0 + q <= lm) ? shard_pm_at(PM, P, ms, m0 + q, T_m, W, N, a) : absent_val();
 #pragma unroll
-      for (int j = 0; j < WALK_CHUNK; ++j) {
-        const double x = buf[j];
+      for (int q = 0; q < WALK_CHUNK; ++q) {
+        const double x = buf[q];
         if (found || is_absent(x)) continue;
-        if (!isnan_d(x)) { fv = idx; found = true; }
-        ++idx;
+        if (!isnan_d(x)) { fv = ix; found = true; }
+        ++ix;
       }
     }
     // backward from the last present month: tail, last valid (lv, lvi), head
@@ -1285,16 +1295,16 @@ __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __res
     for (int m0 = lm; m0 >= fm && !done; m0 -= WALK_CHUNK) {
       double buf[WALK_CHUNK];
 #pragma unroll
-      for (int j = 0; j < WALK_CHUNK; ++j)
-        buf[j] = (m0 - j >= fm) ? shard_pm_at(PM, P, ms, m0 - j, T_m, W, N, a) : absent_val();
+      for (int q = 0; q < WALK_CHUNK; ++q)
+        buf[q] = (m0 - q >= fm) ? shard_pm_at(PM, P, ms, m0 - q, T_m, W, N, a) : absent_val();
 #pragma unroll
-      for (int j = 0; j < WALK_CHUNK; ++j) {
-        const double x = buf[j];
+      for (int q = 0; q < WALK_CHUNK; ++q) {
+        const double x = buf[q];
         if (done || is_absent(x)) continue;
         const bool valid = !isnan_d(x);
         if (valid && !have_lv) { lv = x; lvi = n - 1 - seen; have_lv = true; }
         if (got < k) {
-          out[(int64_t)(SUM_SCALARS + T - 1 - got) * N + a] = x;
+          out[(int64_t)(SUM_SCALARS + T - 1 - got) * os] = x;
           ++got;
         } else if (valid) {
           head = x;
@@ -1304,12 +1314,12 @@ __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __res
       }
     }
   }
-  out[0 * N + a] = (double)n;
-  out[1 * N + a] = (double)fv;
-  out[2 * N + a] = (double)lvi;
-  out[3 * N + a] = lv;
-  out[4 * N + a] = head;
-  out[5 * N + a] = first;
+  out[0 * os] = (double)n;
+  out[1 * os] = (double)fv;
+  out[2 * os] = (double)lvi;
+  out[3 * os] = lv;
+  out[4 * os] = head;
+  out[5 * os] = first;
 }
 
 // F's step: scan_step without outputs (the state transition only).
@@ -1341,22 +1351,28 @@ __device__ __forceinline__ bool same_bits(double x, double y) {
   return __double_as_longlong(x) == __double_as_longlong(y);
 }
 
+// fcarry: F's initial state (the halo pass's carry, [W+2][N]); NULL = empty (the speculative
+// pass).  idx (the halo pass's fallback columns): thread j repairs asset idx[j] for j < *cnt,
+// with carry / next_pm column j (rows ncol apart); NULL = every asset, carry / next_pm [.][N].
 __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
     const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
     int T_m, int64_t N, int J, int skip,
     const double* __restrict__ carry, const double* __restrict__ next_pm,
     const double* __restrict__ st, double* __restrict__ R, double* __restrict__ M,
-    double* __restrict__ NR, uint16_t* __restrict__ IDS) {
+    double* __restrict__ NR, uint16_t* __restrict__ IDS, const double* __restrict__ fcarry,
+    const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int64_t ncol) {
   extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][W][REPAIR_THREADS]
   const int W = J + skip, RS = REPAIR_THREADS;
   const int tid = threadIdx.x;
-  const int64_t a = (int64_t)blockIdx.x * REPAIR_THREADS + tid;
-  if (a >= N) return;  // no barriers below
+  const int64_t j = (int64_t)blockIdx.x * REPAIR_THREADS + tid;
+  if (idx ? (j >= ncol || j >= (int64_t)*cnt) : j >= N) return;  // no barriers below
+  const int64_t a = idx ? (int64_t)idx[j] : j;
+  const int64_t cs = idx ? ncol : N, cj = idx ? j : a;   // carry / next_pm stride and column
   double* rt = lds + tid;
   double* rf = lds + W * RS + tid;
   ScanLane t, f;
-  scan_init(t, rt, RS, W, carry, N, a, true);
-  scan_init(f, rf, RS, W, nullptr, N, a, true);
+  scan_init(t, rt, RS, W, carry, cs, cj, true);
+  scan_init(f, rf, RS, W, fcarry, N, a, true);
   auto same = [&]() -> bool {
     if (!same_bits(t.pff, f.pff) || !same_bits(t.psff, f.psff) || t.prev != f.prev) return false;
     for (int k = 0; k < W; ++k)
@@ -1371,13 +1387,13 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
   for (int m0 = fm < 0 ? 0 : fm; m0 < T_m && !done; m0 += REPAIR_CHUNK) {
     double buf[REPAIR_CHUNK];
 #pragma unroll
-    for (int j = 0; j < REPAIR_CHUNK; ++j)
-      buf[j] = (m0 + j < T_m) ? shard_pm_at(PM, P, ms, m0 + j, T_m, W, N, a) : absent_val();
+    for (int q = 0; q < REPAIR_CHUNK; ++q)
+      buf[q] = (m0 + q < T_m) ? shard_pm_at(PM, P, ms, m0 + q, T_m, W, N, a) : absent_val();
 #pragma unroll
-    for (int j = 0; j < REPAIR_CHUNK; ++j) {
-      const int m = m0 + j;
+    for (int q = 0; q < REPAIR_CHUNK; ++q) {
+      const int m = m0 + q;
       if (m >= T_m || done) break;
-      const double x = buf[j];
+      const double x = buf[q];
       const double mom = scan_step(t, x, m, rt, RS, W, J, N, a, R, M, NR);
       if (IDS) IDS[(int64_t)m * N + a] = (uint16_t)csm_fid(mom);   // the rewritten cell's bucket id
       scan_shadow(f, x, m, rf, RS, W, J);
@@ -1391,13 +1407,199 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
   const double psff = conv ? st[2 * N + a] : t.psff;
   if (prev >= 0) {
     double nr = qnan();
-    const double x = next_pm[a];
+    const double x = next_pm[cj];
     if (!is_absent(x)) {
       const double ps_new = isnan_d(x) ? psff : x;
       nr = ps_new / psff - 1.0;
     }
     NR[(int64_t)prev * N + a] = nr;
   }
+}
+
+// =====================================================================================
+// Halo date shards (the default multi-GPU pass; north_star's "J + skip lookback
+// halo").  A rank holds its shard's daily rows plus H calendar months before it and the first
+// month after it.  k_shard_halo builds the scan state the halo months leave (from an empty
+// state) and the forward month's price; the state is EXACT -- equal to the one the whole
+// history leaves -- whenever the halo holds two valid prices W = J + skip present months apart
+// (fv, lv below): the ring's W factors then all follow a valid price, and the last valid price
+// is a ranked row in both histories.  k_signal<SH> starts from that state and the forward
+// price, so a dense asset's outputs are final after one pass and no record is exchanged for
+// it.  The other assets (listed inside the halo or the shard, long gaps, a forward month with
+// no row) are flagged; only they take the exchange-and-repair path, over a column list.
+// =====================================================================================
+#define HALO_THREADS 256
+#define HALO_U 8
+#define HALO_WALK 8
+#define HALO_MAXG 64
+
+// Month-end of asset a over day rows [d0, d1) (k_signal's reduction: last valid price, NaN if
+// the month has rows but no price, ABSENT if none), walked back from the last row: one load for
+// the usual month whose last row holds a price, else rows HALO_WALK at a time in flight.
+__device__ __forceinline__ double halo_month_price(const double* __restrict__ P, int64_t d0,
+                                                   int64_t d1, int64_t N, int64_t a) {
+  if (d1 <= d0) return absent_val();
+  const double xl = P[(d1 - 1) * N + a];
+  if (xl == xl) return xl;
+  bool p = !is_absent(xl);
+  for (int64_t d = d1 - 2; d >= d0; d -= HALO_WALK) {
+    double xs[HALO_WALK];
+#pragma unroll
+    for (int u = 0; u < HALO_WALK; ++u) xs[u] = d - u >= d0 ? P[(d - u) * N + a] : absent_val();
+#pragma unroll
+    for (int u = 0; u < HALO_WALK; ++u) {
+      if (xs[u] == xs[u]) return xs[u];
+      p |= !is_absent(xs[u]);
+    }
+  }
+  return p ? qnan() : absent_val();
+}
+
+// The halo months' and the forward month's prices, one thread per (asset, month): PMh[j][N],
+// j < H halo month j, j = H the forward month (F = 1).  A wave whose lanes walk a month back
+// (no price on its last day: listings, delistings, absent months) does not hold up the others.
+__global__ __launch_bounds__(HALO_THREADS) void k_halo_pm(const double* __restrict__ P,
+                                                          const int64_t* __restrict__ ms, int H,
+                                                          int T_m, int64_t N,
+                                                          double* __restrict__ PMh) {
+  const int64_t a = (int64_t)blockIdx.x * HALO_THREADS + threadIdx.x;
+  const int j = blockIdx.y;
+  if (a >= N) return;
+  const int m = j < H ? j : H + T_m;
+  PMh[(int64_t)j * N + a] = halo_month_price(P, ms[m], ms[m + 1], N, a);
+}
+
+// months [0, H) of ms are the halo, [H, H + T_m) the shard, [H + T_m, H + T_m + F) the forward
+// month (F 0 or 1), their prices in PMh (k_halo_pm).  before: the panel has months before the
+// halo (else the halo is the whole history and its state exact); after: the panel has months
+// after the shard (else next_pm is ABSENT, exactly).  carry [W+2][N] (csm_signal's layout),
+// next_pm [N], flags [N]: bit 0 the carry may differ from the whole history's, bit 1 next_pm
+// may.
+__global__ __launch_bounds__(HALO_THREADS) void k_shard_halo(
+    const double* __restrict__ PMh, int H, int F, int before, int after, int64_t N, int J,
+    int skip, double* __restrict__ carry, double* __restrict__ next_pm,
+    uint8_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) double hring[];  // [W][HALO_THREADS]
+  const int W = J + skip, RS = HALO_THREADS;
+  const int64_t a = (int64_t)blockIdx.x * HALO_THREADS + threadIdx.x;
+  if (a >= N) return;  // no barriers below
+  double* ring = hring + threadIdx.x;
+  ScanLane s;
+  scan_init(s, ring, RS, W, nullptr, N, a, true);
+  int n = 0, fv = -1, lv = -1;
+  for (int m0 = 0; m0 < H; m0 += HALO_U) {
+    double xs[HALO_U];   // HALO_U month prices in flight
+#pragma unroll
+    for (int u = 0; u < HALO_U; ++u)
+      xs[u] = m0 + u < H ? PMh[(int64_t)(m0 + u) * N + a] : absent_val();
+#pragma unroll
+    for (int u = 0; u < HALO_U; ++u) {
+      const double x = xs[u];
+      if (m0 + u >= H || is_absent(x)) continue;
+      if (!isnan_d(x)) { if (fv < 0) fv = n; lv = n; }
+      ++n;
+      scan_shadow(s, x, m0 + u, ring, RS, W, J);
+    }
+  }
+  int ix = s.head;
+  for (int k = 0; k < W; ++k) {   // ring factors, oldest first (scan_finish's carry_out)
+    carry[(int64_t)k * N + a] = ring[ix * RS];
+    ix = (ix + 1 == W) ? 0 : ix + 1;
+  }
+  carry[(int64_t)W * N + a] = s.pff;
+  carry[(int64_t)(W + 1) * N + a] = s.psff;
+  uint8_t fl = 0;
+  if (before && !(fv >= 0 && lv - fv >= W)) fl |= 1;
+  const double npm = F > 0 ? PMh[(int64_t)H * N + a] : absent_val();
+  if (after && is_absent(npm)) fl |= 2;
+  next_pm[a] = npm;
+  flags[a] = fl;
+}
+
+// This rank's exchange bits, one per asset, 64 per word (a wave's ballot), rows of nw words:
+// 0 an uncertain carry and a present month in the shard; 1 an uncertain forward price and a
+// pending ranked row at the shard's end; 2 a present month in the shard; 3 a present month
+// before the shard's last Hn months (those in the next rank's halo).  The union below decides
+// from every rank's rows which assets really need the exchange.
+__global__ __launch_bounds__(256) void k_shard_need(const uint8_t* __restrict__ flags,
+                                                    const double* __restrict__ st, int64_t N,
+                                                    int T_m, int Hn, int64_t nw,
+                                                    uint64_t* __restrict__ mask) {
+  const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool c0 = false, c1 = false, pa = false, ph = false;
+  if (a < N) {
+    const uint8_t f = flags[a];
+    pa = st[a] > 0.0;
+    c0 = (f & 1) && pa;
+    c1 = (f & 2) && st[N + a] >= 0.0;
+    const double fm = st[3 * N + a];
+    ph = fm >= 0.0 && fm < (double)(T_m - Hn);
+  }
+  const uint64_t b0 = __ballot(c0), b1 = __ballot(c1), b2 = __ballot(pa), b3 = __ballot(ph);
+  if ((threadIdx.x & 63) == 0 && a < N) {
+    const int64_t w = a >> 6;
+    mask[w] = b0;
+    mask[nw + w] = b1;
+    mask[2 * nw + w] = b2;
+    mask[3 * nw + w] = b3;
+  }
+}
+
+// The assets that need the exchange on some rank, from every rank's k_shard_need rows
+// [G][4][nw]: rank g needs asset a when its carry is uncertain and the asset has a row before
+// g's halo (a row in a shard before g - 1, or in shard g - 1 before its last H months), or its
+// forward price is uncertain and a later shard has a row -- otherwise the halo's state / ABSENT
+// IS the whole history's.  The union as an ascending list of asset indices (the same on every
+// rank): idx[0 .. min(count, cap)), *count = its full length (> cap: the list overflowed and
+// the pass must take the all-gather path).  One workgroup.
+#define UNION_THREADS 1024
+__global__ __launch_bounds__(UNION_THREADS) void k_shard_union(const uint64_t* __restrict__ masks,
+                                                               int G, int64_t nw, int64_t cap,
+                                                               int32_t* __restrict__ idx,
+                                                               int32_t* __restrict__ count) {
+  __shared__ int32_t wsum[UNION_THREADS / 64];
+  __shared__ int64_t base;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) base = 0;
+  __syncthreads();
+  auto row = [&](int g, int r, int64_t w) -> uint64_t { return masks[((int64_t)g * 4 + r) * nw + w]; };
+  for (int64_t w0 = 0; w0 < nw; w0 += UNION_THREADS) {
+    const int64_t w = w0 + tid;
+    uint64_t u = 0;
+    if (w < nw) {
+      uint64_t later[HALO_MAXG];   // a row in a shard after g
+      uint64_t suf = 0;
+      for (int g = G - 1; g >= 0; --g) { later[g] = suf; suf |= row(g, 2, w); }
+      uint64_t A = 0, B = 0, hp = 0;   // rows in shards < g - 1 / in g - 1 / in g - 1's head
+      for (int g = 0; g < G; ++g) {
+        const uint64_t hist = A | hp;   // a row before g's halo
+        u |= (row(g, 0, w) & hist) | (row(g, 1, w) & later[g]);
+        A |= B;
+        B = row(g, 2, w);
+        hp = row(g, 3, w);
+      }
+    }
+    const int c = __popcll(u);
+    int inc = c;   // wave inclusive scan, then the waves in order
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int64_t off = base + inc - c;
+    for (int q = 0; q < wid; ++q) off += wsum[q];
+    while (u) {
+      const int b = __builtin_ctzll(u);
+      u &= u - 1;
+      if (off < cap) idx[off] = (int32_t)(w * 64 + b);
+      ++off;
+    }
+    __syncthreads();
+    if (tid == UNION_THREADS - 1) base = off;
+    __syncthreads();
+  }
+  if (tid == 0) *count = (int32_t)(base < 0x7FFFFFFF ? base : 0x7FFFFFFF);
 }
 
 // =====================================================================================
@@ -1414,6 +1616,11 @@ static int64_t* g_dec_timing = nullptr;
 // PRE decile pass (csm_deciles_ids): 1 the merged sweep, then the general kernel for the rows it
 // leaves | 0 the general kernel only
 static int g_tune_dec_merge = 1;
+// wide rows on ids: 2 (auto) the split decile pass (plan, chunked sweep, finish; deciles.inc) for
+// launches of fewer rows than half the CUs (short date shards), else the merged
+// one-workgroup-per-row pass | 1 always split | 0 never.  Same labels and counts; decile means in
+// another fixed order
+static int g_tune_dec_split = 2;
 // csm_momentum_multi: 2 register shift ring, two assets per lane (even N, aligned) | 1 one asset
 // per lane | 0 the shared-memory ring (max(J) + skip > 16 always takes it)
 static int g_tune_mj_reg = 2;
@@ -1438,6 +1645,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "dec_merge") && (value == 0 || value == 1)) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
+  if (!strcmp(key, "dec_split") && value >= 0 && value <= 2) { g_tune_dec_split = value; return CSM_OK; }
   return CSM_E_INVAL;
 }
 
@@ -1483,11 +1691,12 @@ int csm_create(int device, csm_ctx** out) {
 
 int csm_destroy(csm_ctx* ctx) {
   if (ctx) (void)csm_allgather_free(ctx);
-  if (ctx && (ctx->scratch || ctx->dec_flg || ctx->ticket)) {
+  if (ctx && (ctx->scratch || ctx->dec_flg || ctx->ticket || ctx->dsplit)) {
     (void)hipSetDevice(ctx->device);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->dec_flg) (void)hipFree(ctx->dec_flg);
     if (ctx->ticket) (void)hipFree(ctx->ticket);
+    if (ctx->dsplit) (void)hipFree(ctx->dsplit);
   }
   free(ctx);
   return CSM_OK;
@@ -1633,9 +1842,11 @@ static int signal_launch(csm_ctx* ctx, const char* who, const double* P, int64_t
                          double* carry_out, bool sh = false, uint16_t* ids = nullptr) {
   int r = prep(ctx);
   if (r) return r;
-  if (sh && (!PM || carry || next_pm || !carry_out || T_m < 1))
-    return set_err(ctx, CSM_E_INVAL, "%s: a speculative shard pass needs PM and state, no carry / "
-                   "next_pm, and at least one month", who);
+  // (a shard pass starts from an empty state, or -- the halo pass -- from the halo's carry
+  // and forward price)
+  if (sh && (!PM || !carry_out || T_m < 1))
+    return set_err(ctx, CSM_E_INVAL, "%s: a shard pass needs PM and state, and at least one month",
+                   who);
   if (!P || !month_start || !M || !NR || N <= 0 || T_d < 0 || T_m < 0 || J < 1 || skip < 0 ||
       J + skip > 256 || max_month_days < 1)
     return set_err(ctx, CSM_E_INVAL, "%s: bad arguments (N=%lld T_m=%d J=%d skip=%d)", who,
@@ -1796,6 +2007,32 @@ int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T
   return CSM_OK;
 }
 
+// The split decile pass's workspace for T_m rows of N cells (csm_common.h DecSplit), carved
+// from one context buffer; sized for n_bins up to MAXQ so one buffer serves every NB.
+static size_t dsplit_layout(int32_t T_m, int64_t N, DecSplit* sp, char* base) {
+  const int64_t C = (N + SPLIT_CELLS - 1) / SPLIT_CELLS;
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  size_t o = 0;
+  const size_t plan = o; o = al(o + (size_t)T_m * DSPLAN_BYTES);
+  const size_t tab = o;  o = al(o + (size_t)T_m * CSM_FB_BUCKETS);
+  const size_t ph = o;   o = al(o + (size_t)T_m * C * MAXQ * 8);
+  const size_t pl = o;   o = al(o + (size_t)T_m * C * MAXQ * 8);
+  const size_t pc = o;   o = al(o + (size_t)T_m * C * MAXQ * 4);
+  const size_t uc = o;   o = al(o + (size_t)T_m * C * SPLIT_WAVES * 4);
+  const size_t ul = o;   o = al(o + (size_t)T_m * C * SPLIT_WAVES * SPLIT_FL * 4);
+  if (sp) {
+    sp->plan = base + plan;
+    sp->tab = (int8_t*)(base + tab);
+    sp->ph = (double*)(base + ph);
+    sp->pl = (double*)(base + pl);
+    sp->pc = (int32_t*)(base + pc);
+    sp->ucnt = (int32_t*)(base + uc);
+    sp->ulist = (uint32_t*)(base + ul);
+    sp->C = (int)C;
+  }
+  return o;
+}
+
 static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
                             const double* M, const double* NR, int64_t N, int32_t n_bins,
                             const QTab& q, int8_t* L, double* EW, int32_t* CNT, int32_t* NV,
@@ -1820,6 +2057,42 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
       ctx->dec_flg_n = T_m;
     }
     flg = ctx->dec_flg;
+    // wide rows of a short date shard (fewer rows than half the CUs: one workgroup per row
+    // leaves most of the chip idle): the split pass (plan, chunked sweep over the whole chip,
+    // finish with the fused long-short) when the row's (chunk, wave) lists fit the finish
+    // launch's merge.  Same labels and counts as the merged pass; means in another fixed order.
+    const int64_t C = (N + SPLIT_CELLS - 1) / SPLIT_CELLS;
+    const bool split = g_tune_dec_split == 1 ||
+                       (g_tune_dec_split == 2 && (int64_t)T_m * 2 <= (int64_t)ctx->n_cu);
+    if (split && g_tune_dec_merge && !q.legs && N > g_tune_dec_narrow_max &&
+        C * SPLIT_WAVES <= DSPLIT_MAXL) {
+      const size_t need = dsplit_layout(T_m, N, nullptr, nullptr);
+      if (ctx->dsplit_bytes < need) {
+        if (capturing(ctx))
+          return set_err(ctx, CSM_E_INVAL, "%s: the split decile workspace (%zu B) must grow to %zu B "
+                         "during stream capture; run the call once before capturing", who,
+                         ctx->dsplit_bytes, need);
+        if (ctx->dsplit) HIP_CHECK(ctx, hipFree(ctx->dsplit));
+        ctx->dsplit = nullptr;
+        ctx->dsplit_bytes = 0;
+        HIP_CHECK(ctx, hipMalloc(&ctx->dsplit, need));
+        ctx->dsplit_bytes = need;
+      }
+      DecSplit sp;
+      dsplit_layout(T_m, N, &sp, (char*)ctx->dsplit);
+      int64_t* tm = g_dec_timing;
+      double* lsx = NR ? LSw : nullptr;
+      int32_t* tkx = lsx ? ctx->ticket : nullptr;
+      switch (NR ? n_bins : 0) {
+#define DS_CASE(NBV) case NBV: launch_deciles_split<NBV>(T_m, ctx->stream, M, NR, N, n_bins, q, L, EW, CNT, NV, tm, ids, flg, sp, lsx, tkx); break;
+        DS_CASE(0) DS_CASE(2) DS_CASE(3) DS_CASE(4) DS_CASE(5) DS_CASE(10) DS_CASE(20)
+#undef DS_CASE
+        default:
+          return set_err(ctx, CSM_E_INVAL, "%s: n_bins=%d unsupported with NR (use 2,3,4,5,10,20)", who, n_bins);
+      }
+      LAUNCH_CHECK(ctx, who);
+      return CSM_OK;
+    }
   }
   if (!NR) {
     launch_deciles<0>(v2, T_m, ctx->stream, M, nullptr, N, n_bins, q, L, nullptr, nullptr, NV, ids, pre, flg);
@@ -1990,7 +2263,8 @@ int csm_shard_summary_state(csm_ctx* ctx, const double* P, const int64_t* month_
       J + skip > 256)
     return set_err(ctx, CSM_E_INVAL, "csm_shard_summary_state: bad arguments");
   hipLaunchKernelGGL(k_shard_summary_state, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
-                     ctx->stream, PM, P, month_start, T_m, N, J + skip + 1, state, out);
+                     ctx->stream, PM, P, month_start, T_m, N, J + skip + 1, state, out,
+                     (const int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0);
   LAUNCH_CHECK(ctx, "k_shard_summary_state");
   return CSM_OK;
 }
@@ -2012,7 +2286,8 @@ static int shard_repair(csm_ctx* ctx, const double* P, const int64_t* month_star
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_shard_repair, dim3((unsigned)((N + REPAIR_THREADS - 1) / REPAIR_THREADS)),
                      dim3(REPAIR_THREADS), lds, ctx->stream, PM, P, month_start, T_m, N, J, skip,
-                     carry, next_pm, state, R, M, NR, ids);
+                     carry, next_pm, state, R, M, NR, ids, (const double*)nullptr,
+                     (const int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0);
   LAUNCH_CHECK(ctx, "k_shard_repair");
   return CSM_OK;
 }
@@ -2032,6 +2307,111 @@ int csm_shard_repair_ids(csm_ctx* ctx, const double* P, const int64_t* month_sta
   if (!ids) return set_err(ctx, CSM_E_INVAL, "csm_shard_repair_ids: ids is NULL");
   return shard_repair(ctx, P, month_start, PM, T_m, N, J, skip, carry, next_pm, state, R, M, NR,
                       ids);
+}
+
+// ---- halo date shards (k_shard_halo above; include/csmom.h) -------------------------------
+int csm_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                   const int64_t* month_start, int32_t H, int32_t T_m, int32_t F,
+                   int32_t before, int32_t after, int32_t J, int32_t skip, double* halo_pm,
+                   double* carry, double* next_pm, uint8_t* flags) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !carry || !next_pm || !flags || (H + F > 0 && !halo_pm) || N <= 0 ||
+      T_d <= 0 || H < 0 || T_m < 1 || F < 0 || F > 1 || J < 1 || skip < 0 || J + skip > 64)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_halo: bad arguments (H >= 0, T_m >= 1, F in {0, 1}, "
+                   "J + skip <= 64, halo_pm [H + F][N])");
+  const int W = J + skip;
+  const unsigned bx = (unsigned)((N + HALO_THREADS - 1) / HALO_THREADS);
+  if (H + F > 0) {
+    hipLaunchKernelGGL(k_halo_pm, dim3(bx, (unsigned)(H + F)), dim3(HALO_THREADS), 0, ctx->stream,
+                       P, month_start, H, T_m, N, halo_pm);
+    LAUNCH_CHECK(ctx, "k_halo_pm");
+  }
+  const size_t lds = (size_t)W * HALO_THREADS * sizeof(double);
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_shard_halo,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_shard_halo, dim3(bx), dim3(HALO_THREADS), lds, ctx->stream,
+                     (const double*)halo_pm, H, F, before ? 1 : 0, after ? 1 : 0, N, J, skip, carry,
+                     next_pm, flags);
+  LAUNCH_CHECK(ctx, "k_shard_halo");
+  return CSM_OK;
+}
+
+int csm_signal_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                          const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                          int32_t J, int32_t skip, const double* carry, const double* next_pm,
+                          double* PM, double* R, double* M, double* NR, double* state,
+                          uint16_t* ids) {
+  if (!carry || !next_pm)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_shard_halo: needs the halo's carry and next_pm");
+  if (ids && ((N % 4) != 0 || ((uintptr_t)ids & 7u) != 0))
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_shard_halo: ids need N %% 4 == 0, 8-B alignment");
+  return signal_launch(ctx, "csm_signal_shard_halo", P, T_d, N, month_start, T_m, max_month_days,
+                       J, skip, PM, R, M, NR, carry, next_pm, state, true, ids);
+}
+
+int csm_shard_need(csm_ctx* ctx, const uint8_t* flags, const double* state, int64_t N,
+                   int32_t T_m, int32_t H, uint64_t* mask) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!flags || !state || !mask || N <= 0 || T_m < 1 || H < 0)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_need: bad arguments");
+  hipLaunchKernelGGL(k_shard_need, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream,
+                     flags, state, N, T_m, H, (N + 63) / 64, mask);
+  LAUNCH_CHECK(ctx, "k_shard_need");
+  return CSM_OK;
+}
+
+int csm_shard_union(csm_ctx* ctx, const uint64_t* masks, int32_t G, int64_t N, int64_t cap,
+                    int32_t* idx, int32_t* count) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!masks || !idx || !count || G < 1 || G > HALO_MAXG || N <= 0 || cap < 1 ||
+      N > 0x7FFFFFFFLL)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_union: bad arguments (1 <= G <= %d)", HALO_MAXG);
+  hipLaunchKernelGGL(k_shard_union, dim3(1), dim3(UNION_THREADS), 0, ctx->stream, masks, G,
+                     (N + 63) / 64, cap, idx, count);
+  LAUNCH_CHECK(ctx, "k_shard_union");
+  return CSM_OK;
+}
+
+int csm_shard_summary_cols(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                           const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                           const double* state, const int32_t* idx, const int32_t* count,
+                           int64_t cap, double* out) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !PM || !state || !idx || !count || !out || N <= 0 || T_m < 1 ||
+      cap < 1 || J < 1 || skip < 0 || J + skip > 256)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_summary_cols: bad arguments");
+  hipLaunchKernelGGL(k_shard_summary_state, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0,
+                     ctx->stream, PM, P, month_start, T_m, N, J + skip + 1, state, out, idx,
+                     count, cap);
+  LAUNCH_CHECK(ctx, "k_shard_summary_state (columns)");
+  return CSM_OK;
+}
+
+int csm_shard_repair_cols(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                          const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                          const double* carry, const double* next_pm, const double* fcarry,
+                          const double* state, const int32_t* idx, const int32_t* count,
+                          int64_t cap, double* R, double* M, double* NR, uint16_t* ids) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!P || !month_start || !PM || !carry || !next_pm || !fcarry || !state || !idx || !count ||
+      !M || !NR || N <= 0 || T_m < 1 || cap < 1 || J < 1 || skip < 0 || J + skip > 128)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_repair_cols: bad arguments (J + skip <= 128)");
+  const int W = J + skip;
+  const size_t lds = (size_t)2 * W * REPAIR_THREADS * sizeof(double);
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_shard_repair,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_shard_repair, dim3((unsigned)((cap + REPAIR_THREADS - 1) / REPAIR_THREADS)),
+                     dim3(REPAIR_THREADS), lds, ctx->stream, PM, P, month_start, T_m, N, J, skip,
+                     carry, next_pm, state, R, M, NR, ids, fcarry, idx, count, cap);
+  LAUNCH_CHECK(ctx, "k_shard_repair (columns)");
+  return CSM_OK;
 }
 
 int64_t csm_momentum_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip,

@@ -31,7 +31,30 @@ void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* 
                      ids, flg, LS, ticket);
 }
 
+// the split pass: plan -> chunked sweep -> finish (+ the general kernel for the rows the plan or
+// a sweep chunk left, FLG = 1) -- deciles.inc's split section
+template <int NB>
+void launch_deciles_split(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
+                          int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
+                          int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg,
+                          const DecSplit& sp, double* LS, int32_t* ticket) {
+  hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, true, false, 1>), dim3(T_m),
+                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim, ids, flg,
+                     (double*)nullptr, (int32_t*)nullptr, sp);
+  hipLaunchKernelGGL((dec_pre::k_dsplit_sweep<NB>), dim3((unsigned)sp.C, (unsigned)T_m),
+                     dim3(SPLIT_THREADS), 0, st, NR, (const uint16_t*)ids, N, L, flg, sp);
+  // the finish launch: the listed cells of the rows the plan and sweep took, the general path
+  // for the rows they left; LS given, its last workgroup forms the long-short
+  hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, false, false, 2>), dim3(T_m),
+                     dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim, ids, flg,
+                     LS, ticket, sp);
+}
+
 #define INST(NB)                                                                              \
+  template void launch_deciles_split<NB>(int, hipStream_t, const double*, const double*,        \
+                                         int64_t, int, const QTab&, int8_t*, double*, int32_t*, \
+                                         int32_t*, int64_t*, uint16_t*, int32_t*,              \
+                                         const DecSplit&, double*, int32_t*);                 \
   template void launch_deciles_pre<NB>(int, hipStream_t, const double*, const double*, int64_t, \
                                        int, const QTab&, int8_t*, double*, int32_t*, int32_t*,  \
                                        int64_t*, uint16_t*, int32_t*, double*, int32_t*);

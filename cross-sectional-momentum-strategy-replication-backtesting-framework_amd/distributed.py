@@ -9,7 +9,10 @@ rebuilt exactly from one all-gather of prefix-independent per-asset shard summar
 all-gather of the per-date [T_m_local][n_bins] mean/count rows gives every rank the full
 series; the long-short needs panel-wide column existence (run_demo.py:60-65).
 
-Two collectives per pass; no collective touches daily data.  The stage implementation is
+Two collectives per pass; no collective touches daily data.  The default sharded pass
+(run_halo) gives each rank a lookback halo of daily rows instead, so the exchange shrinks to the
+few assets the halo does not settle (collective 1 then moves N / 8 bytes of need bits and a
+fixed-width record of the listed assets).  The stage implementation is
 injected: `Engine` on the GPU (the product), anything with the same methods elsewhere (the
 CPU tests drive this orchestration with gloo and the oracle).
 """
@@ -165,6 +168,68 @@ class DateShardPipeline:
         _, M, NR = st.momentum(PM, J, s, carry=carry, next_pm=next_pm)
         return self._rank_and_gather(M, NR)
 
+    def fallback_cap(self, N):
+        """Columns of the halo pass's fallback exchange: a fixed width per panel (no size
+        exchange, no host sync), so collective 1b moves S x cap f64 per rank whatever G is."""
+        return fallback_cap(N)
+
+    def run_halo(self, P, month_start, H, F, max_month_days, check=True):
+        """The halo date-shard pass (the default sharded path; north_star's "J + skip lookback
+        halo").  P holds this rank's H halo months, its shard and F (0 / 1) forward months;
+        month_start [H + T_m + F + 1] are day offsets into P.
+
+        1. shard_halo: the halo's scan state and the forward month's price (flags where either
+           may differ from the whole history's);
+        2. signal_shard_halo: the fused pass from that state -- final for unflagged assets;
+        3. shard_need -> collective 1a (all-gather of N / 8 bytes of need bits) -> shard_union:
+           the ascending list of the assets any rank needs (the same on every rank);
+        4. shard_summary_cols: the exchange record of the listed assets only -> collective 1b
+           (all-gather of [S][cap] f64) -> fold_carry -> shard_repair_cols.
+        Bit for bit the all-gather pass (tests/test_gpu_shards_api.py, the gloo tests).
+        check=True: one sync to confirm the list fit its fixed width (else the pass reruns on
+        the all-gather path); check=False leaves that to the caller (self.last_count)."""
+        st, J, s = self.st, self.J, self.skip
+        T_m = month_start.numel() - 1 - H - F
+        self._check_months(T_m)
+        N = P.shape[1]
+        m0 = sum(self.months[:self.rank])
+        carry_h, npm_h, flags = st.shard_halo(P, month_start, H, F, J, s, before=m0 > H,
+                                              after=self.rank < self.G - 1)
+        msh = month_start[H:H + T_m + 1]
+        ids = _shard_ids(st, P, msh)
+        PM, _, M, NR, state = st.signal_shard_halo(P, msh, max_month_days, J, s, carry_h, npm_h,
+                                                   **({} if ids is None else {"ids": ids}))
+        self.last_count = None
+        if self.G > 1:
+            cap = self.fallback_cap(N)
+            mask = st.shard_need(flags, state, H)
+            masks = self.gather(mask)                                  # collective 1a
+            idx, cnt = st.shard_union(masks, N, cap)
+            rec = st.shard_summary_cols(PM, state, idx, cnt, J, s)
+            recs = self.gather(rec)                                    # collective 1b
+            carry_u, npm_u = st.fold_carry(recs, self.rank, J, s)
+            st.shard_repair_cols(PM, carry_u, npm_u, carry_h, state, idx, cnt, M, NR, J, s,
+                                 **({} if ids is None else {"ids": ids}))
+            self.last_count = (cnt, cap)
+            if check and int(cnt.max().item()) > cap:   # every rank sees the same list
+                return self._run_allgather_fallback(P, month_start, H, F, max_month_days)
+        return self._rank_and_gather(M, NR, ids)
+
+    def _run_allgather_fallback(self, P, month_start, H, F, max_month_days):
+        """The halo pass's list overflowed its width: the speculative all-gather pass on the
+        shard's own rows (rare: more flagged assets than cap)."""
+        T_m = month_start.numel() - 1 - H - F
+        d0 = int(month_start[H].item())
+        d1 = int(month_start[H + T_m].item())
+        Ps = P[d0:d1].contiguous()
+        msl = (month_start[H:H + T_m + 1] - d0).contiguous()
+        fused = self.fused
+        self.fused = True
+        try:
+            return self.run(Ps, msl, max_month_days)
+        finally:
+            self.fused = fused
+
     def _rank_and_gather(self, M, NR, ids=None) -> ShardResult:
         st, nb = self.st, self.n_bins
         T_m = M.shape[0]
@@ -202,6 +267,80 @@ def _shard_ids(stages, P, month_start):
     if not _wants_ids(stages, P):
         return None
     return torch.empty((month_start.numel() - 1, P.shape[1]), dtype=torch.int16, device=P.device)
+
+
+def fallback_cap(N):
+    """Width of the halo pass's fallback list: N / 32 columns (at least 2,048, at most N)."""
+    return int(max(1, min(N, max(2048, N // 32))))
+
+
+def halo_months(J, skip):
+    """Calendar months of halo a rank holds before its shard: the window's J + skip present
+    months plus three, so up to three absent / price-less months in the halo still leave the
+    carry exact (k_shard_halo's test: two valid prices J + skip present months apart)."""
+    return int(J) + int(skip) + 3
+
+
+def halo_slices(month_start_host, G, H):
+    """Per shard g of a G-way whole-month split: (d0, d1, hm, F, h0, m0, m1) -- the day range
+    of its halo months, shard and forward month, the halo's month count, F (0 for the last
+    shard), and the first halo month, first shard month and end month."""
+    import numpy as np
+    ms = np.asarray(month_start_host, dtype=np.int64)
+    T_m = len(ms) - 1
+    out = []
+    for (m0, m1) in month_partition(T_m, G):
+        h0 = max(0, m0 - H)
+        F = 1 if m1 < T_m else 0
+        out.append((int(ms[h0]), int(ms[m1 + F]), m0 - h0, F, h0, m0, m1))
+    return out
+
+
+def virtual_shards_halo(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, H=None,
+                        cap=None):
+    """The halo pass's G-shard decomposition run sequentially on ONE device (the collectives
+    replaced by stacks): every shard's halo state, fused pass, need mask, the union list, the
+    listed records, fold and repair -- for single-GPU verification that a G-GPU halo run equals
+    the 1-GPU run bit for bit.  Returns (M, NR, L, EW, CNT, LS, count) with count the union
+    list's length."""
+    import numpy as np
+    H = halo_months(J, skip) if H is None else int(H)
+    ms = np.asarray(month_start_host, dtype=np.int64)
+    dev = P.device
+    N = P.shape[1]
+    cap = fallback_cap(N) if cap is None else int(cap)
+    sh = []
+    for (d0, d1, hm, F, h0, m0, m1) in halo_slices(ms, G, H):
+        Pg = P[d0:d1].contiguous()
+        msg = torch.from_numpy(ms[h0:m1 + F + 1] - d0).to(dev)
+        carry_h, npm_h, flags = stages.shard_halo(Pg, msg, hm, F, J, skip, before=h0 > 0,
+                                                  after=m1 < len(ms) - 1)
+        msh = msg[hm:hm + (m1 - m0) + 1]
+        maxd = int(np.diff(ms[m0:m1 + 1]).max()) if m1 > m0 else 1
+        ids = _shard_ids(stages, Pg, msh)
+        PM, _, M, NR, state = stages.signal_shard_halo(Pg, msh, maxd, J, skip, carry_h, npm_h,
+                                                       **({} if ids is None else {"ids": ids}))
+        sh.append((PM, M, NR, state, ids, carry_h, flags))
+    masks = torch.stack([stages.shard_need(x[6], x[3], H) for x in sh])
+    idx, cnt = stages.shard_union(masks, N, cap)
+    if int(cnt.item()) > cap:   # (one sync: this helper verifies; a wider list, same columns)
+        cap = int(cnt.item())
+        idx, cnt = stages.shard_union(masks, N, cap)
+    recs = torch.stack([stages.shard_summary_cols(x[0], x[3], idx, cnt, J, skip) for x in sh])
+    Ms, NRs, Ls, EWs, CNTs = [], [], [], [], []
+    for g, (PM, M, NR, state, ids, carry_h, _) in enumerate(sh):
+        carry_u, npm_u = stages.fold_carry(recs, g, J, skip)
+        stages.shard_repair_cols(PM, carry_u, npm_u, carry_h, state, idx, cnt, M, NR, J, skip,
+                                 **({} if ids is None else {"ids": ids}))
+        if ids is not None:
+            L, EW, CNT, _ = stages.deciles_ids(M, NR, ids, n_bins)
+        else:
+            L, EW, CNT, _ = stages.deciles(M, NR, n_bins)
+        Ms.append(M); NRs.append(NR); Ls.append(L); EWs.append(EW); CNTs.append(CNT)
+    EW = torch.cat(EWs).contiguous()
+    CNT = torch.cat(CNTs).contiguous()
+    LS = stages.long_short(EW, CNT)
+    return torch.cat(Ms), torch.cat(NRs), torch.cat(Ls), EW, CNT, LS, int(cnt.max().item())
 
 
 def virtual_shards(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, fused=False):

@@ -797,6 +797,98 @@ class Engine:
                        _ptr(R), _ptr(M), _ptr(NR))
         return M, NR
 
+    # ------------------------------------------------------------ halo date shards
+    def shard_halo(self, P, month_start, H, F, J=12, skip=1, before=True, after=True, out=None):
+        """csm_shard_halo: P holds H halo months, the shard and F (0 / 1) forward months
+        (month_start [H + T_m + F + 1], day offsets into P); before / after: the panel has
+        months before the halo / after the shard.  Returns (carry [J+skip+2][N], next_pm [N],
+        flags uint8 [N]; bit 0 carry uncertain, bit 1 next_pm uncertain)."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1 - H - F
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (H + T_m + F + 1,), self.device)
+        if out is None:
+            carry, npm = self.empty((J + skip + 2, N)), self.empty((N,))
+            flags = self.empty((N,), torch.uint8)
+        else:
+            carry, npm, flags = out
+        hpm = self.empty((max(H + F, 1), N))
+        self._call("csm_shard_halo", _ptr(P), T_d, N, _ptr(month_start), int(H), int(T_m),
+                   int(F), int(bool(before)), int(bool(after)), int(J), int(skip), _ptr(hpm),
+                   _ptr(carry), _ptr(npm), _ptr(flags))
+        return carry, npm, flags
+
+    def signal_shard_halo(self, P, month_start, max_month_days, J, skip, carry, next_pm,
+                          with_ret=False, out=None, ids=None):
+        """csm_signal_shard_halo: signal_shard from the halo's carry / next_pm (month_start =
+        the shard's T_m + 1 offsets into P).  Returns (PM, R, M, NR, ShardState)."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1
+        W = J + skip
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        _need(carry, "carry", torch.float64, (W + 2, N), self.device)
+        _need(next_pm, "next_pm", torch.float64, (N,), self.device)
+        if out is None:
+            PM, M, NR = self.empty((T_m, N)), self.empty((T_m, N)), self.empty((T_m, N))
+            R = self.empty((T_m, N)) if with_ret else None
+            state = self.empty((5, N))
+        else:
+            PM, R, M, NR, state = out
+        if ids is not None:
+            _need(ids, "ids", torch.int16, (T_m, N), self.device)
+        self._call("csm_signal_shard_halo", _ptr(P), T_d, N, _ptr(month_start), T_m,
+                   int(max_month_days), int(J), int(skip), _ptr(carry), _ptr(next_pm), _ptr(PM),
+                   _ptr(R), _ptr(M), _ptr(NR), _ptr(state), _ptr(ids))
+        return PM, R, M, NR, ShardState(state, P, month_start)
+
+    def shard_need(self, flags, state, H, out=None):
+        """csm_shard_need -> int64 [4][ceil(N / 64)]: this rank's exchange bits (H = the halo
+        length the next rank holds)."""
+        N = flags.numel()
+        T_m = state.month_start.numel() - 1
+        mask = self.empty((4, (N + 63) // 64), torch.int64) if out is None else out
+        self._call("csm_shard_need", _ptr(flags), _ptr(state.t), N, T_m, int(H), _ptr(mask))
+        return mask
+
+    def shard_union(self, masks, N, cap, out=None):
+        """csm_shard_union over the gathered bits [G][4][ceil(N / 64)] -> (idx int32 [cap],
+        count int32 [1]) on the device (no sync)."""
+        G = masks.shape[0]
+        _need(masks, "masks", torch.int64, (G, 4, (N + 63) // 64), self.device)
+        idx, cnt = ((self.empty((cap,), torch.int32), self.empty((1,), torch.int32))
+                    if out is None else out)
+        self._call("csm_shard_union", _ptr(masks), G, N, int(cap), _ptr(idx), _ptr(cnt))
+        return idx, cnt
+
+    def shard_summary_cols(self, PM, state, idx, cnt, J, skip, out=None):
+        """csm_shard_summary_cols: the exchange record [S][cap] of the listed assets."""
+        T_m, N = PM.shape
+        cap = idx.numel()
+        S = 6 + J + skip + 1
+        out = self.empty((S, cap)) if out is None else out
+        _need(out, "summary", torch.float64, (S, cap), self.device)
+        self._call("csm_shard_summary_cols", _ptr(state.P), _ptr(state.month_start), _ptr(PM),
+                   T_m, N, int(J), int(skip), _ptr(state.t), _ptr(idx), _ptr(cnt), cap,
+                   _ptr(out))
+        return out
+
+    def shard_repair_cols(self, PM, carry, next_pm, fcarry, state, idx, cnt, M, NR, J, skip,
+                          R=None, ids=None):
+        """csm_shard_repair_cols: repair the listed assets from their folded carry / next_pm
+        columns ([.][cap]); fcarry = the halo carry the pass started from."""
+        T_m, N = PM.shape
+        cap = idx.numel()
+        W = J + skip
+        _need(carry, "carry", torch.float64, (W + 2, cap), self.device)
+        _need(next_pm, "next_pm", torch.float64, (cap,), self.device)
+        _need(fcarry, "fcarry", torch.float64, (W + 2, N), self.device)
+        self._call("csm_shard_repair_cols", _ptr(state.P), _ptr(state.month_start), _ptr(PM),
+                   T_m, N, int(J), int(skip), _ptr(carry), _ptr(next_pm), _ptr(fcarry),
+                   _ptr(state.t), _ptr(idx), _ptr(cnt), cap, _ptr(R), _ptr(M), _ptr(NR),
+                   _ptr(ids))
+        return M, NR
+
     def sync(self):
         self._call("csm_sync")
 

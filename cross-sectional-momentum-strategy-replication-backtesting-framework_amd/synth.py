@@ -158,3 +158,64 @@ def make_device_panel(N: int, days: pd.DatetimeIndex, month_start: np.ndarray, s
         mend = pd.DatetimeIndex(mend.astype("datetime64[ns]"))
     return DevicePanel(P=P, month_start=ms_dev, month_start_host=np.asarray(month_start),
                        days=days, month_end=mend)
+
+
+@dataclass
+class HaloPanel:
+    """Rank `rank`'s rows of a whole-month date split with its lookback halo: P holds the last
+    H months of the previous shard, this shard, and the first F (0 / 1) months of the next
+    (DateShardPipeline.run_halo's input); month_start [H + T_m + F + 1] are day offsets into P."""
+    P: torch.Tensor
+    month_start: torch.Tensor
+    month_start_host: np.ndarray
+    H: int
+    F: int
+    T_m: int                     # this shard's months
+    shard_days: int              # this shard's business days (its share of the panel)
+
+    @property
+    def shard_month_start(self):
+        return self.month_start[self.H:self.H + self.T_m + 1]
+
+
+def make_halo_panel(N: int, start: str, periods_total: int, world: int, rank: int, H: int,
+                    seed_of, base_seed: int, device, days_per_shard: float | None = None,
+                    **kw) -> HaloPanel:
+    """Shard `rank` of one global panel (make_device_panel(shard=...), rank r seeded with
+    seed_of(r)) with H months of the previous shard and the next shard's first month: the
+    neighbours' panels are generated with their own seeds and sliced, so the halo rows are
+    exactly the rows those ranks hold."""
+    dps = periods_total / world if days_per_shard is None else days_per_shard
+
+    def shard(r):
+        days, ms, _, months = shard_calendar(start, periods_total, world, r)
+        return make_device_panel(N, days, ms, seed=seed_of(r), device=device,
+                                 shard=(r, world, base_seed, dps), **kw), ms
+    me, ms_me = shard(rank)
+    parts, mss = [], []
+    h = 0
+    if rank > 0 and H > 0:
+        prev, ms_p = shard(rank - 1)
+        h = min(H, len(ms_p) - 1)
+        d0 = int(ms_p[len(ms_p) - 1 - h])
+        parts.append(prev.P[d0:])
+        mss.append(ms_p[len(ms_p) - 1 - h:-1] - d0)
+        del prev
+    off = sum(int(p.shape[0]) for p in parts)
+    parts.append(me.P)
+    mss.append(ms_me[:-1] + off)
+    off += int(me.P.shape[0])
+    F = 0
+    if rank < world - 1:
+        nxt, ms_n = shard(rank + 1)
+        parts.append(nxt.P[:int(ms_n[1])])
+        mss.append(np.array([off], dtype=np.int64))
+        off += int(ms_n[1])
+        F = 1
+        del nxt
+    ms_ext = np.concatenate(mss + [np.array([off], dtype=np.int64)]).astype(np.int64)
+    P = torch.cat(parts, 0).contiguous() if len(parts) > 1 else me.P
+    del parts, me
+    return HaloPanel(P=P, month_start=torch.from_numpy(ms_ext).to(torch.device(device)),
+                     month_start_host=ms_ext, H=h, F=F, T_m=len(ms_me) - 1,
+                     shard_days=int(ms_me[-1]))

@@ -44,7 +44,9 @@ int csm_abi_version(void);
  * drive the fallbacks on inputs that would not reach them): "signal_vec" (2 paired 16-B rows |
  * 1 one asset per lane, the odd-N path), "signal_bwf" (0 auto | 1 one-wave blocks | 4 the wide
  * panels' four barrier-free waves with buffer loads), "dec_merge" (1 the merged decile sweep on
- * ids, the general kernel for the rows it leaves | 0 the general kernel only), "mj_reg"
+ * ids, the general kernel for the rows it leaves | 0 the general kernel only), "dec_split" (1
+ * wide rows on ids: the split pass -- plan, chunked sweep, finish | 0 the merged pass with one
+ * workgroup per row; same labels and counts, means in another fixed order), "mj_reg"
  * (csm_momentum_multi: 2 register ring, two assets per lane | 1 one asset | 0 the LDS ring),
  * "dec_narrow_max" (widest row for the narrow-row decile kernels), "cohort_seg" / "cohort_lds"
  * (portfolio cohort-sum kernel: label-sorted segments (rows <= 7168) | per-wave LDS sums |
@@ -303,6 +305,57 @@ int csm_shard_repair_ids(csm_ctx* ctx, const double* P, const int64_t* month_sta
                          const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
                          const double* carry, const double* next_pm, const double* state,
                          double* R, double* M, double* NR, uint16_t* ids);
+
+/*
+ * Halo date shards (the default multi-GPU pass; no reference counterpart, SURVEY 8(e) and
+ * north_star's "J + skip lookback halo").  A rank holds the daily rows of H calendar months
+ * before its shard, its T_m shard months and F (0 or 1) months after it, month_start[H + T_m +
+ * F + 1] (day offsets into P, the 'ME' groups of features.py:38).
+ * csm_shard_halo: the scan state the halo months leave from an empty state (carry
+ *   [(J+skip)+2][N], csm_signal's layout), the forward month's price next_pm[N] (ABSENT when F
+ *   is 0 or the asset has no row in it), and flags[N]: bit 0 the carry may differ from the one
+ *   the whole history leaves (before != 0 -- the panel has months before the halo -- and the
+ *   halo lacks two valid prices J + skip present months apart), bit 1 next_pm may differ
+ *   (after != 0 -- the panel has months after the shard -- and no forward row).  halo_pm:
+ *   workspace [H + F][N] (the halo and forward months' prices).
+ * csm_signal_shard_halo: csm_signal_shard from that carry and next_pm (month_start = the
+ *   shard's T_m + 1 offsets, still into P); unflagged assets' outputs are final.
+ * csm_shard_need: this rank's exchange bits mask[4][ceil(N / 64)] (bit a % 64 of word a / 64):
+ *   row 0 flag bit 0 and a present month in the shard, row 1 flag bit 1 and a pending ranked
+ *   row at its end, row 2 a present month, row 3 a present month before the shard's last H
+ *   months (the part outside the next rank's halo).
+ * csm_shard_union: from every rank's rows [G][4][ceil(N / 64)], the assets some rank needs --
+ *   an uncertain carry and a row before that rank's halo, or an uncertain forward price and a
+ *   row in a later shard -- as the ascending list idx[min(*count, cap)]; *count its full
+ *   length (> cap: overflow -- take the all-gather path).  Same list on every rank.
+ * csm_shard_summary_cols: csm_shard_summary_state's record for the listed assets only,
+ *   out[S][cap] (columns past *count: an asset with no present month).  All-gather it, fold it
+ *   with csm_fold_carry (N = cap), and:
+ * csm_shard_repair_cols: csm_shard_repair of the listed assets, their carry / next_pm columns
+ *   from that fold ([.][cap]); fcarry = this rank's halo carry (the state the pass started from).
+ */
+int csm_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                   const int64_t* month_start, int32_t H, int32_t T_m, int32_t F,
+                   int32_t before, int32_t after, int32_t J, int32_t skip, double* halo_pm,
+                   double* carry, double* next_pm, uint8_t* flags);
+int csm_signal_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                          const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                          int32_t J, int32_t skip, const double* carry, const double* next_pm,
+                          double* PM, double* R, double* M, double* NR, double* state,
+                          uint16_t* ids);
+int csm_shard_need(csm_ctx* ctx, const uint8_t* flags, const double* state, int64_t N,
+                   int32_t T_m, int32_t H, uint64_t* mask);
+int csm_shard_union(csm_ctx* ctx, const uint64_t* masks, int32_t G, int64_t N, int64_t cap,
+                    int32_t* idx, int32_t* count);
+int csm_shard_summary_cols(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                           const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                           const double* state, const int32_t* idx, const int32_t* count,
+                           int64_t cap, double* out);
+int csm_shard_repair_cols(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                          const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                          const double* carry, const double* next_pm, const double* fcarry,
+                          const double* state, const int32_t* idx, const int32_t* count,
+                          int64_t cap, double* R, double* M, double* NR, uint16_t* ids);
 
 /*
  * Portfolio accounting beyond the reference's K = 1 equal-weight case (SURVEY 8(f) rank 2;

@@ -70,10 +70,10 @@ def main():
         L, EW, CNT, _ = eng.deciles_ids(M, NR, IDS, nb)
         return eng.long_short(EW, CNT), M, NR, L
 
-    def staged():
+    def staged():   # the product path (bucket ids), HIP events between its stages
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
         ev[0].record()
-        PM, _, M, NR, st = eng.signal_shard(p1.P, p1.month_start, maxd, J, skip)
+        PM, _, M, NR, st = eng.signal_shard(p1.P, p1.month_start, maxd, J, skip, ids=IDS)
         ev[1].record()
         S1 = eng.shard_summary(PM, J, skip, state=st)
         ev[2].record()
@@ -81,14 +81,32 @@ def main():
         ev[3].record()
         carry, npm = eng.fold_carry(SS, 1, J, skip)
         ev[4].record()
-        eng.shard_repair(PM, carry, npm, st, M, NR, J, skip)
+        eng.shard_repair(PM, carry, npm, st, M, NR, J, skip, ids=IDS)
         ev[5].record()
-        L, EW, CNT, _ = eng.deciles(M, NR, nb)
+        L, EW, CNT, _ = eng.deciles_ids(M, NR, IDS, nb)
         ev[6].record()
         torch.cuda.synchronize()
         names = ["signal+PM", "shard_summary", "stack", "fold_carry", "shard_repair",
-                 "deciles"]
+                 "deciles_ids"]
         return {n: round(ev[i].elapsed_time(ev[i + 1]), 4) for i, n in enumerate(names)}
+
+    def decile_ab():   # the shard's decile pass on ids: split (auto) vs merged, interleaved
+        _, _, M, NR, _ = eng.signal_shard(p1.P, p1.month_start, maxd, J, skip, ids=IDS)
+        out, res = {}, {}
+        for _ in range(reps):
+            for v in (2, 0):
+                assert eng.lib.csm_tune(b"dec_split", v) == 0
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                r = eng.deciles_ids(M, NR, IDS, nb)
+                e1.record()
+                torch.cuda.synchronize()
+                out.setdefault(v, []).append(e0.elapsed_time(e1))
+                res[v] = r
+        assert eng.lib.csm_tune(b"dec_split", 2) == 0
+        same = bool(torch.equal(res[2][0], res[0][0]) and torch.equal(res[2][2], res[0][2]))
+        return {"split_ms": round(float(np.median(out[2])), 4),
+                "merged_ms": round(float(np.median(out[0])), 4), "labels_counts_equal": same}
 
     fns = dict(single=single, unfused=unfused, fused=fused, fused_ids=fused_ids)
     for f in fns.values():
@@ -118,7 +136,8 @@ def main():
     print(json.dumps({"N": N, "T_d": int(p1.P.shape[0]), "T_m": int(p1.month_start.numel() - 1),
                       "ms_median": {k: round(float(np.median(v)), 4) for k, v in times.items()},
                       "ms_min": {k: round(float(np.min(v)), 4) for k, v in times.items()},
-                      "fused_stages_ms": staged(),
+                      "fused_ids_stages_ms": staged(),
+                      "deciles_ids_ab": decile_ab(),
                       "fused_equals_unfused": equal}), flush=True)
 
 

@@ -1,0 +1,120 @@
+"""One-GPU rehearsal of a halo date-shard rank's pass (DateShardPipeline.run_halo) at C4 width:
+rank 1 of a 3-rank whole-month split (a middle rank: halo before, forward month after), each
+rank `days_per_rank` business days -- 1,250 days is an 8-way strong-scaling shard of C4.  The
+collectives are replaced by stacks of this rank's own tensors (G copies: the bytes a G-rank
+all-gather would deliver), so the numbers are the per-rank device cost without xGMI.
+
+Times, interleaved (median of `reps`): the halo pass, the speculative all-gather pass
+(signal_shard from an empty state, full summary, fold, repair) and the 1-GPU pipeline on the
+shard alone; per-stage HIP events of the halo pass; |U| (the assets this rank lists).
+Prints one JSON line.  Usage: exp_shard_halo.py [N] [days_per_rank] [reps] [G]"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+import csmom  # noqa: E402
+from csmom.distributed import fallback_cap, halo_months  # noqa: E402
+from csmom.synth import make_halo_panel  # noqa: E402
+
+
+def main():
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+    dpr = int(sys.argv[2]) if len(sys.argv) > 2 else 1_250
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    G = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+    dev = torch.device("cuda", 0)
+    eng = csmom.Engine(0)
+    J, skip, nb = 12, 1, 10
+    H = halo_months(J, skip)
+    hp = make_halo_panel(N, "1980-01-01", 3 * dpr, 3, 1, H, seed_of=lambda r: 1000 + r,
+                         base_seed=1, device=dev)
+    P, ms, T_m = hp.P, hp.month_start, hp.T_m
+    msh = hp.shard_month_start
+    mh = hp.month_start_host
+    maxd = int(np.diff(mh).max())
+    cap = fallback_cap(N)
+    IDS = torch.empty((T_m, N), dtype=torch.int16, device=dev)
+    # the shard alone, for the speculative pass and the 1-GPU reference point
+    d0, d1 = int(mh[hp.H]), int(mh[hp.H + T_m])
+    Ps = P[d0:d1].contiguous()
+    mss = (msh - d0).contiguous()
+    torch.cuda.synchronize()
+
+    def halo(ev=None):
+        rec = (lambda i: ev[i].record()) if ev else (lambda i: None)
+        rec(0)
+        carry_h, npm_h, flags = eng.shard_halo(P, ms, hp.H, hp.F, J, skip)
+        rec(1)
+        PM, _, M, NR, st = eng.signal_shard_halo(P, msh, maxd, J, skip, carry_h, npm_h, ids=IDS)
+        rec(2)
+        mask = eng.shard_need(flags, st, hp.H)
+        masks = torch.stack([mask] * G)
+        idx, cnt = eng.shard_union(masks, N, cap)
+        rec(3)
+        rcd = eng.shard_summary_cols(PM, st, idx, cnt, J, skip)
+        recs = torch.stack([rcd] * G)
+        rec(4)
+        carry_u, npm_u = eng.fold_carry(recs, 1, J, skip)
+        eng.shard_repair_cols(PM, carry_u, npm_u, carry_h, st, idx, cnt, M, NR, J, skip, ids=IDS)
+        rec(5)
+        L, EW, CNT, _ = eng.deciles_ids(M, NR, IDS, nb)
+        rec(6)
+        EWg = torch.cat([torch.cat([EW, CNT.to(EW.dtype)], 1)] * G)
+        LS = eng.long_short(EW, CNT)
+        rec(7)
+        return LS, cnt, M, NR, L
+
+    def speculative():
+        PM, _, M, NR, st = eng.signal_shard(Ps, mss, maxd, J, skip, ids=IDS)
+        S1 = eng.shard_summary(PM, J, skip, state=st)
+        SS = torch.stack([S1] * G)
+        carry, npm = eng.fold_carry(SS, 1, J, skip)
+        eng.shard_repair(PM, carry, npm, st, M, NR, J, skip, ids=IDS)
+        L, EW, CNT, _ = eng.deciles_ids(M, NR, IDS, nb)
+        return eng.long_short(EW, CNT)
+
+    def single():
+        return eng.pipeline(Ps, mss, J, skip, nb, max_month_days=maxd, min_month_days=0).LS
+
+    fns = dict(halo=lambda: halo()[0], speculative=speculative, single=single)
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    times = {k: [] for k in fns}
+    for _ in range(reps):
+        for k, f in fns.items():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            times[k].append(1e3 * (time.perf_counter() - t0))
+    names = ["shard_halo", "signal_shard_halo", "need+union", "summary_cols", "fold+repair_cols",
+             "deciles_ids", "gather_emul+long_short"]
+    st_ms = {n: [] for n in names}
+    for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+        _, cnt, _, _, _ = halo(ev)
+        torch.cuda.synchronize()
+        for i, n in enumerate(names):
+            st_ms[n].append(ev[i].elapsed_time(ev[i + 1]))
+    S = 6 + J + skip + 1
+    print(json.dumps({
+        "N": N, "days_per_rank": dpr, "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
+        "F": hp.F, "G_emulated": G, "cap": cap, "listed_this_rank": int(cnt.item()),
+        "collective_bytes_per_rank": {"need_bits": 4 * 8 * ((N + 63) // 64),
+                                      "records": 8 * S * cap,
+                                      "allgather_path_records": 8 * S * N},
+        "ms_median": {k: round(float(np.median(v)), 4) for k, v in times.items()},
+        "ms_min": {k: round(float(np.min(v)), 4) for k, v in times.items()},
+        "halo_stages_ms_median": {n: round(float(np.median(v)), 4) for n, v in st_ms.items()},
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -273,6 +273,56 @@ def test_narrow_fallback_rows_with_long_short(engine, case):
     assert bits_equal(LS.cpu().numpy(), engine.long_short(EW, CNT).cpu().numpy())
 
 
+@pytest.fixture
+def tune_split(engine):
+    lib = engine.lib
+    yield lambda v: lib.csm_tune(b"dec_split", v)
+    lib.csm_tune(b"dec_split", 2)
+
+
+@pytest.mark.parametrize("case", MERGE_CASES)
+def test_deciles_ids_split_equals_merged(engine, tune_split, case):
+    """The split decile pass (plan -> chunked sweep -> finish, the general kernel for the rows
+    it leaves) against the one-workgroup-per-row merged pass: labels, counts and ranked rows bit
+    for bit, means within 1e-13 (another fixed summation order); labels equal the oracle's."""
+    rng = np.random.default_rng(11)
+    x = np.stack([_stress_row(case), _stress_row("lognormal_mild"), _stress_row(case)])
+    nr = rng.normal(0.01, 0.1, x.shape)
+    nr[rng.random(x.shape) < 0.03] = np.nan
+    M, NR, IDS = _up(x), _up(nr), _ids_dev(x)
+    got = {}
+    for v in (1, 0):
+        assert tune_split(v) == 0
+        got[v] = engine.deciles_ids(M, NR, IDS, 10, with_nv=True)
+    (L1, EW1, C1, N1), (L0, EW0, C0, N0) = got[1], got[0]
+    assert torch.equal(L1, L0) and torch.equal(C1, C0) and torch.equal(N1, N0), case
+    a, b = EW1.cpu().numpy(), EW0.cpu().numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b)) and max_rel(a, b) <= 1e-13, case
+    for r in range(x.shape[0]):
+        assert np.array_equal(L1.cpu().numpy()[r], _oracle_labels(x[r])), (case, r)
+    L2, _, _, _ = engine.deciles_ids(M, None, IDS, 10)          # labels only (no next_ret)
+    assert torch.equal(L2, L1), case
+
+
+@pytest.mark.parametrize("N,T", [(40_000, 2_200), (16_388, 900), (65_536, 700)])
+def test_pipeline_split_equals_merged(engine, tune_split, N, T):
+    """The C4 path (csm_pipeline: signal + ids -> decile pass -> long-short) with the split and
+    the merged decile pass: labels / counts bit for bit, means and long-short within 1e-13, and
+    the split pass's labels equal the oracle's qcut; rows of one, several and a partial chunk."""
+    pan = _panel(N=N, T=T, seed=N % 97)
+    P, ms = _up(pan["P"]), _up(pan["month_start"])
+    got = {}
+    for v in (1, 0):
+        assert tune_split(v) == 0
+        got[v] = engine.pipeline(P, ms, 12, 1, 10)
+    a, b = got[1], got[0]
+    assert torch.equal(a.L, b.L) and torch.equal(a.CNT, b.CNT) and torch.equal(a.NV, b.NV)
+    for k in ("EW", "LS"):
+        x, y = getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy()
+        assert np.array_equal(np.isnan(x), np.isnan(y)) and max_rel(x, y) <= 1e-13, k
+    assert np.array_equal(a.L.cpu().numpy(), O.assign_deciles(a.M.cpu().numpy(), 10))
+
+
 def test_pipeline_deciles_repeatable(engine):
     """The wide-row decile pass on ids is deterministic (fixed summation order): two pipeline
     calls give the same bits; labels equal the oracle's on every date."""

@@ -328,3 +328,126 @@ def test_chunked_scan_with_tail_next_pm(engine):
     _, Mc, NRc = engine.momentum_chunked(PM[:-1].contiguous(), 12, 1, chunks=5, next_pm=npm)
     assert bits_equal(NRc.cpu().numpy(), NR.cpu().numpy())
     assert bits_equal(Mc.cpu().numpy(), M.cpu().numpy())
+
+
+# ------------------------------------------------------------------ halo date shards
+def _halo_equal(out, res, ew=True):
+    M, NR, L, EW, CNT, LS, cnt = res
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L)
+    assert torch.equal(CNT, out.CNT)
+    if ew:
+        assert bits_equal(EW.cpu().numpy(), out.EW.cpu().numpy())
+        assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+    return cnt
+
+
+@pytest.mark.parametrize("J,skip", [(12, 1), (3, 0), (9, 2)])
+@pytest.mark.parametrize("G", [2, 3, 5, 8])
+def test_halo_virtual_shards_equal_unsharded(engine, J, skip, G):
+    """Halo shards (k_shard_halo state + k_signal<SH> from it; the exchange and repair only for
+    the assets the halo leaves uncertain) == one pass, bit for bit, on the reference-generated
+    edge panel (late listings, delistings, absent and all-NaN months)."""
+    from csmom.distributed import virtual_shards_halo
+    z = load_golden("edge")
+    P, ms = _up(z["P"]), z["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), J, skip, 10)
+    _halo_equal(out, virtual_shards_halo(engine, P, ms, G, J, skip, 10))
+
+
+@pytest.mark.parametrize("J,skip,G", [(24, 1, 3), (48, 1, 2), (48, 0, 4)])
+def test_halo_shards_long_windows(engine, J, skip, G):
+    from csmom.distributed import virtual_shards_halo
+    z = load_golden("longwin")
+    P, ms = _up(z["P"]), z["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), J, skip, 10)
+    _halo_equal(out, virtual_shards_halo(engine, P, ms, G, J, skip, 10))
+
+
+@pytest.mark.parametrize("G", [2, 7])
+@pytest.mark.parametrize("H", [None, 0, 2])
+def test_halo_shards_sparse_panel(engine, G, H):
+    """Gappy panel (25 % absent months, 15 % NaN months): most assets are flagged and go
+    through the exchange; H = 0 (no halo at all) and H = 2 (shorter than the window) flag
+    every asset with history -- still bit for bit."""
+    from oracle.synth_np import make_panel
+    from csmom.distributed import virtual_shards_halo
+    pan = make_panel(512, 2600, seed=11, nan_day=0.05, absent_month=0.25, nan_month=0.15,
+                     cents=True)
+    P, ms = _up(pan["P"]), pan["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), 12, 1, 10, with_ret=True)
+    cnt = _halo_equal(out, virtual_shards_halo(engine, P, ms, G, 12, 1, 10, H=H), ew=False)
+    assert cnt > 0
+
+
+@pytest.mark.parametrize("G", [2, 7])
+def test_halo_shards_four_wave_blocks(engine, G):
+    from oracle.synth_np import make_panel
+    from csmom.distributed import virtual_shards_halo
+    pan = make_panel(1_000, 2600, seed=13, nan_day=0.05, absent_month=0.2, nan_month=0.1,
+                     cents=True)
+    P, ms = _up(pan["P"]), pan["month_start"].astype(np.int64)
+    out = engine.run(P, _up(ms), 12, 1, 10, with_ret=True)
+    lib = engine.lib
+    try:
+        assert lib.csm_tune(b"signal_bwf", 4) == 0
+        res = virtual_shards_halo(engine, P, ms, G, 12, 1, 10)
+    finally:
+        lib.csm_tune(b"signal_bwf", 0)
+    _halo_equal(out, res, ew=False)
+
+
+@pytest.mark.parametrize("G", [2, 5, 8])
+def test_halo_shards_bucket_ids(engine, G):
+    """Wide rows: halo shards write bucket ids (the repair rewrites the ids of replayed cells)
+    and rank from them -- csm_pipeline's labels, counts and means bit for bit (both sides take
+    the split decile pass at these row counts), the oracle's labels; few assets need the
+    exchange on this panel."""
+    from oracle.synth_np import make_panel
+    from csmom.distributed import virtual_shards_halo
+    pan = make_panel(20_000, 1_400, seed=17, with_volume=False, nan_day=0.03, absent_month=0.05,
+                     nan_month=0.05, cents=True)
+    P, ms = _up(pan["P"]), pan["month_start"].astype(np.int64)
+    out = engine.pipeline(P, _up(ms), 12, 1, 10)
+    res = virtual_shards_halo(engine, P, ms, G, 12, 1, 10)
+    _halo_equal(out, res)
+    ref = O.pipeline(pan["P"], ms, 12, 1, 10)
+    assert np.array_equal(res[2].cpu().numpy(), ref["L"])
+
+
+def test_halo_flags_and_union(engine):
+    """k_shard_halo's flags on hand-made assets; k_shard_need / k_shard_union bit layout."""
+    from csmom.synth import bday_calendar
+    days, ms_h, _ = bday_calendar("2001-01-01", 22 * 40)
+    T_d, N = len(days), 256
+    rng = np.random.default_rng(3)
+    P = np.exp(np.cumsum(rng.normal(0, 0.01, (T_d, N)), 0)) * 50.0
+    ABS = np.array([0x7FF4000000000001], dtype=np.uint64).view(np.float64)[0]
+    H, T_m = 16, 20
+    d_h, d_f = ms_h[H], ms_h[H + T_m]
+    P[:, 1][:d_h] = ABS                       # listed at the shard start: no halo history
+    P[:, 2][:ms_h[H - 5]] = ABS               # 5 halo months: fewer than J + skip + 1
+    P[ms_h[H + T_m]:ms_h[H + T_m + 1], 3] = ABS   # no row in the forward month
+    P[:, 4][d_h:] = ABS                       # delisted at the shard start (no forward row,
+                                              # but no pending row either: not needed)
+    msd = _up(ms_h[:H + T_m + 2].astype(np.int64))
+    Pd = _up(P[:ms_h[H + T_m + 1]])
+    carry, npm, flags = engine.shard_halo(Pd, msd, H, 1, 12, 1, before=True, after=True)
+    f = flags.cpu().numpy()
+    assert f[0] == 0 and f[1] == 1 and f[2] == 1 and f[3] == 2 and f[4] == 2
+    assert O.is_absent(npm.cpu().numpy()[3:4]).all()
+    PM, _, M, NR, st = engine.signal_shard_halo(Pd, msd[H:H + T_m + 1], 23, 12, 1, carry, npm)
+    mask = engine.shard_need(flags, st, H).cpu().numpy().view(np.uint64)
+    cand = mask[0] | mask[1]
+    bits = [(int(cand[a >> 6]) >> (a & 63)) & 1 for a in range(N)]
+    assert bits[:5] == [0, 1, 1, 1, 0] and sum(bits) == 3
+    pres = [(int(mask[2][a >> 6]) >> (a & 63)) & 1 for a in range(N)]
+    assert pres[:5] == [1, 1, 1, 1, 0] and sum(pres) == N - 1
+    # three ranks with these bits: rank 1 has history before its halo (rank 0's head rows) for
+    # assets 1 and 2, and later rows for asset 3's pending row; a cap of 2 overflows
+    idx, cnt = engine.shard_union(torch.stack([engine.shard_need(flags, st, H)] * 3), N, 2)
+    assert int(cnt.item()) == 3 and idx.cpu().numpy().tolist() == [1, 2]
+    # one rank alone: no rank before or after it, so nothing needs the exchange
+    idx, cnt = engine.shard_union(engine.shard_need(flags, st, H)[None], N, 2)
+    assert int(cnt.item()) == 0

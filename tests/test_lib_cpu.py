@@ -75,19 +75,20 @@ def test_tune_keys_documented_in_header_are_accepted():
              b"dec_merge": ([0, 1], 1), b"dec_narrow_max": ([0, 16384], 16384),
              b"mj_reg": ([0, 1, 2], 2), b"cohort_lds": ([0, 1], 1), b"cohort_seg": ([0, 1], 1),
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
-             b"turn_gen_grid": ([1, 2048], 8192), b"gen_reset": ([0, 1], 1), b"turn_vwg": ([0, 1], 1)}
+             b"turn_gen_grid": ([1, 2048], 8192), b"gen_reset": ([0, 1], 1), b"turn_vwg": ([0, 1], 1),
+             b"dec_split": ([0, 1, 2], 2)}
     for key, (vals, default) in cases.items():
         for v in vals:
             assert lib.csm_tune(key, v) == 0, (key, v)
         assert lib.csm_tune(key, default) == 0
     for key, v in ((b"signal_vec", 3), (b"signal_bwf", 2), (b"dec_merge", 2), (b"overlap_rows", 2),
-                   (b"turn_want", 0), (b"gen_reset", 2), (b"no_such_knob", 1)):
+                   (b"turn_want", 0), (b"gen_reset", 2), (b"dec_split", 3), (b"no_such_knob", 1)):
         assert lib.csm_tune(key, v) != 0, (key, v)
     # result-corrupting profiling knobs and negative-result variants are gone
     for key in (b"dec_ablate", b"signal_store", b"signal_rr", b"signal_db", b"signal_mw",
                 b"dec_reg", b"dec_nreg", b"dec_wave_max", b"dec_ids", b"month_end_rows",
                 b"signal_nbuf", b"signal_bw", b"signal_bl", b"turn_list", b"sort_wave",
-                b"seg_stage2", b"turn_prep", b"dec_chunked", b"dec_split"):
+                b"seg_stage2", b"turn_prep", b"dec_chunked"):
         assert lib.csm_tune(key, 0) != 0 and lib.csm_tune(key, 1) != 0, key
     assert lib.csm_tune(None, 1) != 0
 
