@@ -20,6 +20,7 @@ import os
 import sys
 import time
 from pathlib import Path
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -66,9 +67,11 @@ def parse(argv=None):
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="C4 / C2 at N > 1: strong = the fixed panel date-sharded over the ranks "
                          "(BASELINE C4), weak = every rank a full-size month range")
-    ap.add_argument("--shard-mode", default="fused", choices=["fused", "unfused"],
-                    help="N>1 date shards: speculative fused signal + repair, or month-end + "
-                         "carried scan")
+    ap.add_argument("--shard-mode", default="halo", choices=["halo", "fused", "unfused"],
+                    help="N>1 date shards: halo (each rank holds J + skip + 3 lookback months of "
+                         "daily rows; only the assets the halo leaves uncertain are exchanged), "
+                         "speculative fused signal + all-gather + repair, or month-end + carried "
+                         "scan")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-assets", type=int, default=150000)   # ~10-15 s of oracle time
     ap.add_argument("--seed", type=int, default=4)
@@ -318,8 +321,8 @@ def main(argv=None):
     import torch.distributed as dist
 
     import csmom
-    from csmom.distributed import CsmCollective, DateShardPipeline
-    from csmom.synth import make_device_panel, shard_calendar
+    from csmom.distributed import CsmCollective, DateShardPipeline, halo_months
+    from csmom.synth import make_device_panel, make_halo_panel, shard_calendar
 
     world, rank, dev = dist_setup(args)
     local = dev.index
@@ -329,8 +332,15 @@ def main(argv=None):
     days_per_rank = args.days or cfg["days"]
     total_days = days_per_rank * world if args.scaling == "weak" else days_per_rank
     days, ms_host, mend, months = shard_calendar(cfg["start"], total_days, world, rank)
-    panel = make_device_panel(N, days, ms_host, seed=args.seed * 1000 + rank, device=dev,
-                              shard=(rank, world, args.seed, total_days / world))
+    halo = world > 1 and args.shard_mode == "halo"
+    if halo:   # this rank's shard with H lookback months and the next month (neighbours' rows)
+        hp = make_halo_panel(N, cfg["start"], total_days, world, rank, halo_months(12, 1),
+                             seed_of=lambda r: args.seed * 1000 + r, base_seed=args.seed,
+                             device=dev)
+        panel = SimpleNamespace(P=hp.P, month_start=hp.month_start)
+    else:
+        panel = make_device_panel(N, days, ms_host, seed=args.seed * 1000 + rank, device=dev,
+                                  shard=(rank, world, args.seed, total_days / world))
     T_d, T_m = len(days), len(ms_host) - 1
 
     eng = csmom.Engine(local)
@@ -339,7 +349,7 @@ def main(argv=None):
     # preallocated outputs: the timed loop performs no allocation
     max_days = int(np.diff(ms_host).max())
     min_days = int(np.diff(ms_host)[1:-1].min()) if len(ms_host) > 3 else 1 << 30   # interior months
-    fused = eng.use_fused(panel.P, None, max_days)
+    fused = eng.use_fused(panel.P, None, max_days) or halo
     coll = CsmCollective(eng) if world > 1 and args.collective == "csm" else None
     pipe = (DateShardPipeline(eng, months, J, skip, nb,
                               fused=fused and args.shard_mode == "fused", collective=coll)
@@ -381,6 +391,8 @@ def main(argv=None):
 
     def step(ev=scratch_events):
         if pipe is not None:
+            if halo:   # (the fallback list's fit is checked once, after the timed loop)
+                return pipe.run_halo(hp.P, hp.month_start, hp.H, hp.F, max_days, check=False).LS
             r = pipe.run(panel.P, panel.month_start, max_days)
             return r.LS
         rec = (lambda e: e.record()) if ev is not None else (lambda e: None)
@@ -462,8 +474,19 @@ def main(argv=None):
     # N > 1: EVERY rank runs the (collective-bearing) pass and checks its own months; the
     # counts are summed over the ranks.
     from oracle import csmom_oracle as O
+    halo_info = None
     if world > 1:
-        res = pipe.run(panel.P, panel.month_start, max_days)
+        if halo:   # the timed passes' list fit (every rank sees the same list); then a checked pass
+            cnt, cap = pipe.last_count
+            listed = int(cnt.max().item())
+            if listed > cap:
+                raise SystemExit(f"halo pass: {listed} listed assets exceed the list width {cap}; "
+                                 "the timed passes are invalid (rerun with --shard-mode fused)")
+            halo_info = dict(H=hp.H, F=hp.F, listed_assets=listed, list_width=cap,
+                             rows_read_with_halo=int(hp.P.shape[0]), shard_days=hp.shard_days)
+            res = pipe.run_halo(hp.P, hp.month_start, hp.H, hp.F, max_days)
+        else:
+            res = pipe.run(panel.P, panel.month_start, max_days)
         Mh, Lh, LSh, EWh, CNTh = res.M, res.L, res.LS, res.EW, res.CNT
     else:
         Mh, Lh, LSh, EWh, CNTh = M, L, LS, EW, CNT
@@ -546,7 +569,11 @@ def main(argv=None):
                     "NaN days, absent and all-NaN months); N>1: rank r holds date shard r of "
                     "one global panel (prices continue across shards)",
             "hipgraph": graph is not None,
-            "engine_path": (("speculative fused k_signal + k_shard_repair" if pipe.fused else
+            "halo": halo_info,
+            "engine_path": (("halo date shards: k_shard_halo state -> k_signal<SH> (+ ids) -> "
+                             "need bits all-gather -> listed assets' records all-gather, fold, "
+                             "column repair -> decile pass on ids" if halo else
+                             "speculative fused k_signal + k_shard_repair" if pipe.fused else
                              "k_month_end + carried k_momentum") if pipe is not None else
                             "fused k_signal (+ bucket ids) -> k_deciles on ids (+ long-short, one "
                             "launch tail)" if use_ids else

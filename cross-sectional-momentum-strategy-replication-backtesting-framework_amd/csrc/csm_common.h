@@ -130,7 +130,8 @@ __device__ __forceinline__ uint32_t csm_fid(double x) {
 
 // The split decile pass on ids (deciles.inc, wide rows): device workspace of the plan / sweep /
 // finish launches, carved from the context's split buffer (csmom.hip dsplit_layout).
-#define SPLIT_CELLS 16384   // cells per sweep chunk (fixed: chunking depends on N only)
+#define SPLIT_CELLS 16384   // default cells per sweep chunk (csm_tune "dec_split_cells"; the
+                            // chunking depends on N and that knob only, never on the launch)
 #define SPLIT_THREADS 256
 #define SPLIT_WAVES (SPLIT_THREADS / 64)
 #define SPLIT_FL 1024       // uncertain cells a sweep wave can list per chunk
@@ -144,7 +145,8 @@ struct DecSplit {
   int32_t* pc;
   int32_t* ucnt;     // [T_m][C][SPLIT_WAVES] uncertain cells listed per (chunk, wave)
   uint32_t* ulist;   // [T_m][C][SPLIT_WAVES][SPLIT_FL] their cell indices
-  int C;             // chunks per row: ceil(N / SPLIT_CELLS)
+  int C;             // chunks per row: ceil(N / cells)
+  int64_t cells;     // cells per chunk (a multiple of 4 * SPLIT_THREADS)
 };
 
 // narrow-row decile launcher (deciles_narrow.hip), NB in {0,2,3,4,5,10,20}

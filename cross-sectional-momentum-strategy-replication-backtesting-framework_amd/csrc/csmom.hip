@@ -1243,6 +1243,27 @@ __device__ __forceinline__ double shard_pm_at(const double* __restrict__ PM,
   return p ? (v ? last : qnan()) : absent_val();
 }
 
+// WALK_CHUNK month prices of asset a, months m0, m0 + dm, m0 + 2 dm, ... within [lo, hi]
+// (ABSENT outside): the kept months' PM loads are issued together first, the rare months PM
+// does not keep are re-derived after them -- one memory round trip per chunk, not per month.
+__device__ __forceinline__ void shard_pm_chunk(const double* __restrict__ PM,
+                                               const double* __restrict__ P,
+                                               const int64_t* __restrict__ ms, int m0, int dm,
+                                               int lo, int hi, int T_m, int W, int64_t N,
+                                               int64_t a, double (&buf)[WALK_CHUNK]) {
+#pragma unroll
+  for (int q = 0; q < WALK_CHUNK; ++q) {
+    const int m = m0 + q * dm;
+    const bool in = m >= lo && m <= hi;
+    buf[q] = (in && shard_pm_kept(m, T_m, W)) ? PM[(int64_t)m * N + a] : absent_val();
+  }
+#pragma unroll
+  for (int q = 0; q < WALK_CHUNK; ++q) {
+    const int m = m0 + q * dm;
+    if (m >= lo && m <= hi && !shard_pm_kept(m, T_m, W)) buf[q] = shard_pm_at(PM, P, ms, m, T_m, W, N, a);
+  }
+}
+
 // Same record as k_shard_summary (n, fv, lvi, lv, head, first; tail of the last T present
 // month prices, ABSENT-padded at the front) from the SH state's n / first / last month.
 // idx (the halo pass's fallback columns): output column j < ncol is asset idx[j] (record rows
@@ -1277,9 +1298,7 @@ __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __res
     bool found = false;
     for (int m0 = fm; m0 <= lm && !found; m0 += WALK_CHUNK) {
       double buf[WALK_CHUNK];
-#pragma unroll
-      for (int q = 0; q < WALK_CHUNK; ++q)
-        buf[q] = (m0 + q <= lm) ? shard_pm_at(PM, P, ms, m0 + q, T_m, W, N, a) : absent_val();
+      shard_pm_chunk(PM, P, ms, m0, 1, fm, lm, T_m, W, N, a, buf);
 #pragma unroll
       for (int q = 0; q < WALK_CHUNK; ++q) {
         const double x = buf[q];
@@ -1294,9 +1313,7 @@ __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __res
     bool have_lv = false, done = false;
     for (int m0 = lm; m0 >= fm && !done; m0 -= WALK_CHUNK) {
       double buf[WALK_CHUNK];
-#pragma unroll
-      for (int q = 0; q < WALK_CHUNK; ++q)
-        buf[q] = (m0 - q >= fm) ? shard_pm_at(PM, P, ms, m0 - q, T_m, W, N, a) : absent_val();
+      shard_pm_chunk(PM, P, ms, m0, -1, fm, lm, T_m, W, N, a, buf);
 #pragma unroll
       for (int q = 0; q < WALK_CHUNK; ++q) {
         const double x = buf[q];
@@ -1384,11 +1401,10 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
   int64_t seen = 0;
   bool conv = same();
   bool done = conv || npres == 0;
+  static_assert(REPAIR_CHUNK == WALK_CHUNK, "the repair walks months in shard_pm_chunk's batches");
   for (int m0 = fm < 0 ? 0 : fm; m0 < T_m && !done; m0 += REPAIR_CHUNK) {
     double buf[REPAIR_CHUNK];
-#pragma unroll
-    for (int q = 0; q < REPAIR_CHUNK; ++q)
-      buf[q] = (m0 + q < T_m) ? shard_pm_at(PM, P, ms, m0 + q, T_m, W, N, a) : absent_val();
+    shard_pm_chunk(PM, P, ms, m0, 1, 0, T_m - 1, T_m, W, N, a, buf);
 #pragma unroll
     for (int q = 0; q < REPAIR_CHUNK; ++q) {
       const int m = m0 + q;
@@ -1430,7 +1446,7 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
 // =====================================================================================
 #define HALO_THREADS 256
 #define HALO_U 8
-#define HALO_WALK 8
+#define HALO_WALK 24   // a business month's day rows in one batch of loads
 #define HALO_MAXG 64
 
 // Month-end of asset a over day rows [d0, d1) (k_signal's reduction: last valid price, NaN if
@@ -1455,9 +1471,9 @@ __device__ __forceinline__ double halo_month_price(const double* __restrict__ P,
   return p ? qnan() : absent_val();
 }
 
-// The halo months' and the forward month's prices, one thread per (asset, month): PMh[j][N],
-// j < H halo month j, j = H the forward month (F = 1).  A wave whose lanes walk a month back
-// (no price on its last day: listings, delistings, absent months) does not hold up the others.
+// The halo months' and the forward months' prices, one thread per (asset, month): PMh[j][N],
+// j < H halo month j, j = H + f forward month f < F.  A wave whose lanes walk a month back (no
+// price on its last day: listings, delistings, absent months) does not hold up the others.
 __global__ __launch_bounds__(HALO_THREADS) void k_halo_pm(const double* __restrict__ P,
                                                           const int64_t* __restrict__ ms, int H,
                                                           int T_m, int64_t N,
@@ -1465,16 +1481,16 @@ __global__ __launch_bounds__(HALO_THREADS) void k_halo_pm(const double* __restri
   const int64_t a = (int64_t)blockIdx.x * HALO_THREADS + threadIdx.x;
   const int j = blockIdx.y;
   if (a >= N) return;
-  const int m = j < H ? j : H + T_m;
+  const int m = j < H ? j : j + T_m;
   PMh[(int64_t)j * N + a] = halo_month_price(P, ms[m], ms[m + 1], N, a);
 }
 
 // months [0, H) of ms are the halo, [H, H + T_m) the shard, [H + T_m, H + T_m + F) the forward
-// month (F 0 or 1), their prices in PMh (k_halo_pm).  before: the panel has months before the
-// halo (else the halo is the whole history and its state exact); after: the panel has months
-// after the shard (else next_pm is ABSENT, exactly).  carry [W+2][N] (csm_signal's layout),
-// next_pm [N], flags [N]: bit 0 the carry may differ from the whole history's, bit 1 next_pm
-// may.
+// months, their prices in PMh (k_halo_pm).  before: the panel has months before the halo (else
+// the halo is the whole history and its state exact); after: the panel has months after the
+// forward months (else an asset with no row in them has next_pm ABSENT, exactly).  carry
+// [W+2][N] (csm_signal's layout), next_pm [N] (the first forward month with a row), flags [N]:
+// bit 0 the carry may differ from the whole history's, bit 1 next_pm may.
 __global__ __launch_bounds__(HALO_THREADS) void k_shard_halo(
     const double* __restrict__ PMh, int H, int F, int before, int after, int64_t N, int J,
     int skip, double* __restrict__ carry, double* __restrict__ next_pm,
@@ -1510,7 +1526,8 @@ __global__ __launch_bounds__(HALO_THREADS) void k_shard_halo(
   carry[(int64_t)(W + 1) * N + a] = s.psff;
   uint8_t fl = 0;
   if (before && !(fv >= 0 && lv - fv >= W)) fl |= 1;
-  const double npm = F > 0 ? PMh[(int64_t)H * N + a] : absent_val();
+  double npm = absent_val();
+  for (int f = 0; f < F && is_absent(npm); ++f) npm = PMh[(int64_t)(H + f) * N + a];
   if (after && is_absent(npm)) fl |= 2;
   next_pm[a] = npm;
   flags[a] = fl;
@@ -1621,6 +1638,7 @@ static int g_tune_dec_merge = 1;
 // one-workgroup-per-row pass | 1 always split | 0 never.  Same labels and counts; decile means in
 // another fixed order
 static int g_tune_dec_split = 2;
+static int64_t g_tune_dec_split_cells = SPLIT_CELLS;   // cells per split-sweep chunk
 // csm_momentum_multi: 2 register shift ring, two assets per lane (even N, aligned) | 1 one asset
 // per lane | 0 the shared-memory ring (max(J) + skip > 16 always takes it)
 static int g_tune_mj_reg = 2;
@@ -1646,6 +1664,10 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
   if (!strcmp(key, "dec_split") && value >= 0 && value <= 2) { g_tune_dec_split = value; return CSM_OK; }
+  if (!strcmp(key, "dec_split_cells") && value >= 4 * SPLIT_THREADS && value % (4 * SPLIT_THREADS) == 0) {
+    g_tune_dec_split_cells = value;
+    return CSM_OK;
+  }
   return CSM_E_INVAL;
 }
 
@@ -2010,7 +2032,8 @@ int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T
 // The split decile pass's workspace for T_m rows of N cells (csm_common.h DecSplit), carved
 // from one context buffer; sized for n_bins up to MAXQ so one buffer serves every NB.
 static size_t dsplit_layout(int32_t T_m, int64_t N, DecSplit* sp, char* base) {
-  const int64_t C = (N + SPLIT_CELLS - 1) / SPLIT_CELLS;
+  const int64_t CC = g_tune_dec_split_cells;
+  const int64_t C = (N + CC - 1) / CC;
   auto al = [](size_t x) { return (x + 255) / 256 * 256; };
   size_t o = 0;
   const size_t plan = o; o = al(o + (size_t)T_m * DSPLAN_BYTES);
@@ -2029,6 +2052,7 @@ static size_t dsplit_layout(int32_t T_m, int64_t N, DecSplit* sp, char* base) {
     sp->ucnt = (int32_t*)(base + uc);
     sp->ulist = (uint32_t*)(base + ul);
     sp->C = (int)C;
+    sp->cells = CC;
   }
   return o;
 }
@@ -2061,7 +2085,7 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
     // leaves most of the chip idle): the split pass (plan, chunked sweep over the whole chip,
     // finish with the fused long-short) when the row's (chunk, wave) lists fit the finish
     // launch's merge.  Same labels and counts as the merged pass; means in another fixed order.
-    const int64_t C = (N + SPLIT_CELLS - 1) / SPLIT_CELLS;
+    const int64_t C = (N + g_tune_dec_split_cells - 1) / g_tune_dec_split_cells;
     const bool split = g_tune_dec_split == 1 ||
                        (g_tune_dec_split == 2 && (int64_t)T_m * 2 <= (int64_t)ctx->n_cu);
     if (split && g_tune_dec_merge && !q.legs && N > g_tune_dec_narrow_max &&
@@ -2317,8 +2341,8 @@ int csm_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
   int r = prep(ctx);
   if (r) return r;
   if (!P || !month_start || !carry || !next_pm || !flags || (H + F > 0 && !halo_pm) || N <= 0 ||
-      T_d <= 0 || H < 0 || T_m < 1 || F < 0 || F > 1 || J < 1 || skip < 0 || J + skip > 64)
-    return set_err(ctx, CSM_E_INVAL, "csm_shard_halo: bad arguments (H >= 0, T_m >= 1, F in {0, 1}, "
+      T_d <= 0 || H < 0 || T_m < 1 || F < 0 || F > 8 || J < 1 || skip < 0 || J + skip > 64)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_halo: bad arguments (H >= 0, T_m >= 1, 0 <= F <= 8, "
                    "J + skip <= 64, halo_pm [H + F][N])");
   const int W = J + skip;
   const unsigned bx = (unsigned)((N + HALO_THREADS - 1) / HALO_THREADS);

@@ -115,7 +115,7 @@ class DateShardPipeline:
     """
 
     def __init__(self, stages, months_per_rank, J=12, skip=1, n_bins=10, group=None,
-                 fused=False, collective=None):
+                 fused=False, collective=None, halo=None, fwd=None):
         self.st = stages
         # collective: None = torch.distributed (all_gather_stack), or a CsmCollective
         self.gather = (collective.all_gather_stack if collective is not None
@@ -129,6 +129,10 @@ class DateShardPipeline:
         if len(self.months) != self.G:
             raise ValueError(f"months_per_rank has {len(self.months)} entries for {self.G} ranks")
         self.Tmax = max(self.months)
+        # run_halo: the lookback months every rank holds (rank r: min(halo, its first month))
+        self.halo = halo_months(J, skip) if halo is None else int(halo)
+        # ... and the forward months after it (the next rank's first ones)
+        self.fwd = FWD_MONTHS if fwd is None else int(fwd)
 
     def _check_months(self, T_m):
         if T_m != self.months[self.rank]:
@@ -175,13 +179,14 @@ class DateShardPipeline:
 
     def run_halo(self, P, month_start, H, F, max_month_days, check=True):
         """The halo date-shard pass (the default sharded path; north_star's "J + skip lookback
-        halo").  P holds this rank's H halo months, its shard and F (0 / 1) forward months;
+        halo").  P holds this rank's H halo months, its shard and F forward months;
         month_start [H + T_m + F + 1] are day offsets into P.
 
         1. shard_halo: the halo's scan state and the forward month's price (flags where either
            may differ from the whole history's);
         2. signal_shard_halo: the fused pass from that state -- final for unflagged assets;
-        3. shard_need -> collective 1a (all-gather of N / 8 bytes of need bits) -> shard_union:
+        3. shard_need -> collective 1a (all-gather of N / 2 bytes: four bits per asset) ->
+           shard_union:
            the ascending list of the assets any rank needs (the same on every rank);
         4. shard_summary_cols: the exchange record of the listed assets only -> collective 1b
            (all-gather of [S][cap] f64) -> fold_carry -> shard_repair_cols.
@@ -193,8 +198,12 @@ class DateShardPipeline:
         self._check_months(T_m)
         N = P.shape[1]
         m0 = sum(self.months[:self.rank])
+        rest = sum(self.months) - m0 - T_m   # months after this shard
+        if H != min(self.halo, m0) or F != min(self.fwd, rest):
+            raise ValueError(f"rank {self.rank}: P holds {H} halo / {F} forward months, the "
+                             f"pipeline expects {min(self.halo, m0)} / {min(self.fwd, rest)}")
         carry_h, npm_h, flags = st.shard_halo(P, month_start, H, F, J, s, before=m0 > H,
-                                              after=self.rank < self.G - 1)
+                                              after=rest > F)
         msh = month_start[H:H + T_m + 1]
         ids = _shard_ids(st, P, msh)
         PM, _, M, NR, state = st.signal_shard_halo(P, msh, max_month_days, J, s, carry_h, npm_h,
@@ -202,7 +211,9 @@ class DateShardPipeline:
         self.last_count = None
         if self.G > 1:
             cap = self.fallback_cap(N)
-            mask = st.shard_need(flags, state, H)
+            # (row 3: rows before the part of this shard the NEXT rank's halo covers)
+            Hn = min(self.halo, m0 + T_m)
+            mask = st.shard_need(flags, state, Hn)
             masks = self.gather(mask)                                  # collective 1a
             idx, cnt = st.shard_union(masks, N, cap)
             rec = st.shard_summary_cols(PM, state, idx, cnt, J, s)
@@ -269,6 +280,9 @@ def _shard_ids(stages, P, month_start):
     return torch.empty((month_start.numel() - 1, P.shape[1]), dtype=torch.int16, device=P.device)
 
 
+FWD_MONTHS = 3   # forward months a halo rank holds: next_pm is exact unless all three lack a row
+
+
 def fallback_cap(N):
     """Width of the halo pass's fallback list: N / 32 columns (at least 2,048, at most N)."""
     return int(max(1, min(N, max(2048, N // 32))))
@@ -281,17 +295,18 @@ def halo_months(J, skip):
     return int(J) + int(skip) + 3
 
 
-def halo_slices(month_start_host, G, H):
+def halo_slices(month_start_host, G, H, fwd=None):
     """Per shard g of a G-way whole-month split: (d0, d1, hm, F, h0, m0, m1) -- the day range
-    of its halo months, shard and forward month, the halo's month count, F (0 for the last
-    shard), and the first halo month, first shard month and end month."""
+    of its halo months, shard and forward months, the halo's month count, the forward month
+    count F (fewer at the panel's end), and the first halo month, first shard month and end
+    month."""
     import numpy as np
     ms = np.asarray(month_start_host, dtype=np.int64)
     T_m = len(ms) - 1
     out = []
     for (m0, m1) in month_partition(T_m, G):
         h0 = max(0, m0 - H)
-        F = 1 if m1 < T_m else 0
+        F = min(FWD_MONTHS if fwd is None else fwd, T_m - m1)
         out.append((int(ms[h0]), int(ms[m1 + F]), m0 - h0, F, h0, m0, m1))
     return out
 
@@ -314,14 +329,15 @@ def virtual_shards_halo(stages, P, month_start_host, G, J=12, skip=1, n_bins=10,
         Pg = P[d0:d1].contiguous()
         msg = torch.from_numpy(ms[h0:m1 + F + 1] - d0).to(dev)
         carry_h, npm_h, flags = stages.shard_halo(Pg, msg, hm, F, J, skip, before=h0 > 0,
-                                                  after=m1 < len(ms) - 1)
+                                                  after=m1 + F < len(ms) - 1)
         msh = msg[hm:hm + (m1 - m0) + 1]
         maxd = int(np.diff(ms[m0:m1 + 1]).max()) if m1 > m0 else 1
         ids = _shard_ids(stages, Pg, msh)
         PM, _, M, NR, state = stages.signal_shard_halo(Pg, msh, maxd, J, skip, carry_h, npm_h,
                                                        **({} if ids is None else {"ids": ids}))
         sh.append((PM, M, NR, state, ids, carry_h, flags))
-    masks = torch.stack([stages.shard_need(x[6], x[3], H) for x in sh])
+    masks = torch.stack([stages.shard_need(x[6], x[3], min(H, m1))
+                         for x, (_, _, _, _, _, _, m1) in zip(sh, halo_slices(ms, G, H))])
     idx, cnt = stages.shard_union(masks, N, cap)
     if int(cnt.item()) > cap:   # (one sync: this helper verifies; a wider list, same columns)
         cap = int(cnt.item())

@@ -799,10 +799,10 @@ class Engine:
 
     # ------------------------------------------------------------ halo date shards
     def shard_halo(self, P, month_start, H, F, J=12, skip=1, before=True, after=True, out=None):
-        """csm_shard_halo: P holds H halo months, the shard and F (0 / 1) forward months
+        """csm_shard_halo: P holds H halo months, the shard and F (0..8) forward months
         (month_start [H + T_m + F + 1], day offsets into P); before / after: the panel has
-        months before the halo / after the shard.  Returns (carry [J+skip+2][N], next_pm [N],
-        flags uint8 [N]; bit 0 carry uncertain, bit 1 next_pm uncertain)."""
+        months before the halo / after the forward months.  Returns (carry [J+skip+2][N],
+        next_pm [N], flags uint8 [N]; bit 0 carry uncertain, bit 1 next_pm uncertain)."""
         T_d, N = P.shape
         T_m = month_start.numel() - 1 - H - F
         _need(P, "P", torch.float64, (T_d, N), self.device)

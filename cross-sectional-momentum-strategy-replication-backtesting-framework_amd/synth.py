@@ -163,7 +163,7 @@ def make_device_panel(N: int, days: pd.DatetimeIndex, month_start: np.ndarray, s
 @dataclass
 class HaloPanel:
     """Rank `rank`'s rows of a whole-month date split with its lookback halo: P holds the last
-    H months of the previous shard, this shard, and the first F (0 / 1) months of the next
+    H months of the previous shard, this shard, and the first F months of the next
     (DateShardPipeline.run_halo's input); month_start [H + T_m + F + 1] are day offsets into P."""
     P: torch.Tensor
     month_start: torch.Tensor
@@ -180,9 +180,9 @@ class HaloPanel:
 
 def make_halo_panel(N: int, start: str, periods_total: int, world: int, rank: int, H: int,
                     seed_of, base_seed: int, device, days_per_shard: float | None = None,
-                    **kw) -> HaloPanel:
+                    F: int = 3, **kw) -> HaloPanel:
     """Shard `rank` of one global panel (make_device_panel(shard=...), rank r seeded with
-    seed_of(r)) with H months of the previous shard and the next shard's first month: the
+    seed_of(r)) with H months of the previous shard and the next shard's first F months: the
     neighbours' panels are generated with their own seeds and sliced, so the halo rows are
     exactly the rows those ranks hold."""
     dps = periods_total / world if days_per_shard is None else days_per_shard
@@ -205,14 +205,15 @@ def make_halo_panel(N: int, start: str, periods_total: int, world: int, rank: in
     parts.append(me.P)
     mss.append(ms_me[:-1] + off)
     off += int(me.P.shape[0])
-    F = 0
-    if rank < world - 1:
+    f = 0
+    if rank < world - 1 and F > 0:
         nxt, ms_n = shard(rank + 1)
-        parts.append(nxt.P[:int(ms_n[1])])
-        mss.append(np.array([off], dtype=np.int64))
-        off += int(ms_n[1])
-        F = 1
+        f = min(F, len(ms_n) - 1)
+        parts.append(nxt.P[:int(ms_n[f])])
+        mss.append(ms_n[:f] + off)
+        off += int(ms_n[f])
         del nxt
+    F = f
     ms_ext = np.concatenate(mss + [np.array([off], dtype=np.int64)]).astype(np.int64)
     P = torch.cat(parts, 0).contiguous() if len(parts) > 1 else me.P
     del parts, me

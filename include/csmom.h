@@ -309,14 +309,14 @@ int csm_shard_repair_ids(csm_ctx* ctx, const double* P, const int64_t* month_sta
 /*
  * Halo date shards (the default multi-GPU pass; no reference counterpart, SURVEY 8(e) and
  * north_star's "J + skip lookback halo").  A rank holds the daily rows of H calendar months
- * before its shard, its T_m shard months and F (0 or 1) months after it, month_start[H + T_m +
- * F + 1] (day offsets into P, the 'ME' groups of features.py:38).
+ * before its shard, its T_m shard months and F (0..8) months after it, month_start[H + T_m + F
+ * + 1] (day offsets into P, the 'ME' groups of features.py:38).
  * csm_shard_halo: the scan state the halo months leave from an empty state (carry
- *   [(J+skip)+2][N], csm_signal's layout), the forward month's price next_pm[N] (ABSENT when F
- *   is 0 or the asset has no row in it), and flags[N]: bit 0 the carry may differ from the one
- *   the whole history leaves (before != 0 -- the panel has months before the halo -- and the
- *   halo lacks two valid prices J + skip present months apart), bit 1 next_pm may differ
- *   (after != 0 -- the panel has months after the shard -- and no forward row).  halo_pm:
+ *   [(J+skip)+2][N], csm_signal's layout), next_pm[N] = the price of the first forward month
+ *   with a row (ABSENT if none), and flags[N]: bit 0 the carry may differ from the one the
+ *   whole history leaves (before != 0 -- the panel has months before the halo -- and the halo
+ *   lacks two valid prices J + skip present months apart), bit 1 next_pm may differ (after !=
+ *   0 -- the panel has months after the forward months -- and no forward row).  halo_pm:
  *   workspace [H + F][N] (the halo and forward months' prices).
  * csm_signal_shard_halo: csm_signal_shard from that carry and next_pm (month_start = the
  *   shard's T_m + 1 offsets, still into P); unflagged assets' outputs are final.

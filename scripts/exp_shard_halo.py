@@ -1,13 +1,14 @@
 """One-GPU rehearsal of a halo date-shard rank's pass (DateShardPipeline.run_halo) at C4 width:
 rank 1 of a 3-rank whole-month split (a middle rank: halo before, forward month after), each
 rank `days_per_rank` business days -- 1,250 days is an 8-way strong-scaling shard of C4.  The
-collectives are replaced by stacks of this rank's own tensors (G copies: the bytes a G-rank
-all-gather would deliver), so the numbers are the per-rank device cost without xGMI.
+collectives are replaced by stacks of this rank's own tensors (the records: G copies, the bytes a
+G-rank all-gather would deliver; the need bits: the three ranks' own, so the union -- and the
+listed count -- is the real one), so the numbers are the per-rank device cost without xGMI.
 
 Times, interleaved (median of `reps`): the halo pass, the speculative all-gather pass
 (signal_shard from an empty state, full summary, fold, repair) and the 1-GPU pipeline on the
 shard alone; per-stage HIP events of the halo pass; |U| (the assets this rank lists).
-Prints one JSON line.  Usage: exp_shard_halo.py [N] [days_per_rank] [reps] [G]"""
+Prints one JSON line.  Usage: exp_shard_halo.py [N] [days_per_rank] [reps] [G] [split_cells]"""
 import json
 import sys
 import time
@@ -28,12 +29,31 @@ def main():
     dpr = int(sys.argv[2]) if len(sys.argv) > 2 else 1_250
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     G = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+    cells = int(sys.argv[5]) if len(sys.argv) > 5 else 0     # split-sweep chunk (0: default)
     dev = torch.device("cuda", 0)
     eng = csmom.Engine(0)
+    if cells:
+        assert eng.lib.csm_tune(b"dec_split_cells", cells) == 0
     J, skip, nb = 12, 1, 10
     H = halo_months(J, skip)
-    hp = make_halo_panel(N, "1980-01-01", 3 * dpr, 3, 1, H, seed_of=lambda r: 1000 + r,
-                         base_seed=1, device=dev)
+    def panel(r):
+        return make_halo_panel(N, "1980-01-01", 3 * dpr, 3, r, H, seed_of=lambda q: 1000 + q,
+                               base_seed=1, device=dev)
+
+    def bits(p, r):   # a rank's need bits (untimed), for the union the timed rank computes
+        c, n, f = eng.shard_halo(p.P, p.month_start, p.H, p.F, J, skip, before=r > 0,
+                                 after=r < 2)
+        msr = p.shard_month_start
+        _, _, _, _, s = eng.signal_shard_halo(p.P, msr, int(np.diff(p.month_start_host).max()),
+                                              J, skip, c, n)
+        return eng.shard_need(f, s, H)   # (the next rank's halo length)
+
+    other = {}
+    for r in (0, 2):
+        p = panel(r)
+        other[r] = bits(p, r)
+        del p
+    hp = panel(1)
     P, ms, T_m = hp.P, hp.month_start, hp.T_m
     msh = hp.shard_month_start
     mh = hp.month_start_host
@@ -49,12 +69,13 @@ def main():
     def halo(ev=None):
         rec = (lambda i: ev[i].record()) if ev else (lambda i: None)
         rec(0)
-        carry_h, npm_h, flags = eng.shard_halo(P, ms, hp.H, hp.F, J, skip)
+        carry_h, npm_h, flags = eng.shard_halo(P, ms, hp.H, hp.F, J, skip, before=True,
+                                               after=True)
         rec(1)
         PM, _, M, NR, st = eng.signal_shard_halo(P, msh, maxd, J, skip, carry_h, npm_h, ids=IDS)
         rec(2)
-        mask = eng.shard_need(flags, st, hp.H)
-        masks = torch.stack([mask] * G)
+        mask = eng.shard_need(flags, st, H)
+        masks = torch.stack([other[0], mask, other[2]])   # the 3 ranks' bits (the union's input)
         idx, cnt = eng.shard_union(masks, N, cap)
         rec(3)
         rcd = eng.shard_summary_cols(PM, st, idx, cnt, J, skip)
@@ -104,8 +125,26 @@ def main():
         for i, n in enumerate(names):
             st_ms[n].append(ev[i].elapsed_time(ev[i + 1]))
     S = 6 + J + skip + 1
+    diag = None
+    if len(sys.argv) > 6 and sys.argv[6] == "diag":   # who is listed, and why
+        carry_h, npm_h, flags = eng.shard_halo(P, ms, hp.H, hp.F, J, skip)
+        _, _, _, _, st = eng.signal_shard_halo(P, msh, maxd, J, skip, carry_h, npm_h)
+        mask = eng.shard_need(flags, st, H)
+        idx, cnt = eng.shard_union(torch.stack([other[0], mask, other[2]]), N, cap)
+        n = min(int(cnt.item()), cap)
+        ii = idx[:n].long()
+        f = flags[ii].cpu().numpy()
+        t = st.t[:, ii].cpu().numpy()
+        bit = lambda m, r: ((m[r][ii // 64] >> (ii % 64)) & 1).cpu().numpy()
+        b0 = bit(other[0], 3)
+        b2 = bit(other[2], 2)
+        from collections import Counter
+        diag = Counter(f"flag{int(a)}_n{'>0' if c > 0 else '0'}_pend{int(d >= 0)}_head0{int(h)}"
+                       f"_later{int(l)}" for a, c, d, h, l in zip(f, t[0], t[1], b0, b2))
+        diag = dict(diag.most_common(12))
     print(json.dumps({
-        "N": N, "days_per_rank": dpr, "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
+        "diag": diag,
+        "N": N, "days_per_rank": dpr, "split_cells": cells or 16384, "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
         "F": hp.F, "G_emulated": G, "cap": cap, "listed_this_rank": int(cnt.item()),
         "collective_bytes_per_rank": {"need_bits": 4 * 8 * ((N + 63) // 64),
                                       "records": 8 * S * cap,

@@ -78,9 +78,10 @@ class OracleStages:
                 flags[a] |= 1
         npm = O.absent_like(N)
         if F > 0:
-            d0, d1 = ms_[H + T_m], ms_[H + T_m + 1]
-            pmf, _ = O.month_end(P_[d0:d1], np.array([0, d1 - d0]))
-            npm = pmf[0]
+            d0, d1 = ms_[H + T_m], ms_[H + T_m + F]
+            pmf, _ = O.month_end(P_[d0:d1], ms_[H + T_m:H + T_m + F + 1] - d0)
+            for f in range(F - 1, -1, -1):   # the first forward month with a row
+                npm = np.where(O.is_absent(pmf[f]), npm, pmf[f])
         if after:
             flags[O.is_absent(npm)] |= 2
         return carry, torch.from_numpy(npm), torch.from_numpy(flags)
@@ -231,7 +232,7 @@ def _worker_halo(rank, world, port, J, skip, H, cap, q):
         P = torch.from_numpy(np.ascontiguousarray(z["P"][d0:d1]))
         msl = torch.from_numpy(ms[h0:m1 + F + 1] - d0)
         pipe = DateShardPipeline(OracleStages(), [b - a for a, b in parts], J, skip, 10,
-                                 fused=False)
+                                 fused=False, halo=H)
         if cap is not None:
             pipe.fallback_cap = lambda N: cap
         r = pipe.run_halo(P, msl, hm, F, int(np.diff(ms).max()))

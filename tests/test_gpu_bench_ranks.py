@@ -125,6 +125,8 @@ def test_bench_c4_self_launch_strong_scaling(engine, tmp_path):
                          "--seed", str(SEED), "--dump", str(dump)])
     assert line["n_gpus"] == 2 and line["decile_match_pct"] == 100.0
     assert line["scaling"] == "strong" and line["config"]["bdays"] == DAYS
+    assert line["engine_path"].startswith("halo date shards")     # the default sharded pass
+    assert 0 <= line["halo"]["listed_assets"] <= line["halo"]["list_width"]
     assert line["config"]["parallelism"] == "date-shard x2"
     assert abs(line["value"] - N * DAYS * line["steps"] / (line["ms_per_step"] * 1e-3 * line["steps"])) \
         <= 1e-6 * line["value"]
@@ -136,12 +138,14 @@ def test_bench_c4_self_launch_strong_scaling(engine, tmp_path):
 
 
 def test_bench_c4_two_ranks_gloo(engine, tmp_path):
-    """torchrun's environment, weak scaling: every rank a DAYS-long month range."""
+    """torchrun's environment, weak scaling: every rank a DAYS-long month range; the
+    speculative all-gather pass (--shard-mode fused)."""
     N, DAYS, SEED = 40_000, 1_100, 4
     dump = tmp_path / "c4.npz"
     line = _spawn_bench(["--gpus", "2", "--backend", "gloo", "--assets", str(N), "--days",
                          str(DAYS), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
-                         "--seed", str(SEED), "--dump", str(dump), "--scaling", "weak"])
+                         "--seed", str(SEED), "--dump", str(dump), "--scaling", "weak",
+                         "--shard-mode", "fused"])
     assert line["n_gpus"] == 2 and line["decile_match_pct"] == 100.0
     assert "all 2 ranks" in line["decile_check"]
     assert line["engine_path"].startswith("speculative fused")
