@@ -418,10 +418,16 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort(
 __device__ __forceinline__ uint32_t byte_eq0(uint32_t z) {   // 0x80 in each byte of z that is 0
   return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
 }
+// LM (nullable): the row's leg bitplanes [rows][2][nwm] uint64, nwm = 4 ceil(N / 256) -- plane 0
+// the top decile (NB - 1), plane 1 decile 0 -- for the steady equal-weight turnover rows
+// (k_turnover_ew_mask): the ballots themselves, word 4 g + e holding cell 4 (64 g + l) + e at
+// bit l (a fixed order of each 256-cell group, the same in every row; the counts it serves do
+// not depend on the order).
 template <int NB>
 __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
     const int8_t* __restrict__ L, int64_t N, int C, int64_t rows, uint16_t* __restrict__ PERM,
-    int32_t* __restrict__ OFF, double* __restrict__ FWp, PanAddr pa) {
+    int32_t* __restrict__ OFF, double* __restrict__ FWp, PanAddr pa,
+    uint64_t* __restrict__ LM = nullptr, int64_t nwm = 0) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * PF_WAVES + (threadIdx.x >> 6);
   if (row >= rows) return;   // no barriers below
@@ -441,6 +447,10 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
     const int wi = k * 64 + lane;
     vr[k] = wi < nw ? L4[wi] : 0xFFFFFFFFu;
   }
+  // (held in registers for the second pass: without this the compiler re-issues the label
+  // loads there -- a second read of the row -- to save registers)
+#pragma unroll
+  for (int k = 0; k < LS_RW; ++k) asm volatile("" : "+v"(vr[k]));
   int nb0 = 0, nt0 = 0;   // per-lane counts: bottom (decile 0), top (decile NB - 1)
 #pragma unroll
   for (int k = 0; k < LS_RW; ++k) {
@@ -458,6 +468,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
     FWp[(row * C + c) * 2 + leg] = c == 0 ? (double)(leg == 0 ? nt0 : nb0) : 0.0;
   }
   int pb = 0, pt = rb;   // next position of each leg's segment
+  // plane words 4 k + e (the ballots of byte e of group k) collect in lane 4 (k % 16) + e and
+  // leave as one 512-byte store per plane every 16 groups
+  uint64_t pw_t = 0, pw_b = 0;
 #pragma unroll
   for (int k = 0; k < LS_RW; ++k) {
     if (k * 64 >= nw) break;
@@ -473,6 +486,15 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
       bt += __popcll(mt & lt);
       totb += __popcll(mb);
       tott += __popcll(mt);
+      pw_t = lane == 4 * (k & 15) + e ? mt : pw_t;
+      pw_b = lane == 4 * (k & 15) + e ? mb : pw_b;
+    }
+    if (LM && ((k & 15) == 15 || (k + 1) * 64 >= nw)) {   // (wave-uniform)
+      const int64_t w = 4 * (k & ~15) + lane;
+      if (w < nwm && lane < 4 * ((k & 15) + 1)) {
+        LM[(row * 2) * nwm + w] = pw_t;
+        LM[(row * 2 + 1) * nwm + w] = pw_b;
+      }
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {   // lane-major then byte order = ascending asset id
@@ -1288,6 +1310,95 @@ __device__ __forceinline__ void turnover_body(
   }
 }
 
+// Steady equal-weight rows from the leg bitplanes k_label_sort_legs_ew wrote: ONE WAVE per
+// (chunk, row), 64 cells per plane word (chunks of whole 256-cell groups: Ct == 1 or CH % 256
+// == 0).  A full leg's turnover is three exact member counts
+// (k_turnover's count path: members at t, at t - K_q, at both), here popcounts of plane words
+// -- 10 words per 64 cells instead of 5 label bytes per cell -- and the same final arithmetic on
+// the same integers, so the TURN / COST partials are k_turnover's bits.  Rows that are not all
+// full go onto the general launch's work list as k_turnover's steady launch puts them.
+#define TM_WAVES 4
+__global__ __launch_bounds__(64 * TM_WAVES) void k_turnover_ew_mask(
+    const uint64_t* __restrict__ LM, int64_t nwm, int T_m, int B, int64_t N, KSet ks, int64_t CH,
+    int Ct, double half_spread, double* __restrict__ TURNp, double* __restrict__ COSTp,
+    int32_t* __restrict__ gen_list, int32_t* __restrict__ gen_count,
+    const double* __restrict__ TPv, const uint32_t* __restrict__ TPm) {
+  const int lane = threadIdx.x & 63;
+  const int rows = T_m * B;
+  const int bid = (int)(blockIdx.x * TM_WAVES + (threadIdx.x >> 6));
+  if (bid >= rows * Ct) return;   // no barriers below
+  const int c = bid % Ct, tb = bid / Ct;
+  const int t = tb / B, b = tb - t * B;
+  const int nq = ks.n;
+  const uint32_t m = TPm[tb];
+  if (m & TP_EMPTY) return;   // k_turn_prep wrote its partials
+  const uint32_t need = (1u << (2 * nq)) - 1u;
+  if ((m & need) != need) {   // the general launch's row
+    if (gen_list && lane == 0) {
+      const int slot = atomicAdd(gen_count, 1);
+      if (slot < rows * Ct) gen_list[slot] = bid;
+    }
+    return;
+  }
+  // chunk c's cells [c CH, min(N, (c + 1) CH)): whole 256-cell groups, 4 words each (cells past
+  // N hold no member)
+  const int64_t w0 = (int64_t)c * CH / 64;
+  const int64_t a1 = (int64_t)(c + 1) * CH < N ? (int64_t)(c + 1) * CH : N;
+  const int64_t w1 = (a1 + 255) / 256 * 4;
+  const uint64_t* r1 = LM + (int64_t)tb * 2 * nwm;
+  uint32_t n1[2] = {0, 0}, n0[TO_MAXQ][2], nb[TO_MAXQ][2];
+#pragma unroll
+  for (int q = 0; q < TO_MAXQ; ++q) n0[q][0] = n0[q][1] = nb[q][0] = nb[q][1] = 0;
+  for (int64_t w = w0 + lane; w < w1; w += 64) {
+    uint64_t x1[2], x0[TO_MAXQ][2];
+#pragma unroll
+    for (int li = 0; li < 2; ++li) x1[li] = r1[li * nwm + w];
+#pragma unroll
+    for (int q = 0; q < TO_MAXQ; ++q) {
+      const uint64_t* r0 = LM + ((int64_t)(t - (q < nq ? ks.K[q] : 0)) * B + b) * 2 * nwm;
+#pragma unroll
+      for (int li = 0; li < 2; ++li) x0[q][li] = q < nq ? r0[li * nwm + w] : 0ull;
+    }
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      n1[li] += __popcll(x1[li]);
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q) {
+        n0[q][li] += __popcll(x0[q][li]);
+        nb[q][li] += __popcll(x1[li] & x0[q][li]);
+      }
+    }
+  }
+  auto wsum = [](uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+#pragma unroll
+  for (int li = 0; li < 2; ++li) {
+    n1[li] = wsum(n1[li]);
+#pragma unroll
+    for (int q = 0; q < TO_MAXQ; ++q) { n0[q][li] = wsum(n0[q][li]); nb[q][li] = wsum(nb[q][li]); }
+  }
+  if (lane < nq) {
+    const int q = lane;
+    const double* tp = TPv + (int64_t)tb * TP_STRIDE;
+    double x = 0.0;   // (k_turnover: the waves' f64 charge sums, +0.0 on an all-full row)
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      uint32_t c0 = 0, cb = 0;
+#pragma unroll
+      for (int qq = 0; qq < TO_MAXQ; ++qq)
+        if (qq == q) { c0 = n0[qq][li]; cb = nb[qq][li]; }
+      const double i1 = tp[li * (TO_MAXQ + 1)];
+      const double i0 = tp[li * (TO_MAXQ + 1) + 1 + q];
+      const double skq = tp[2 * (TO_MAXQ + 1) + 2 * q + li];
+      x += ((double)(n1[li] - cb) * i1 + (double)(c0 - cb) * i0 + (double)cb * fabs(i1 - i0)) * skq;
+    }
+    TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.5 * x;
+    COSTp[((int64_t)q * rows + tb) * Ct + c] = x * half_spread;
+  }
+}
+
 // Steady value-weight rows of the G = B / Bg panels that share one weight row (the grouped
 // layout: G look-backs of one panel, TO_MAXG at most): one workgroup per (month t, weight panel
 // p, chunk c) serves the G rows (t, g * Bg + p).  A cell's weights of months t and t - K_q and
@@ -1716,6 +1827,8 @@ static int g_tune_gen_reset = 1;
 // 1: grouped batches' steady value-weight rows by k_turnover_vwg (a weight panel's groups in one
 // workgroup) | 0 by the per-row launch (A/B; the same bits)
 static int g_tune_turn_vwg = 1;
+// steady equal-weight legs turnover from the leg bitplanes (k_turnover_ew_mask) | 0 from labels
+static int g_tune_turn_mask = 1;
 static int32_t* g_gen_probe = nullptr;
 
 __global__ void k_copy_i32(const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
@@ -1786,7 +1899,7 @@ template <int NB>
 static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
                           const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
                           double* SWp, double* FWp, char* segws, int64_t perm_b, int64_t off_b,
-                          int64_t wsrt_b, bool legs, const PanAddr& pa) {
+                          int64_t wsrt_b, bool legs, const PanAddr& pa, int64_t lm_b = 0) {
   const dim3 g((unsigned)(pl.C * T_m * B), 1u, pl.kpar ? (unsigned)K : 1u);
   if (g_tune_cohort_seg && segws && !pl.kpar && K * (NB + 1) <= SEG_MAXKD) {
     uint16_t* PERM = (uint16_t*)(segws + perm_b);
@@ -1811,7 +1924,8 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
       } else {
         if ((N & 3) == 0)   // one wave per row (C5's equal-weight legs)
           hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
-                             dim3(PF_THREADS), 0, st, L, N, pl.C, (int64_t)T_m * B, PERM, OFF, FWp, pa);
+                             dim3(PF_THREADS), 0, st, L, N, pl.C, (int64_t)T_m * B, PERM, OFF, FWp, pa,
+                             g_tune_turn_mask ? (uint64_t*)(segws + lm_b) : nullptr, (N + 255) / 256 * 4);
         else
           hipLaunchKernelGGL((k_label_sort<NB, false, true>), g1, dim3(PF_THREADS), (size_t)N, st, L, W, N,
                              pl.C, PERM, OFF, WSRT, FWp, pa);
@@ -1860,7 +1974,7 @@ template <int NB>
 static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int8_t* const* L,
                              const double* NR, int T_m, int B, int64_t N, int K, char* const* ws,
                              int64_t swr_b, int64_t sw_b, int64_t fw_b, int64_t perm_b,
-                             int64_t off_b, bool legs, bool grouped = false) {
+                             int64_t off_b, bool legs, bool grouped, int64_t lm_b) {
   const int xcd = B >= 8;
   const dim3 g2(xcd ? (unsigned)(8 * ((B + 7) / 8) * T_m) : (unsigned)(T_m * B));
   const PanAddr pa = pan_plain(B, N);
@@ -1872,7 +1986,8 @@ static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int
     const int64_t rows = (int64_t)T_m * nrow_b;
     if (legs && (N & 3) == 0)
       hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((rows + PF_WAVES - 1) / PF_WAVES)),
-                         dim3(PF_THREADS), 0, st, Lq, N, 1, rows, PERM, OFF, FWp, pl_a);
+                         dim3(PF_THREADS), 0, st, Lq, N, 1, rows, PERM, OFF, FWp, pl_a,
+                         g_tune_turn_mask ? (uint64_t*)(w + lm_b) : nullptr, (N + 255) / 256 * 4);
     else if (legs)
       hipLaunchKernelGGL((k_label_sort<NB, false, true>), dim3((unsigned)rows), dim3(PF_THREADS), (size_t)N,
                          st, Lq, (const double*)nullptr, N, 1, PERM, OFF, (double*)nullptr, FWp, pl_a);
@@ -1912,6 +2027,7 @@ struct PfLayout {
   int64_t tp_b, tpm_b;               // byte offsets: k_turn_prep's per-row factors and masks
   bool seg;                          // label-sort buffers present (N <= SEG_MAXN)
   int64_t perm_b, off_b, wsrt_b;     // byte offsets: uint16 [rows][N], int32 [rows][nb+1], f64 [rows][N]
+  int64_t lm_b, nwm;                 // leg bitplanes uint64 [rows][2][nwm] (k_label_sort_legs_ew)
 };
 static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax) {
   PfLayout l;
@@ -1932,13 +2048,15 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
   l.tpm_b = l.tp_b + l.rows * TP_STRIDE * 8;               // then u32 [rows] full-leg masks
   l.bytes = l.tpm_b + l.rows * 4 + 256;
   l.seg = N <= SEG_MAXN;
-  l.perm_b = l.off_b = l.wsrt_b = 0;
+  l.perm_b = l.off_b = l.wsrt_b = l.lm_b = 0;
+  l.nwm = (N + 255) / 256 * 4;
   if (l.seg) {
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     l.perm_b = al(l.bytes);
     l.off_b = al(l.perm_b + l.rows * seg_stride(N) * 2);
     l.wsrt_b = al(l.off_b + l.rows * (n_bins + 1) * 4);
-    l.bytes = al(l.wsrt_b + l.rows * seg_stride(N) * 8);
+    l.lm_b = al(l.wsrt_b + l.rows * seg_stride(N) * 8);
+    l.bytes = al(l.lm_b + l.rows * 2 * l.nwm * 8);
   }
   return l;
 }
@@ -1974,6 +2092,10 @@ int csm_tune_portfolio(const char* key, int value) {
     g_tune_turn_vwg = value;
     return CSM_OK;
   }
+  if (key && !strcmp(key, "turn_mask") && (value == 0 || value == 1)) {
+    g_tune_turn_mask = value;
+    return CSM_OK;
+  }
   return CSM_E_INVAL;
 }
 
@@ -2004,7 +2126,7 @@ static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const do
   double* ws = (double*)workspace;
   hipStream_t st = ctx->stream;
   switch (n_bins) {
-#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b, legs, pa); break;
+#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b, legs, pa, lay.lm_b); break;
     PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20) PF_CASE(30)
 #undef PF_CASE
     default:
@@ -2059,7 +2181,7 @@ int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const d
   char* ws[SEG_MAXJ];
   for (int q = 0; q < nJ; ++q) ws[q] = (char*)workspaces[q];
   switch (n_bins) {
-#define PJ_CASE(NBV) case NBV: launch_cohort_js<NBV>(st, lay.p, nJ, L, NR, T_m, B, N, Kmax, ws, lay.swr * 8, lay.sw * 8, lay.fw * 8, lay.perm_b, lay.off_b, legs != 0); break;
+#define PJ_CASE(NBV) case NBV: launch_cohort_js<NBV>(st, lay.p, nJ, L, NR, T_m, B, N, Kmax, ws, lay.swr * 8, lay.sw * 8, lay.fw * 8, lay.perm_b, lay.off_b, legs != 0, false, lay.lm_b); break;
     PJ_CASE(2) PJ_CASE(3) PJ_CASE(4) PJ_CASE(5) PJ_CASE(10) PJ_CASE(20) PJ_CASE(30)
 #undef PJ_CASE
   }
@@ -2092,7 +2214,7 @@ int csm_cohort_sums_js_grouped(csm_ctx* ctx, int32_t nJ, const int8_t* L, const 
   hipStream_t st = ctx->stream;
   char* ws = (char*)workspace;
   switch (n_bins) {
-#define PJ_CASE(NBV) case NBV: launch_cohort_js<NBV>(st, lay.p, nJ, &L, NR, T_m, B, N, Kmax, &ws, lay.swr * 8, lay.sw * 8, lay.fw * 8, lay.perm_b, lay.off_b, legs != 0, true); break;
+#define PJ_CASE(NBV) case NBV: launch_cohort_js<NBV>(st, lay.p, nJ, &L, NR, T_m, B, N, Kmax, &ws, lay.swr * 8, lay.sw * 8, lay.fw * 8, lay.perm_b, lay.off_b, legs != 0, true, lay.lm_b); break;
     PJ_CASE(2) PJ_CASE(3) PJ_CASE(4) PJ_CASE(5) PJ_CASE(10) PJ_CASE(20) PJ_CASE(30)
 #undef PJ_CASE
   }
@@ -2113,6 +2235,15 @@ int csm_cohort_sums_legs(csm_ctx* ctx, const int8_t* L, const double* NR, const 
     return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums_legs: rows of <= %d assets (N=%lld)", SEG_MAXN,
                    (long long)N);
   return cohort_sums(ctx, L, NR, W, T_m, B, N, n_bins, Kmax, workspace, true, pan_plain(B, N));
+}
+
+// Whether the cohort pass of this layout ran k_label_sort_legs_ew (legs, equal weights, N % 4 ==
+// 0, the segment path -- launch_cohort's and launch_cohort_js's choice), so the workspace holds
+// the leg bitplanes.  (Tune knobs are set before a workspace is sized, csmom.h.)
+static bool legs_masks(const PfLayout& lay, bool legs, int64_t N, int Kmax, int n_bins) {
+  return g_tune_turn_mask && legs && (N & 3) == 0 && lay.seg && g_tune_cohort_seg &&
+         !lay.p.kpar && (int64_t)Kmax * (n_bins + 1) <= SEG_MAXKD &&
+         (lay.p.Ct == 1 || lay.p.CHt % 256 == 0);
 }
 
 static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W,
@@ -2182,6 +2313,16 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
                              st, L, W, T_m, B, N, ks, n_bins, lay.p.CHt, lay.p.Ct, half_spread,
                              k_impact, aum, ADV, SIG, ws + lay.turn, ws + lay.cost, gen_list,
                              gen_count, (const double*)TPv, (const uint32_t*)TPm, pa);
+          continue;
+        }
+        // equal-weight legs after the legs label sort: the steady rows' member counts from the
+        // leg bitplanes it wrote (k_turnover_ew_mask), not from label bytes
+        if (!gen && !W && !imp && legs_masks(lay, legs, N, Kmax, n_bins)) {
+          hipLaunchKernelGGL(k_turnover_ew_mask, dim3((unsigned)((nblk + TM_WAVES - 1) / TM_WAVES)),
+                             dim3(64 * TM_WAVES), 0, st,
+                             (const uint64_t*)((char*)workspace + lay.lm_b), lay.nwm, T_m, B, N, ks,
+                             lay.p.CHt, lay.p.Ct, half_spread, ws + lay.turn, ws + lay.cost,
+                             gen_list, gen_count, (const double*)TPv, (const uint32_t*)TPm);
           continue;
         }
         hipLaunchKernelGGL(kern, dim3(gen ? gen_grid : (unsigned)nblk), dim3(PF_THREADS), 0, st,

@@ -44,8 +44,9 @@ int csm_abi_version(void);
  * drive the fallbacks on inputs that would not reach them): "signal_vec" (2 paired 16-B rows |
  * 1 one asset per lane, the odd-N path), "signal_bwf" (0 auto | 1 one-wave blocks | 4 the wide
  * panels' four barrier-free waves with buffer loads), "dec_merge" (1 the merged decile sweep on
- * ids, the general kernel for the rows it leaves | 0 the general kernel only), "dec_split" (1
- * wide rows on ids: the split pass -- plan, chunked sweep, finish | 0 the merged pass with one
+ * ids, the general kernel for the rows it leaves | 0 the general kernel only), "dec_split" (2
+ * auto: wide rows on ids take the split pass -- plan, chunked sweep, finish -- in launches of
+ * fewer rows than half the CUs (short date shards) | 1 always | 0 the merged pass with one
  * workgroup per row; same labels and counts, means in another fixed order), "mj_reg"
  * (csm_momentum_multi: 2 register ring, two assets per lane | 1 one asset | 0 the LDS ring),
  * "dec_narrow_max" (widest row for the narrow-row decile kernels), "cohort_seg" / "cohort_lds"
@@ -57,8 +58,11 @@ int csm_abi_version(void);
  * plans | 0 one per (K, month, panel, decile)), "gen_reset" (1 the turnover work-list counter
  * reset by a kernel | 0 by hipMemsetAsync, round 3's form, kept for the graph-replay diagnosis
  * of tests/test_gpu_capture.py), "turn_vwg" (1 a grouped batch's steady value-weight turnover
- * rows by one workgroup per weight panel | 0 one per row).  Returns CSM_E_INVAL for an unknown
- * key or value. */
+ * rows by one workgroup per weight panel | 0 one per row), "turn_mask" (1 steady equal-weight
+ * legs turnover rows counted from the legs label sort's leg bitplanes | 0 from the label
+ * bytes), "dec_split_cells" (cells per chunk of the split decile sweep, default 16384, a
+ * multiple of 1024; the split workspace is the context's).
+ * Returns CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aids: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
  * wall-clock ticks (100 MHz) at its phase boundaries; "gen_probe" = device int32 that receives

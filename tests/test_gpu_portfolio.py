@@ -495,3 +495,38 @@ def test_grouped_equals_side_by_side(engine, G, Bg, vw, legs, mode, ncols):
         for f in ("PR", "LS", "TURN", "COST", "NET"):
             a, b = getattr(grp[K], f).cpu().numpy(), getattr(plain[K], f).cpu().numpy()
             assert a.shape == b.shape and bits_equal(a, b), (K, f)
+
+
+@pytest.mark.parametrize("B,Ks,ncols", [(1, (3, 6, 9, 12), 500), (16, (3, 6, 9, 12), 500),
+                                        (8, (12, 3), 1000), (5, (1, 7, 7), 372)])
+def test_turnover_mask_bit_identical(engine, B, Ks, ncols):
+    """Steady equal-weight legs turnover from the leg bitplanes of the legs label sort
+    (k_turnover_ew_mask, popcounts of 64-cell words) against the label-byte path (turn_mask 0):
+    LS / TURN / COST / NET bit for bit -- plain batches and the grouped shared-return path of the
+    bootstrap sweep; row widths that end inside a plane word."""
+    z = load_golden("c1")
+    PM, _ = engine.month_end(_up(np.ascontiguousarray(z["P"][:, :ncols])),
+                             _up(z["month_start"].astype(np.int64)))
+    T_m, N = PM.shape
+    _, M, NR = engine.momentum(PM, 12, 1)
+    L, _, _, _ = engine.deciles(M, None, 10)
+    rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 7 * i, axis=1) for i in range(B)],
+                                 axis=1).reshape(T_m, B * N))
+    L, NR = rep(L), rep(NR)
+    lib = engine.lib
+    got = {}
+    try:
+        for mode in (1, 0):
+            assert lib.csm_tune(b"turn_mask", mode) == 0
+            plain = engine.portfolio_multi(L, NR, 10, Ks=Ks, B=B, legs_only=True)
+            grp = engine.portfolio_multi_js_grouped(torch.stack([L, L]), NR, 10, Ks=Ks, B=B,
+                                                    legs_only=True)
+            got[mode] = (plain, grp)
+    finally:
+        lib.csm_tune(b"turn_mask", 1)
+    for i in range(2):
+        for K in set(Ks):
+            for f in ("LS", "TURN", "COST", "NET"):
+                a = getattr(got[1][i][K], f).cpu().numpy()
+                b = getattr(got[0][i][K], f).cpu().numpy()
+                assert bits_equal(a, b), (i, K, f)
