@@ -4,9 +4,19 @@
 // translation unit so the kernel builds in parallel with csmom.hip.
 #include "csm_common.h"
 
-#define DEC_THREADS 512
-#define HB 8192
-#define CAP 4096
+// (overridable for same-box A/B builds: -DDEC_PRE_THREADS=256 -DDEC_PRE_HB=4096 ...)
+#ifndef DEC_PRE_THREADS
+#define DEC_PRE_THREADS 512
+#endif
+#ifndef DEC_PRE_HB
+#define DEC_PRE_HB 8192
+#endif
+#ifndef DEC_PRE_CAP
+#define DEC_PRE_CAP 4096
+#endif
+#define DEC_THREADS DEC_PRE_THREADS
+#define HB DEC_PRE_HB
+#define CAP DEC_PRE_CAP
 #define DEC_LU 8
 namespace dec_pre {
 #include "deciles.inc"

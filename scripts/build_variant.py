@@ -2,7 +2,9 @@
 path, with __graft_entry__'s flags, for same-box A/B runs through CSMOM_LIB:
     git worktree add /tmp/base <commit>
     python scripts/build_variant.py /tmp/base ab/libcsmom_base.so
-    CSMOM_LIB=ab/libcsmom_base.so python bench.py ..."""
+    CSMOM_LIB=ab/libcsmom_base.so python bench.py ...
+EXTRA_FLAGS="-DNAME=value ..." adds compile definitions (a variant of the same tree)."""
+import os
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -18,7 +20,7 @@ csrc = src_root / G.CSRC.relative_to(G.ROOT)
 srcs = [csrc / p.name for p in G.SRCS]
 objdir = out.parent / (out.stem + "_obj")
 objdir.mkdir(parents=True, exist_ok=True)
-cflags = [f for f in G.FLAGS if f != "-shared"]
+cflags = [f for f in G.FLAGS if f != "-shared"] + os.environ.get("EXTRA_FLAGS", "").split()
 
 
 def cc(src):
