@@ -84,6 +84,9 @@ def parse(argv=None):
                          "instead of the decile pass's last workgroup (csm_deciles_ids_ls)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="C2 / C3: month chunks of the time-chunked scan (0 = Engine.default_chunks)")
+    ap.add_argument("--c2-unfused", action="store_true",
+                    help="C2 A/B: k_month_end + the three-launch chunked scan (summary, fold, scan) "
+                         "instead of the one-launch month-end + chunked scan (csm_signal_chunked)")
     ap.add_argument("--match-dates", type=int, default=0,
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -368,6 +371,13 @@ def main(argv=None):
     narrow_ids = (not fused and pipe is None and not args.no_ids and chunks > 1 and N % 4 == 0
                   and N <= 16384)
     IDS = eng.empty((T_m, N), torch.int16) if (use_ids or narrow_ids) else None
+    # C2: month-end and the chunked scan in one launch (k_signal_tc; its workspace is zeroed
+    # once here and leaves its sync words zero after every launch)
+    tc = narrow_ids and not args.c2_unfused and max_days <= 23 and N % 2 == 0
+    tc_ws = None
+    if tc:
+        nbytes = int(eng.lib.csm_signal_chunked_workspace(T_m, N, J, skip, min(chunks, 64)))
+        tc_ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
     ws = None
     if chunks > 1:
         nbytes = int(eng.lib.csm_momentum_chunked_workspace(T_m, N, J, skip, chunks))
@@ -379,6 +389,9 @@ def main(argv=None):
     stage_names = (["signal(k_signal+ids)", "deciles+long_short(k_deciles<ids>)"] if use_ids and fused_ls else
                    ["signal(k_signal+ids)", "deciles(k_deciles<ids>)", "long_short"] if use_ids else
                    ["signal(k_signal)", "deciles(k_deciles)", "long_short"] if fused else
+                   ["signal(k_signal_tc+ids)", "deciles+long_short(k_deciles<ids>)"]
+                   if tc and fused_ls else
+                   ["signal(k_signal_tc+ids)", "deciles(k_deciles<ids>)", "long_short"] if tc else
                    ["month_end(k_month_end)", scan_name,
                     "deciles+long_short(k_deciles<ids>)"] if narrow_ids and fused_ls else
                    ["month_end(k_month_end)", scan_name, "deciles(k_deciles<ids>)", "long_short"]
@@ -404,6 +417,9 @@ def main(argv=None):
                            out=(None, None, M, NR, IDS), min_month_days=min_days)
         elif fused:
             eng.signal(panel.P, panel.month_start, max_days, J, skip, out=(None, None, M, NR))
+        elif tc:
+            eng.signal_chunked(panel.P, panel.month_start, max_days, J, skip, chunks=chunks,
+                               out=(None, M, NR, IDS), workspace=tc_ws)
         else:
             eng.month_end(panel.P, panel.month_start, PM=PM)
             i += 1
@@ -526,8 +542,8 @@ def main(argv=None):
         roofline = None
         if world == 1:
             me_ms = stage_ms[0] / args.steps
-            if fused:
-                kname = "k_signal"
+            if fused or tc:
+                kname = "k_signal_tc" if tc else "k_signal"
                 alg_me = 8.0 * N * T_d + 16.0 * N * T_m       # read P once, write mom + next_ret
             else:
                 kname = "k_month_end"
@@ -578,6 +594,9 @@ def main(argv=None):
                             "fused k_signal (+ bucket ids) -> k_deciles on ids (+ long-short, one "
                             "launch tail)" if use_ids else
                             "fused k_signal" if fused else
+                            f"k_signal_tc (month-end + {min(chunks, 64)}-chunk scan + bucket ids, one "
+                            f"launch) -> narrow k_deciles on ids (+ long-short in the same launch)"
+                            if tc else
                             f"k_month_end + scan ({chunks} month chunks, + bucket ids) -> narrow "
                             f"k_deciles on ids (+ long-short in the same launch)" if narrow_ids else
                             f"k_month_end + scan ({chunks} month chunks)"),

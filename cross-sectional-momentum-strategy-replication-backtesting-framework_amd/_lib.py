@@ -93,6 +93,9 @@ SIGNATURES = {
                                      _p, _i32, _i32, _p, _p, _p, _p, _p]),
     "csm_momentum_chunked": (ctypes.c_int, [_p, _p, _i32, _i64, _i32, _i32, _i32, _p, _p, _p,
                                             _p, _p]),
+    "csm_signal_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),
+    "csm_signal_chunked": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32,
+                                          _p, _p, _p, _p, _p]),
     "csm_momentum_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),
     "csm_momentum_multi_chunked_workspace": (ctypes.c_int64, [_i32, _i64, _i32, _i32, _i32]),
     "csm_momentum_multi_chunked": (ctypes.c_int, [_p, _p, _i32, _i64, _p, _i32, _i32, _i32, _p,

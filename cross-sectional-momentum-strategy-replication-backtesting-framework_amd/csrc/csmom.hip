@@ -1193,6 +1193,504 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 }
 
 // =====================================================================================
+// Kernel AB-TC: month-end + time-chunked scan in ONE launch, for narrow panels (C2: 5,000
+// assets, where one wave per 128 assets walking all 300 months leaves the chip idle and the
+// unfused path costs four launches: k_month_end, k_shard_summary_chunked, k_fold_carry,
+// k_momentum_chunked).  A workgroup owns (chunk g, 256-asset column x).
+//   1. Its eight waves reduce the chunk's daily rows to month prices in LDS (wave w: asset
+//      half w % 2, months w / 2, w / 2 + 4, ...: four months of each half in flight).
+//   2. Its first four waves (one asset per lane) build the chunk's exchange record from them
+//      (k_shard_summary_chunked's fields + the last present month) and publish it.
+//   3. They wait for the records of chunks 0..g-1 of the column and
+//   4. fold them into the scan state at the chunk's first month: the newest T = W + 1
+//      present month prices (k_fold_carry's window) are replayed into the ring.  WR > 0
+//      (compile-time W): the window is located from the present-row counts, 16 chunks per
+//      load trip, and read from at most three chunks' tails (two trips for a dense asset);
+//      histories it does not settle (a window over four or more chunks, a last present month
+//      with no valid price, a NaN window start with no earlier price in the loaded rows) take
+//      k_fold_carry's general walk, as WR = 0 does for every asset.
+//   5. They scan the chunk's months from LDS (WR > 0: the ring in registers).
+// The pending ranked row at a chunk's end is not finished with a forward price: the chunk with
+// the asset's next present row writes its next_ret (the fold hands it the pending month when
+// the rebuilt ring says that row ranked -- exactly when the chunk that scanned it left it
+// pending, so one writer per cell), as the sequential scan does; the last chunk writes NaN for
+// one still pending.  Same factors, same order, same divisions as k_month_end -> k_momentum:
+// bit-identical R / M / NR / ids.
+// Hand-off (MI355X_MICROARCH.md, visibility, row 1): records stored write-through (agent
+// relaxed atomic stores), every storing wave drains (vmcnt 0), a barrier, ONE lane stores the
+// flag; the consumer polls each flag with relaxed agent loads, ONE agent acquire, a barrier,
+// plain loads.  Workgroups take tickets in arrival order and ticket t is chunk t / nbx, so
+// every record a workgroup waits for belongs to an earlier ticket -- a workgroup already
+// running: no residency assumption.  Spins are bounded (timeout word).  The last workgroup to
+// finish zeroes the flags; the ticket and done counters wrap to 0 themselves, so the sync
+// words are zero again for the next launch (or graph replay).
+// sync [0] ticket, [1] done, [2] timeout, [3] pad, [4 ..) flags [G][nbx].  Records
+// [G][nbx][SR][256] f64: one (chunk, column)'s record is whole cache lines of its own.
+// =====================================================================================
+#define TC_THREADS 512   // eight waves reduce months; the first four fold and scan
+#define TC_MONTH_WAVES (TC_THREADS / 128)   // month slots per asset half
+#define TC_COLS 256      // assets per workgroup
+#define TC_MAXD 23       // day rows per month (a business month)
+#define TC_MAXG 64       // chunks
+#define TC_MAXC 32       // months per chunk
+#define TC_SYNC0 4       // sync words before the flags
+#define TC_SPINS (1u << 21)
+#define TC_NC 16         // chunk counts per load trip of the window search
+// -DTC_TIMING (experiment builds, scripts/build_variant.py): per-workgroup phase stamps
+// (wall clock, 100 MHz) in 8 u64 words per ticket after the records (workspace grows)
+#ifdef TC_TIMING
+#define TC_STAMP(k) do { if (tid == 0) stamp[k] = wall_clock64(); } while (0)
+#else
+#define TC_STAMP(k) do { } while (0)
+#endif
+
+typedef __attribute__((address_space(1))) unsigned int tc_gu32;
+typedef __attribute__((address_space(1))) unsigned long long tc_gu64;
+
+__device__ __forceinline__ void tc_put(double* p, double v) {   // write-through (sc1) store
+  __hip_atomic_store((tc_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// scan_step with the ring in registers, oldest first (the same factors, product order and
+// stores as scan_step's LDS ring)
+template <int WR>
+__device__ __forceinline__ double scan_step_reg(ScanLane& s, double x, int m, double (&fr)[WR],
+                                                int J, int64_t N, int64_t a,
+                                                double* __restrict__ R, double* __restrict__ M,
+                                                double* __restrict__ NR) {
+  const double NaN = qnan();
+  const int64_t o = (int64_t)m * N + a;
+  if (is_absent(x)) {
+    if (R) R[o] = NaN;
+    M[o] = NaN;
+    NR[o] = NaN;
+    return NaN;
+  }
+  const bool xv = !isnan_d(x);
+  const double pnew = xv ? x : s.pff;
+  const double ret = pnew / s.pff - 1.0;
+  s.pff = pnew;
+#pragma unroll
+  for (int k = 0; k + 1 < WR; ++k) fr[k] = fr[k + 1];
+  fr[WR - 1] = 1.0 + ret;
+  double acc = fr[0];
+#pragma unroll
+  for (int k = 1; k < WR; ++k)
+    if (k < J) acc = acc * fr[k];
+  const double mom = acc - 1.0;
+  const bool ranked = !isnan_d(mom);
+  const double ps_new = xv ? x : s.psff;
+  if (s.prev >= 0) NR[(int64_t)s.prev * N + a] = ps_new / s.psff - 1.0;
+  if (ranked) {
+    s.psff = ps_new;
+    s.prev = m;
+  } else {
+    NR[o] = NaN;
+    s.prev = -1;
+  }
+  if (R) R[o] = ret;
+  M[o] = mom;
+  return mom;
+}
+
+// k_fold_carry's general walk for chunk g of one asset (column pointer cp, chunk stride hs):
+// the ring into LDS (ring[k * RS], oldest first), returns pff / psff / the pending month.
+__device__ __forceinline__ void tc_fold_general(const double* cp, int64_t hs, int g, int W,
+                                                int J, double* ring, int RS, ScanLane& sl) {
+  const int T = W + 1, SR = SUM_SCALARS + T + 1;
+  const double NaN = qnan();
+  auto at = [&](int h, int r) -> double { return cp[(int64_t)h * hs + (int64_t)r * TC_COLS]; };
+  for (int k = 0; k < W; ++k) ring[k * RS] = NaN;
+  int64_t s = 0;          // present rows of chunks h..g-1
+  int64_t frel = 0, lrel = 0;
+  bool hasf = false, haslv = false, below = false;
+  double lvlast = NaN, lvbelow = NaN;
+  int lpm = -1, nv = 0, src_h = -1, src_j = -1;
+  for (int hb = g - 1; hb >= 0; hb -= 4) {   // one backward pass, four chunks per trip
+    double n4[4], f4[4], li4[4], lv4[4], lp4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = hb - u >= 0 ? hb - u : 0;
+      n4[u] = at(h, 0); f4[u] = at(h, 1); li4[u] = at(h, 2); lv4[u] = at(h, 3);
+      lp4[u] = at(h, SR - 1);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = hb - u;
+      if (h < 0) break;
+      const int64_t n = (int64_t)n4[u];
+      bool took = false;
+      if (nv < T) {
+        const int k = (int)(n < T ? n : T);
+        const int take = k < T - nv ? k : T - nv;
+        if (take > 0) { nv += take; src_h = h; src_j = T - take; took = true; }
+      }
+      if (took) below = false;
+      else if (src_h >= 0 && !below && li4[u] >= 0.0) { below = true; lvbelow = lv4[u]; }
+      if (lpm < 0 && n > 0) lpm = (int)lp4[u];
+      if (!haslv && li4[u] >= 0.0) { haslv = true; lvlast = lv4[u]; lrel = (int64_t)li4[u] - (s + n); }
+      if (f4[u] >= 0.0) { hasf = true; frel = (int64_t)f4[u] - (s + n); }
+      s += n;
+    }
+  }
+  const int64_t off = s, f = hasf ? off + frel : -1;
+  double pff = NaN;   // the price before the window's oldest row
+  if (nv > 0) {
+    const int k0 = (int)fmin(at(src_h, 0), (double)T);
+    for (int j = src_j - 1; j > T - 1 - k0; --j) {
+      const double xv = at(src_h, SUM_SCALARS + j);
+      if (!isnan_d(xv)) { pff = xv; break; }
+    }
+    if (isnan_d(pff)) pff = at(src_h, 4);
+    if (isnan_d(pff) && below) pff = lvbelow;
+  }
+  int cc = 0;   // replay oldest -> newest; the newest W rets become the ring
+  for (int h = src_h; h >= 0 && h < g; ++h) {
+    const int kh = (int)fmin(at(h, 0), (double)T);
+    for (int jb = (h == src_h) ? src_j : T - kh; jb < T; jb += SUM_U) {
+      double xs[SUM_U];
+#pragma unroll
+      for (int u = 0; u < SUM_U; ++u) xs[u] = jb + u < T ? at(h, SUM_SCALARS + jb + u) : NaN;
+#pragma unroll
+      for (int u = 0; u < SUM_U; ++u) {
+        if (jb + u >= T) break;
+        const double xv = xs[u];
+        const double nx = isnan_d(xv) ? pff : xv;
+        const double ret = nx / pff - 1.0;
+        pff = nx;
+        const int pos = cc - (nv - W);
+        if (pos >= 0) ring[pos * RS] = 1.0 + ret;
+        ++cc;
+      }
+    }
+  }
+  sl.pff = lvlast;
+  const int64_t li = off + lrel;
+  sl.psff = (f >= 0 && haslv && li >= f + W) ? lvlast : NaN;   // (k_fold_carry's psff)
+  // the last present row's mom_J from the rebuilt ring, in scan_step's order: ranked (its
+  // next_ret still pending) exactly when the chunk that scanned it left it pending
+  double acc = ring[0];
+  for (int k = 1; k < J; ++k) acc = acc * ring[k * RS];
+  sl.prev = (lpm >= 0 && !isnan_d(acc - 1.0)) ? lpm : -1;
+}
+
+// The window search of WR > 0 (see the kernel's comment): true when it settled the state (ring
+// factors in fr, sl), false when the general walk must run.  win: this lane's LDS column of T
+// rows (stride RS).
+template <int WR>
+__device__ __forceinline__ bool tc_fold_fast(const double* cp, int64_t hs, int g, int J,
+                                             double* win, int RS, double (&fr)[WR],
+                                             ScanLane& sl) {
+  constexpr int T = WR + 1, SR = SUM_SCALARS + T + 1;
+  const double NaN = qnan();
+  auto at = [&](int h, int r) -> double { return cp[(int64_t)h * hs + (int64_t)r * TC_COLS]; };
+  // trip 1: chunk g - 1's record and the counts of the 16 chunks before it
+  double r1[SR], nc[TC_NC];
+#pragma unroll
+  for (int r = 0; r < SR; ++r) r1[r] = at(g - 1, r);
+#pragma unroll
+  for (int u = 0; u < TC_NC; ++u) nc[u] = g - 2 - u >= 0 ? at(g - 2 - u, 0) : 0.0;
+  const int k1 = (int)fmin(r1[0], (double)T);
+  const double h1 = r1[4], lp1 = r1[SR - 1], n1 = r1[0];
+  int nv = k1;
+  // the older chunks in the window (newest first): index, rows taken, window rows before it
+  int c0 = -1, t0 = 0, b0 = 0, c1 = -1, t1 = 0, b1 = 0;
+  bool over = false;
+  for (int base = g - 2; base >= 0 && nv < T && !over; base -= TC_NC) {
+    if (base != g - 2) {   // later trips (long absences): the next 16 counts
+#pragma unroll
+      for (int u = 0; u < TC_NC; ++u) nc[u] = base - u >= 0 ? at(base - u, 0) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < TC_NC; ++u) {   // (guards, not breaks: nc stays in registers)
+      const int h = base - u;
+      const int k = (int)fmin(nc[u], (double)T);
+      if (h >= 0 && nv < T && !over && k > 0) {
+        const int take = k < T - nv ? k : T - nv;
+        if (c0 < 0) { c0 = h; t0 = take; b0 = nv; }
+        else if (c1 < 0) { c1 = h; t1 = take; b1 = nv; }
+        else over = true;
+        if (!over) nv += take;
+      }
+    }
+  }
+  if (over) return false;
+  if (nv == 0) {   // no present month before the chunk: the empty state
+#pragma unroll
+    for (int k = 0; k < WR; ++k) fr[k] = NaN;
+    sl.pff = NaN; sl.psff = NaN; sl.prev = -1; sl.head = 0;
+    return true;
+  }
+  // the window in LDS: chunk g - 1's newest k1 rows, then the older chunks' (trip 2)
+#pragma unroll
+  for (int j = 0; j < T; ++j)
+    if (j >= T - k1) win[j * RS] = r1[SUM_SCALARS + j];   // (r1 is dead from here)
+  // trip 2: the older window chunks' tails, head, last present month and count
+  double x0[T + 3], x1[T + 3];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    x0[j] = c0 >= 0 ? at(c0, SUM_SCALARS + j) : NaN;
+    x1[j] = c1 >= 0 ? at(c1, SUM_SCALARS + j) : NaN;
+  }
+  x0[T] = c0 >= 0 ? at(c0, 4) : NaN;
+  x1[T] = c1 >= 0 ? at(c1, 4) : NaN;
+  x0[T + 1] = c0 >= 0 ? at(c0, SR - 1) : -1.0;
+  x1[T + 1] = -1.0;
+  x0[T + 2] = c0 >= 0 ? at(c0, 0) : 0.0;
+  x1[T + 2] = c1 >= 0 ? at(c1, 0) : 0.0;
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    if (c0 >= 0 && j >= T - t0) win[(j - b0) * RS] = x0[j];
+    if (c1 >= 0 && j >= T - t1) win[(j - b1) * RS] = x1[j];
+  }
+  const int lpm = k1 > 0 ? (int)lp1 : (int)x0[T + 1];
+  // the last present month must hold a valid price (else the general walk's psff rule)
+  const double last = win[(T - 1) * RS];
+  if (isnan_d(last)) return false;
+  // the price before the window's oldest row: needed when the window is the whole history
+  // (its first factor is kept) or when that row has no valid price.  With nv < T every window
+  // chunk gave all its rows and the count walk saw every earlier chunk empty: NaN.  Else the
+  // oldest window chunk's rows before the window (newest first), then its head; not found:
+  // the general walk (a valid price further back).
+  const double first = win[(T - nv) * RS];
+  double pff = NaN;
+  if (nv == T && isnan_d(first)) {
+    const int kc = (int)fmin(c1 >= 0 ? x1[T + 2] : c0 >= 0 ? x0[T + 2] : n1, (double)T);
+    const int tk = c1 >= 0 ? t1 : c0 >= 0 ? t0 : k1;
+    bool found = false;
+#pragma unroll
+    for (int j = T - 1; j >= 0; --j) {
+      // (a window of chunk g - 1 alone took all its tail: no row before it to search)
+      const double xv = c1 >= 0 ? x1[j] : x0[j];
+      if (!found && j < T - tk && j >= T - kc && !isnan_d(xv)) { pff = xv; found = true; }
+    }
+    if (!found) {
+      const double hd = c1 >= 0 ? x1[T] : c0 >= 0 ? x0[T] : h1;
+      if (!isnan_d(hd)) { pff = hd; found = true; }
+    }
+    if (!found) return false;
+  }
+  // replay the window oldest -> newest into the ring (factor of window row j at slot j - 1)
+#pragma unroll
+  for (int k = 0; k < WR; ++k) fr[k] = NaN;
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    if (j >= T - nv) {
+      const double xv = win[j * RS];
+      const double nx = isnan_d(xv) ? pff : xv;
+      const double ret = nx / pff - 1.0;
+      pff = nx;
+      if (j >= 1) fr[j - 1] = 1.0 + ret;
+    }
+  }
+  double acc = fr[0];
+#pragma unroll
+  for (int k = 1; k < WR; ++k)
+    if (k < J) acc = acc * fr[k];
+  const bool ranked = !isnan_d(acc - 1.0);
+  sl.pff = last;
+  sl.psff = ranked ? last : NaN;
+  sl.prev = ranked ? lpm : -1;
+  sl.head = 0;
+  return true;
+}
+
+template <int WR>
+__global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
+    const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
+    int J, int skip, int G, int nbx, double* __restrict__ R, double* __restrict__ M,
+    double* __restrict__ NR, uint16_t* __restrict__ IDS, double* __restrict__ rec,
+    unsigned* __restrict__ sync) {
+  extern __shared__ __attribute__((aligned(16))) double tc_lds[];   // ring [T][256], pm [C][256]
+  __shared__ int s_t, s_last;
+  const int tid = threadIdx.x;
+  const int W = WR > 0 ? WR : J + skip, T = W + 1, SR = SUM_SCALARS + T + 1;
+  const unsigned total = (unsigned)G * (unsigned)nbx;
+#ifdef TC_TIMING
+  unsigned long long stamp[8];
+#endif
+  TC_STAMP(0);
+  if (tid == 0) s_t = (int)atomicInc(sync, total - 1u);   // wraps to 0 after the last ticket
+  __syncthreads();
+  const int t = s_t, g = t / nbx, x = t - g * nbx;
+  int m0, m1;
+  chunk_range(T_m, G, g, m0, m1);
+  const int RS = TC_COLS;
+  double* ring = tc_lds;            // [T][256]: the general walk's ring, the fast window
+  double* pmL = tc_lds + T * RS;    // [C][256]: the chunk's month prices
+  const int wv = tid >> 6, lane = tid & 63;
+  const bool worker = tid < TC_COLS;   // folds and scans asset la = tid (wave-uniform)
+  const int la = worker ? tid : 0;
+  const int64_t a = (int64_t)x * TC_COLS + la;
+  const bool live = worker && a < N;
+  const double NaN = qnan();
+
+  // ---- 1. month prices of the chunk (k_signal's reduction), into LDS ----
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lm = 128 * (wv & 1) + 2 * lane;   // this lane's asset pair in phase 1
+  const int64_t am = (int64_t)x * TC_COLS + lm;
+  const int voff = (int)((am < N ? am : 0) * 8);
+  const int rowb = (int)(N * 8);
+  for (int m = m0 + (wv >> 1); m < m1; m += TC_MONTH_WAVES) {
+    const int64_t f0 = month_start[m], nn = month_start[m + 1] - f0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(P + f0 * N), (short)0, (int)(nn * N * 8), 0x00020000);
+    double2 X[TC_MAXD];
+#pragma unroll
+    for (int k = 0; k < TC_MAXD; ++k) {   // rows past the month: out of range, no request
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + k * rowb, 0, 0);
+      X[k] = *reinterpret_cast<const double2*>(&w);
+    }
+    const int nnm = (int)nn;
+    double pm[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      double last = 0.0;
+      bool p = false, v = false;
+#pragma unroll
+      for (int k = 0; k < TC_MAXD; ++k) {
+        const double xv = comp(X[k], c);
+        const bool in = k < nnm;   // wave-uniform
+        const bool ok = in && xv == xv;
+        p |= in && !is_absent(xv);
+        v |= ok;
+        last = ok ? xv : last;
+      }
+      pm[c] = p ? (v ? last : qnan()) : absent_val();
+    }
+    *reinterpret_cast<double2*>(pmL + (m - m0) * RS + lm) = make_double2(pm[0], pm[1]);
+  }
+  __syncthreads();
+  TC_STAMP(1);
+
+  // ---- 2. this chunk's record (k_shard_summary_chunked's fields + last present month) ----
+  const int64_t hstride = (int64_t)nbx * SR * RS;   // chunk stride of a column's records
+  double* cp = rec + (int64_t)x * SR * RS + la;     // this asset's column of records
+  const int tm = m1 - m0;
+  if (worker) {
+    const double* col = pmL + la;
+    double* o = cp + (int64_t)g * hstride;
+    int n = 0, fv = -1, lvi = -1, lpm = -1;
+    double lv = NaN, first = absent_val();
+    for (int j = 0; j < tm; ++j) {
+      const double xv = col[j * RS];
+      if (is_absent(xv)) continue;
+      if (n == 0) first = xv;
+      if (!isnan_d(xv)) { if (fv < 0) fv = n; lvi = n; lv = xv; }
+      lpm = m0 + j;
+      ++n;
+    }
+    const int k = n < T ? n : T;
+    for (int j = 0; j < T - k; ++j) tc_put(o + (SUM_SCALARS + j) * RS, absent_val());
+    int got = 0;
+    double head = NaN;
+    int j = tm - 1;
+    for (; j >= 0 && got < k; --j) {
+      const double xv = col[j * RS];
+      if (is_absent(xv)) continue;
+      tc_put(o + (SUM_SCALARS + T - 1 - got) * RS, xv);
+      ++got;
+    }
+    for (; j >= 0; --j) {
+      const double xv = col[j * RS];
+      if (is_absent(xv)) continue;
+      if (!isnan_d(xv)) { head = xv; break; }
+    }
+    tc_put(o + 0 * RS, (double)n);
+    tc_put(o + 1 * RS, (double)fv);
+    tc_put(o + 2 * RS, (double)lvi);
+    tc_put(o + 3 * RS, lv);
+    tc_put(o + 4 * RS, head);
+    tc_put(o + 5 * RS, first);
+    tc_put(o + (int64_t)(SR - 1) * RS, (double)lpm);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+  __syncthreads();
+  if (tid == 0)
+    __hip_atomic_store((tc_gu32*)(sync + TC_SYNC0 + (int64_t)g * nbx + x), 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  TC_STAMP(2);
+
+  // ---- 3. wait for the records of chunks 0..g-1 of this column ----
+  if (g > 0) {
+    if (tid == 0) {
+      bool ok = true;
+      for (int h = 0; h < g && ok; ++h) {
+        const tc_gu32* f = (const tc_gu32*)(sync + TC_SYNC0 + (int64_t)h * nbx + x);
+        unsigned spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > TC_SPINS) {   // never expected: give up, mark the launch
+            __hip_atomic_store((tc_gu32*)(sync + 2), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            ok = false;
+            break;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  TC_STAMP(3);
+
+  // ---- 4. the scan state at month m0 ----
+  ScanLane sl;
+  sl.head = 0; sl.pff = NaN; sl.psff = NaN; sl.prev = -1;
+  double fr[WR > 0 ? WR : 1];
+#pragma unroll
+  for (int k = 0; k < (WR > 0 ? WR : 1); ++k) fr[k] = NaN;
+  if (worker) {
+    double* rl = ring + la;
+    if (g > 0 && live) {
+      bool done = false;
+      if constexpr (WR > 0) done = tc_fold_fast<WR>(cp, hstride, g, J, rl, RS, fr, sl);
+      if (!done) {
+        tc_fold_general(cp, hstride, g, W, J, rl, RS, sl);
+        if constexpr (WR > 0) {
+#pragma unroll
+          for (int k = 0; k < WR; ++k) fr[k] = rl[k * RS];
+        }
+      }
+    } else if (WR == 0) {
+      for (int k = 0; k < W; ++k) rl[k * RS] = NaN;
+    }
+  }
+  TC_STAMP(4);
+
+  // ---- 5. scan the chunk's months from LDS ----
+  if (live) {
+    for (int m = m0; m < m1; ++m) {
+      const double xv = pmL[(m - m0) * RS + la];
+      double mom;
+      if constexpr (WR > 0) mom = scan_step_reg<WR>(sl, xv, m, fr, J, N, a, R, M, NR);
+      else mom = scan_step(sl, xv, m, ring + la, RS, W, J, N, a, R, M, NR);
+      if (IDS) IDS[(int64_t)m * N + a] = (uint16_t)csm_fid(mom);
+    }
+    if (g == G - 1 && sl.prev >= 0) NR[(int64_t)sl.prev * N + a] = NaN;   // (scan_finish)
+  }
+
+  // ---- 6. the last workgroup out zeroes the flags for the next launch ----
+  __syncthreads();
+  TC_STAMP(5);
+#ifdef TC_TIMING
+  if (tid == 0) {
+    stamp[6] = (unsigned long long)g;
+    stamp[7] = (unsigned long long)x;
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(
+        rec + (int64_t)total * SR * RS) + (int64_t)t * 8;
+    for (int k = 0; k < 8; ++k) o[k] = stamp[k];
+  }
+#endif
+  if (tid == 0) s_last = atomicInc(sync + 1, total - 1u) == total - 1u;
+  __syncthreads();
+  if (s_last)
+    for (unsigned i = tid; i < total; i += TC_THREADS) sync[TC_SYNC0 + i] = 0u;
+}
+
+// =====================================================================================
 // Speculative date shards (the fused multi-GPU pass).  A rank runs k_signal<SH>
 // on its month range from an EMPTY scan state (trajectory F) before the earlier shards' carry
 // is known, writing PM and a [5][N] end-state record (present months, pending row, its psff,
@@ -2563,6 +3061,64 @@ int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_
     return set_err(ctx, CSM_E_INVAL, "csm_momentum_chunked_ids: ids must be non-NULL and 8-B "
                    "aligned, N %% 4 == 0 (N=%lld)", (long long)N);
   return momentum_chunked(ctx, PM, T_m, N, J, skip, C, R, M, NR, next_pm, workspace, ids);
+}
+
+// ---- the fused time-chunked signal (k_signal_tc, narrow panels) ----
+static int64_t tc_sync_bytes(int G, int nbx) {
+  return ((int64_t)(TC_SYNC0 + (int64_t)G * nbx) * 4 + 255) / 256 * 256;
+}
+
+int64_t csm_signal_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip, int32_t C) {
+  if (N <= 0 || C < 1 || J < 1 || skip < 0) return 0;
+  (void)T_m;
+  const int64_t nbx = (N + TC_COLS - 1) / TC_COLS, SR = SUM_SCALARS + J + skip + 2;
+  int64_t b = tc_sync_bytes(C, (int)nbx) + (int64_t)C * nbx * SR * TC_COLS * (int64_t)sizeof(double);
+#ifdef TC_TIMING
+  b += (int64_t)C * nbx * 64;
+#endif
+  return b;
+}
+
+int csm_signal_chunked(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                       const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                       int32_t J, int32_t skip, int32_t C, double* R, double* M, double* NR,
+                       uint16_t* ids, void* workspace) {
+  int r = prep(ctx);
+  if (r) return r;
+  const int W = J + skip;
+  if (!P || !month_start || !M || !NR || !workspace || N <= 0 || (N % 2) != 0 || T_d <= 0 ||
+      T_m < 0 || J < 1 || skip < 0 || W > 32 || C < 1 || C > TC_MAXG || max_month_days < 0 ||
+      max_month_days > TC_MAXD || !aligned16(P) || !aligned16(M) || !aligned16(NR) ||
+      (R && !aligned16(R)) || (ids && ((uintptr_t)ids & 3u) != 0) || N * 8 * TC_MAXD > INT32_MAX ||
+      ((uintptr_t)workspace & 255u) != 0)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_chunked: bad arguments (N=%lld even, T_m=%d, "
+                   "J + skip <= 32, 1 <= C <= %d, months of <= %d day rows, 16-B aligned P / M / "
+                   "NR / R, 4-B aligned ids, 256-B aligned workspace)", (long long)N, T_m,
+                   TC_MAXG, TC_MAXD);
+  if (T_m == 0) return CSM_OK;
+  if (C > T_m) C = T_m;
+  const int maxc = (T_m + C - 1) / C;
+  if (maxc > TC_MAXC)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_chunked: %d months per chunk (at most %d: more "
+                   "chunks)", maxc, TC_MAXC);
+  const int nbx = (int)((N + TC_COLS - 1) / TC_COLS);
+  unsigned* sync = (unsigned*)workspace;
+  double* rec = (double*)((char*)workspace + tc_sync_bytes(C, nbx));
+  const size_t lds = (size_t)(W + 1 + maxc) * TC_COLS * sizeof(double);
+  // the C2 look-back (J = 12, skip = 1) with its ring in registers; any other, from LDS
+  const void* kfn = W == 13 ? (const void*)k_signal_tc<13> : (const void*)k_signal_tc<0>;
+  if (lds > 65536)
+    HIP_CHECK(ctx, hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (W == 13)
+    hipLaunchKernelGGL(k_signal_tc<13>, dim3((unsigned)(C * nbx)), dim3(TC_THREADS), lds,
+                       ctx->stream, P, month_start, T_m, N, J, skip, C, nbx, R, M, NR, ids, rec,
+                       sync);
+  else
+    hipLaunchKernelGGL(k_signal_tc<0>, dim3((unsigned)(C * nbx)), dim3(TC_THREADS), lds,
+                       ctx->stream, P, month_start, T_m, N, J, skip, C, nbx, R, M, NR, ids, rec,
+                       sync);
+  LAUNCH_CHECK(ctx, "k_signal_tc");
+  return CSM_OK;
 }
 
 }  // extern "C"

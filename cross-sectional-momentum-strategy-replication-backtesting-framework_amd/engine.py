@@ -263,6 +263,41 @@ class Engine:
                        _ptr(M), _ptr(NR), _ptr(next_pm), _ptr(workspace))
         return R, M, NR
 
+    def signal_chunked(self, P, month_start, max_month_days, J=12, skip=1, chunks=None,
+                       with_ret=False, with_ids=True, out=None, workspace=None):
+        """csm_signal_chunked: month-end + time-chunked scan in one launch (narrow panels, C2):
+        the same R / M / NR / ids bits as month_end -> momentum_chunked(_ids).  Even N, months
+        of <= 23 day rows.  workspace: a zero-filled uint8 buffer of
+        csm_signal_chunked_workspace bytes (kept by the caller across calls: each launch leaves
+        its sync words zero).  Returns (R, M, NR, IDS, workspace)."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
+        C = self.default_chunks(T_m, N, J, skip) if chunks is None else int(chunks)
+        C = max(1, min(C, 64, max(T_m, 1)))
+        if out is None:
+            R = self.empty((T_m, N)) if with_ret else None
+            M, NR = self.empty((T_m, N)), self.empty((T_m, N))
+            IDS = self.empty((T_m, N), torch.int16) if with_ids else None
+        else:
+            R, M, NR, IDS = out
+        if IDS is not None:
+            _need(IDS, "IDS", torch.int16, (T_m, N), self.device)
+        nbytes = int(self.lib.csm_signal_chunked_workspace(T_m, N, int(J), int(skip), C))
+        if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
+            workspace = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+        self._call("csm_signal_chunked", _ptr(P), T_d, N, _ptr(month_start), T_m,
+                   int(max_month_days), int(J), int(skip), C, _ptr(R), _ptr(M), _ptr(NR),
+                   _ptr(IDS), _ptr(workspace))
+        return R, M, NR, IDS, workspace
+
+    @staticmethod
+    def signal_chunked_timed_out(workspace):
+        """Whether a csm_signal_chunked launch on this workspace gave up a wait (sync word 2;
+        never set by a correct launch).  Synchronises."""
+        return bool(workspace[8:12].view(torch.int32).item() != 0)
+
     def signal(self, P, month_start, max_month_days, J=12, skip=1, with_pm=False,
                with_ret=False, carry=None, next_pm=None, carry_out=None, out=None):
         """Fused month-end + scan (csm_signal): one pass over the daily panel, no PM round

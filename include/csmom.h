@@ -149,6 +149,24 @@ int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_
                              int32_t skip, int32_t C, double* R, double* M, double* NR,
                              const double* next_pm, uint16_t* ids, void* workspace);
 /*
+ * Month-end + time-chunked scan in ONE launch for narrow panels (C2; replaces csm_month_end ->
+ * csm_momentum_chunked_ids, four launches): a workgroup reduces one chunk's daily rows of 256
+ * assets to month prices in LDS, publishes the chunk's exchange record, folds the records of
+ * the earlier chunks of its columns (in-launch hand-off, bounded spins) and scans its months.
+ * The same R / M / NR / ids bits as csm_month_end -> csm_momentum (month_start / P as
+ * csm_signal; no carry, no next_pm: whole panels).  R and ids nullable.  Even N, months of at
+ * most 23 day rows (max_month_days), J + skip <= 32, 1 <= C <= 64 chunks of at most 32
+ * months, 16-B aligned P / M / NR / R, 4-B aligned ids.  workspace:
+ * csm_signal_chunked_workspace(T_m, N, J, skip, C) bytes, 256-B aligned and ZERO-FILLED before
+ * its first use (a launch leaves its sync words zero again; word 2 is set if a wait gave up,
+ * which no correct launch does).
+ */
+int64_t csm_signal_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip, int32_t C);
+int csm_signal_chunked(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                       const int64_t* month_start, int32_t T_m, int32_t max_month_days,
+                       int32_t J, int32_t skip, int32_t C, double* R, double* M, double* NR,
+                       uint16_t* ids, void* workspace);
+/*
  * The two together for narrow sweep panels (C3): every look-back Js[q] (1 <= nJ <= 4, host
  * arrays as csm_momentum_multi) from ONE time-chunked scan -- one summary / fold for max(J) (plus
  * each J's subset-ffilled price) and one chunked multi-J scan instead of three launches per J.
