@@ -34,6 +34,10 @@ def main():
     eng = csmom.Engine(0)
     if cells:
         assert eng.lib.csm_tune(b"dec_split_cells", cells) == 0
+    import os
+    split = os.environ.get("CSM_DEC_SPLIT")   # A/B: 0 = one workgroup per date row, 1 / 2 split
+    if split is not None:
+        assert eng.lib.csm_tune(b"dec_split", int(split)) == 0
     J, skip, nb = 12, 1, 10
     H = halo_months(J, skip)
     def panel(r):
@@ -156,7 +160,8 @@ def main():
         diag = dict(diag.most_common(12))
     print(json.dumps({
         "diag": diag,
-        "N": N, "days_per_rank": dpr, "split_cells": cells or 16384, "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
+        "N": N, "days_per_rank": dpr, "split_cells": cells or 16384,
+        "dec_split": __import__("os").environ.get("CSM_DEC_SPLIT", "default (2: auto)"), "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
         "F": hp.F, "G_emulated": G, "cap": cap, "listed_this_rank": int(cnt.item()),
         "collective_bytes_per_rank": {"need_bits": 4 * 8 * ((N + 63) // 64),
                                       "records": 8 * S * cap,
