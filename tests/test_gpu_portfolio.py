@@ -498,14 +498,22 @@ def test_grouped_equals_side_by_side(engine, G, Bg, vw, legs, mode, ncols):
 
 
 @pytest.mark.parametrize("B,Ks,ncols", [(1, (3, 6, 9, 12), 500), (16, (3, 6, 9, 12), 500),
-                                        (8, (12, 3), 1000), (5, (1, 7, 7), 372)])
-def test_turnover_mask_bit_identical(engine, B, Ks, ncols):
+                                        (8, (12, 3), 1000), (5, (1, 7, 7), 372),
+                                        (3, (3, 6, 9, 12), 4600)])
+@pytest.mark.parametrize("key", [b"turn_mask", b"turn_gi"])
+def test_turnover_mask_bit_identical(engine, B, Ks, ncols, key):
     """Steady equal-weight legs turnover from the leg bitplanes of the legs label sort
-    (k_turnover_ew_mask, popcounts of 64-cell words) against the label-byte path (turn_mask 0):
-    LS / TURN / COST / NET bit for bit -- plain batches and the grouped shared-return path of the
-    bootstrap sweep; row widths that end inside a plane word."""
+    (k_turnover_ew_mask, popcounts of 64-cell words) against the label-byte path (turn_mask 0),
+    and the general rows with several cell groups' label words per load round against one
+    group per round (turn_gi 0):
+    PR / LS / TURN / COST / NET bit for bit -- plain batches and the grouped shared-return path
+    of the bootstrap sweep; row widths that end inside a plane word, rows of several cell
+    groups per lane."""
     z = load_golden("c1")
-    PM, _ = engine.month_end(_up(np.ascontiguousarray(z["P"][:, :ncols])),
+    P = z["P"]
+    if ncols > P.shape[1]:   # rows wider than a lane's one cell group: tiled columns
+        P = np.tile(P, (1, -(-ncols // P.shape[1])))
+    PM, _ = engine.month_end(_up(np.ascontiguousarray(P[:, :ncols])),
                              _up(z["month_start"].astype(np.int64)))
     T_m, N = PM.shape
     _, M, NR = engine.momentum(PM, 12, 1)
@@ -517,13 +525,13 @@ def test_turnover_mask_bit_identical(engine, B, Ks, ncols):
     got = {}
     try:
         for mode in (1, 0):
-            assert lib.csm_tune(b"turn_mask", mode) == 0
+            assert lib.csm_tune(key, mode) == 0
             plain = engine.portfolio_multi(L, NR, 10, Ks=Ks, B=B, legs_only=True)
             grp = engine.portfolio_multi_js_grouped(torch.stack([L, L]), NR, 10, Ks=Ks, B=B,
                                                     legs_only=True)
             got[mode] = (plain, grp)
     finally:
-        lib.csm_tune(b"turn_mask", 1)
+        lib.csm_tune(key, 1)
     for i in range(2):
         for K in set(Ks):
             for f in ("LS", "TURN", "COST", "NET"):
