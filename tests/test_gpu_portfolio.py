@@ -503,9 +503,9 @@ def test_grouped_equals_side_by_side(engine, G, Bg, vw, legs, mode, ncols):
 def test_turnover_mask_bit_identical(engine, B, Ks, ncols, key=b"turn_mask"):
     """Steady equal-weight legs turnover from the leg bitplanes of the legs label sort
     (k_turnover_ew_mask, popcounts of 64-cell words) against the label-byte path (turn_mask 0):
-    PR / LS / TURN / COST / NET bit for bit -- plain batches and the grouped shared-return path
-    of the bootstrap sweep; row widths that end inside a plane word, rows of several cell
-    groups per lane."""
+    LS / TURN / COST / NET bit for bit -- plain batches and the grouped shared-return path of
+    the bootstrap sweep; row widths that end inside a plane word, rows of several cell groups
+    per lane."""
     z = load_golden("c1")
     P = z["P"]
     if ncols > P.shape[1]:   # rows wider than a lane's one cell group: tiled columns
