@@ -1704,8 +1704,10 @@ __global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
 // k_fold_carry -> k_momentum(carry) pass.
 // =====================================================================================
 #define REPAIR_THREADS 64
-#define REPAIR_CHUNK 8
-#define WALK_CHUNK 8
+#ifndef WALK_CHUNK
+#define WALK_CHUNK 8   // months per load round of the summary / repair walks
+#endif
+#define REPAIR_CHUNK WALK_CHUNK
 
 // Month price of asset a in month m of a speculative shard: PM where k_signal<SH> kept it,
 // else the month-end of the daily rows (k_signal's reduction: last valid price, NaN if the
