@@ -35,6 +35,9 @@ def main():
     if cells:
         assert eng.lib.csm_tune(b"dec_split_cells", cells) == 0
     import os
+    for kv in filter(None, os.environ.get("CSM_TUNE", "").split(",")):   # A/B: key=value,...
+        k, v = kv.split("=")
+        assert eng.lib.csm_tune(k.encode(), int(v)) == 0, kv
     split = os.environ.get("CSM_DEC_SPLIT")   # A/B: 0 = one workgroup per date row, 1 / 2 split
     if split is not None:
         assert eng.lib.csm_tune(b"dec_split", int(split)) == 0
@@ -161,7 +164,8 @@ def main():
     print(json.dumps({
         "diag": diag,
         "N": N, "days_per_rank": dpr, "split_cells": cells or 16384,
-        "dec_split": __import__("os").environ.get("CSM_DEC_SPLIT", "default (2: auto)"), "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
+        "dec_split": __import__("os").environ.get("CSM_DEC_SPLIT", "default (2: auto)"),
+        "tune": __import__("os").environ.get("CSM_TUNE", ""), "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
         "F": hp.F, "G_emulated": G, "cap": cap, "listed_this_rank": int(cnt.item()),
         "collective_bytes_per_rank": {"need_bits": 4 * 8 * ((N + 63) // 64),
                                       "records": 8 * S * cap,
