@@ -87,6 +87,9 @@ def parse(argv=None):
     ap.add_argument("--c2-unfused", action="store_true",
                     help="C2 A/B: k_month_end + the three-launch chunked scan (summary, fold, scan) "
                          "instead of the one-launch month-end + chunked scan (csm_signal_chunked)")
+    ap.add_argument("--no-oracle-mom", action="store_true",
+                    help="N = 1 decile check: qcut the engine's mom_J instead of the oracle's own "
+                         "month-end + scan of the panel (that pass adds ~10-20 s at C4)")
     ap.add_argument("--match-dates", type=int, default=0,
                     help="decile-match check on this many evenly spaced dates (0 = every date)")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -510,10 +513,24 @@ def main(argv=None):
         dates = sorted({int(x) for x in np.linspace(0, T_m - 1, args.match_dates)})
     else:
         dates = list(range(T_m))
+    # N = 1: the reference labels come from the ORACLE's mom_J -- the oracle's month-end and scan
+    # over this very panel, in column blocks (per-asset arithmetic: a block is exact) -- and the
+    # engine's mom_J is checked against it bit for bit on every cell
+    Mo, mom_exact = None, None
+    if world == 1 and not args.no_oracle_mom:
+        Mo = np.empty((T_m, N))
+        same = 0
+        for c0 in range(0, N, 20_000):
+            c1 = min(N, c0 + 20_000)
+            PMb, _ = O.month_end(panel.P[:, c0:c1].cpu().numpy(), ms_host)
+            _, Mb, _, _ = O.momentum_scan(PMb, J, skip)
+            Mo[:, c0:c1] = Mb
+            same += int((Mb.view(np.uint64) == Mh[:, c0:c1].cpu().numpy().view(np.uint64)).sum())
+        mom_exact = 100.0 * same / (T_m * N)
     tot = ok = 0
     for t0 in range(0, len(dates), 64):
         blk = dates[t0:t0 + 64]
-        mrows = Mh[blk].cpu().numpy()
+        mrows = Mo[blk] if Mo is not None else Mh[blk].cpu().numpy()
         lrows = Lh[blk].cpu().numpy()
         for row, got in zip(mrows, lrows):
             ref = np.full(N, -1, dtype=np.int8)
@@ -529,7 +546,9 @@ def main(argv=None):
     match = dict(pct=100.0 * ok / tot,
                  sample=f"{int(ndates)} of {tm_all} dates x {N} assets"
                         f"{f' (all {world} ranks)' if world > 1 else ''}: oracle qcut of the "
-                        f"engine's mom_J")
+                        + ("ORACLE's mom_J (oracle month-end + scan on this panel; engine mom_J "
+                           f"bit-exact on {mom_exact:.4f} % of cells)" if Mo is not None
+                           else "engine's mom_J"))
     if rank == 0 and args.dump:
         np.savez(args.dump, LS=LSh.cpu().numpy(), EW=EWh.cpu().numpy(), CNT=CNTh.cpu().numpy())
 
@@ -617,6 +636,7 @@ def main(argv=None):
             "stage_ms": ({k: round(v / args.steps, 4) for k, v in zip(stage_names, stage_ms)}
                          if world == 1 else None),
             "decile_match_pct": match["pct"] if match else None,
+            "mom_bit_exact_pct": mom_exact,
             "decile_check": match["sample"] if match else None,
             "cpu_baseline": None,
             # context only (not measured by this run): the reference's own pandas path
