@@ -2156,7 +2156,7 @@ int csm_tune(const char* key, int value) {
   if (!key) return CSM_E_INVAL;
   if (!strcmp(key, "cohort_lds") || !strcmp(key, "cohort_seg") || !strcmp(key, "turn_want") ||
       !strcmp(key, "overlap_rows") || !strcmp(key, "turn_gen_grid") || !strcmp(key, "gen_reset") ||
-      !strcmp(key, "turn_vwg") || !strcmp(key, "turn_mask"))
+      !strcmp(key, "turn_vwg") || !strcmp(key, "turn_mask") || !strcmp(key, "ls_opt"))
     return csm_tune_portfolio(key, value);
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_bwf") && (value == 0 || value == 1 || value == 4)) { g_tune_signal_bwf = value; return CSM_OK; }

@@ -423,7 +423,9 @@ __device__ __forceinline__ uint32_t byte_eq0(uint32_t z) {   // 0x80 in each byt
 // (k_turnover_ew_mask): the ballots themselves, word 4 g + e holding cell 4 (64 g + l) + e at
 // bit l (a fixed order of each 256-cell group, the same in every row; the counts it serves do
 // not depend on the order).
-template <int NB>
+// LSO: prefix ranks by v_mbcnt (fewer VALU operations per label word than the popcount of the
+// masked ballot; the same values)
+template <int NB, bool LSO = false>
 __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
     const int8_t* __restrict__ L, int64_t N, int C, int64_t rows, uint16_t* __restrict__ PERM,
     int32_t* __restrict__ OFF, double* __restrict__ FWp, PanAddr pa,
@@ -482,8 +484,13 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const uint64_t mb = __ballot((eb >> (8 * e + 7)) & 1u), mt = __ballot((et >> (8 * e + 7)) & 1u);
-      bb += __popcll(mb & lt);
-      bt += __popcll(mt & lt);
+      if constexpr (LSO) {   // set bits of the ballot below this lane: v_mbcnt (2 ops)
+        bb += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+        bt += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mt, 0u));
+      } else {
+        bb += __popcll(mb & lt);
+        bt += __popcll(mt & lt);
+      }
       totb += __popcll(mb);
       tott += __popcll(mt);
       pw_t = lane == 4 * (k & 15) + e ? mt : pw_t;
@@ -1829,6 +1836,8 @@ static int g_tune_gen_reset = 1;
 static int g_tune_turn_vwg = 1;
 // steady equal-weight legs turnover from the leg bitplanes (k_turnover_ew_mask) | 0 from labels
 static int g_tune_turn_mask = 1;
+// the one-wave legs label sort's prefix ranks by v_mbcnt (1) | masked popcounts (0)
+static int g_tune_ls_opt = 1;
 static int32_t* g_gen_probe = nullptr;
 
 __global__ void k_copy_i32(const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
@@ -1923,7 +1932,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
                            (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa, B);
       } else {
         if ((N & 3) == 0)   // one wave per row (C5's equal-weight legs)
-          hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
+          hipLaunchKernelGGL((g_tune_ls_opt ? k_label_sort_legs_ew<NB, true> : k_label_sort_legs_ew<NB, false>), dim3((unsigned)((T_m * (int64_t)B + PF_WAVES - 1) / PF_WAVES)),
                              dim3(PF_THREADS), 0, st, L, N, pl.C, (int64_t)T_m * B, PERM, OFF, FWp, pa,
                              g_tune_turn_mask ? (uint64_t*)(segws + lm_b) : nullptr, (N + 255) / 256 * 4);
         else
@@ -1985,7 +1994,8 @@ static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int
     double* FWp = (double*)(w + fw_b);
     const int64_t rows = (int64_t)T_m * nrow_b;
     if (legs && (N & 3) == 0)
-      hipLaunchKernelGGL((k_label_sort_legs_ew<NB>), dim3((unsigned)((rows + PF_WAVES - 1) / PF_WAVES)),
+      hipLaunchKernelGGL((g_tune_ls_opt ? k_label_sort_legs_ew<NB, true> : k_label_sort_legs_ew<NB, false>),
+                         dim3((unsigned)((rows + PF_WAVES - 1) / PF_WAVES)),
                          dim3(PF_THREADS), 0, st, Lq, N, 1, rows, PERM, OFF, FWp, pl_a,
                          g_tune_turn_mask ? (uint64_t*)(w + lm_b) : nullptr, (N + 255) / 256 * 4);
     else if (legs)
@@ -2094,6 +2104,10 @@ int csm_tune_portfolio(const char* key, int value) {
   }
   if (key && !strcmp(key, "turn_mask") && (value == 0 || value == 1)) {
     g_tune_turn_mask = value;
+    return CSM_OK;
+  }
+  if (key && !strcmp(key, "ls_opt") && (value == 0 || value == 1)) {
+    g_tune_ls_opt = value;
     return CSM_OK;
   }
   return CSM_E_INVAL;

@@ -60,7 +60,8 @@ int csm_abi_version(void);
  * of tests/test_gpu_capture.py), "turn_vwg" (1 a grouped batch's steady value-weight turnover
  * rows by one workgroup per weight panel | 0 one per row), "turn_mask" (1 steady equal-weight
  * legs turnover rows counted from the legs label sort's leg bitplanes | 0 from the label
- * bytes), "dec_split_cells" (cells per chunk of the split decile sweep, default 16384, a
+ * bytes), "ls_opt" (1 the one-wave legs label sort's prefix ranks by v_mbcnt | 0 masked
+ * popcounts), "dec_split_cells" (cells per chunk of the split decile sweep, default 16384, a
  * multiple of 1024; the split workspace is the context's).
  * Returns CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);

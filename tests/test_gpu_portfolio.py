@@ -500,9 +500,11 @@ def test_grouped_equals_side_by_side(engine, G, Bg, vw, legs, mode, ncols):
 @pytest.mark.parametrize("B,Ks,ncols", [(1, (3, 6, 9, 12), 500), (16, (3, 6, 9, 12), 500),
                                         (8, (12, 3), 1000), (5, (1, 7, 7), 372),
                                         (3, (3, 6, 9, 12), 4600)])
-def test_turnover_mask_bit_identical(engine, B, Ks, ncols, key=b"turn_mask"):
+@pytest.mark.parametrize("key", [b"turn_mask", b"ls_opt"])
+def test_turnover_mask_bit_identical(engine, B, Ks, ncols, key):
     """Steady equal-weight legs turnover from the leg bitplanes of the legs label sort
-    (k_turnover_ew_mask, popcounts of 64-cell words) against the label-byte path (turn_mask 0):
+    (k_turnover_ew_mask, popcounts of 64-cell words) against the label-byte path (turn_mask 0),
+    and the legs label sort's prefix ranks by v_mbcnt against masked popcounts (ls_opt 0):
     LS / TURN / COST / NET bit for bit -- plain batches and the grouped shared-return path of
     the bootstrap sweep; row widths that end inside a plane word, rows of several cell groups
     per lane."""

@@ -77,7 +77,7 @@ def test_tune_keys_documented_in_header_are_accepted():
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
              b"turn_gen_grid": ([1, 2048], 8192), b"gen_reset": ([0, 1], 1), b"turn_vwg": ([0, 1], 1),
              b"dec_split": ([0, 1, 2], 2), b"dec_split_cells": ([1024, 4096], 16384),
-             b"turn_mask": ([0, 1], 1)}
+             b"turn_mask": ([0, 1], 1), b"ls_opt": ([0, 1], 1)}
     for key, (vals, default) in cases.items():
         for v in vals:
             assert lib.csm_tune(key, v) == 0, (key, v)
