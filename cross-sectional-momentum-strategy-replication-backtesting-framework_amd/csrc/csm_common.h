@@ -124,6 +124,11 @@ __device__ __forceinline__ int csm_fbucket(double x) {
   const int k = b - (0x3FB00000 >> 10);   // bits(1/16) >> 42
   return k < 0 ? 0 : (k > CSM_FB_BUCKETS - 1 ? CSM_FB_BUCKETS - 1 : k);
 }
+// set bits of a wave mask below this lane (v_mbcnt_lo / hi: 2 ops; the popcount of the masked
+// ballot is 4)
+__device__ __forceinline__ int lane_prefix(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 __device__ __forceinline__ uint32_t csm_fid(double x) {
   return x == x ? (uint32_t)csm_fbucket(x) : CSM_FB_NAN;
 }
