@@ -160,7 +160,8 @@ int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_
  * months, 16-B aligned P / M / NR / R, 4-B aligned ids.  workspace:
  * csm_signal_chunked_workspace(T_m, N, J, skip, C) bytes, 256-B aligned and ZERO-FILLED before
  * its first use (a launch leaves its sync words zero again; word 2 is set if a wait gave up,
- * which no correct launch does).
+ * which no correct launch does).  One launch at a time per workspace: two launches in flight
+ * on different streams must not share one (their tickets and flags would mix).
  */
 int64_t csm_signal_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip, int32_t C);
 int csm_signal_chunked(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
