@@ -133,6 +133,7 @@ class DateShardPipeline:
         self.halo = halo_months(J, skip) if halo is None else int(halo)
         # ... and the forward months after it (the next rank's first ones)
         self.fwd = FWD_MONTHS if fwd is None else int(fwd)
+        self._rows = {}   # collective 2's row index (every rank's months in order), per device
 
     def _check_months(self, T_m):
         if T_m != self.months[self.rank]:
@@ -249,17 +250,22 @@ class DateShardPipeline:
         else:
             L, EW, CNT, _ = st.deciles(M, NR, nb)
         if self.G > 1:
-            pad_ew = torch.full((self.Tmax, nb), float("nan"), dtype=EW.dtype, device=EW.device)
-            pad_cnt = torch.zeros((self.Tmax, nb), dtype=CNT.dtype, device=CNT.device)
-            pad_ew[:T_m] = EW
-            pad_cnt[:T_m] = CNT
-            # one collective for both: counts ride as exact float64
-            packed = torch.cat([pad_ew, pad_cnt.to(EW.dtype)], dim=1)
+            # one collective for both: counts ride as exact float64; the padding rows past a
+            # rank's months are never read, so they stay unwritten
+            packed = torch.empty((self.Tmax, 2 * nb), dtype=EW.dtype, device=EW.device)
+            packed[:T_m, :nb] = EW
+            packed[:T_m, nb:] = CNT
             allp = self.gather(packed)                                  # collective 2
-            ews = [allp[g, :self.months[g], :nb] for g in range(self.G)]
-            cns = [allp[g, :self.months[g], nb:] for g in range(self.G)]
-            EW = torch.cat(ews, 0).contiguous()
-            CNT = torch.cat(cns, 0).to(torch.int32).contiguous()
+            # every rank's months in order: one row gather over the stacked blocks
+            key = (str(EW.device), nb)
+            idx = self._rows.get(key)
+            if idx is None:
+                idx = torch.cat([torch.arange(m, dtype=torch.int64) + g * self.Tmax
+                                 for g, m in enumerate(self.months)]).to(EW.device)
+                self._rows[key] = idx
+            flat = allp.reshape(self.G * self.Tmax, 2 * nb).index_select(0, idx)
+            EW = flat[:, :nb].contiguous()
+            CNT = flat[:, nb:].to(torch.int32)
         LS = st.long_short(EW, CNT)
         return ShardResult(M=M, NR=NR, L=L, EW=EW, CNT=CNT, LS=LS)
 
