@@ -139,3 +139,36 @@ def test_rejects_bad_args(engine):
         engine.signal_chunked(P, ms, 24, 12, 1)
     with pytest.raises(csmom.CsmError):   # more than 32 months per chunk
         engine.signal_chunked(P, ms, 23, 12, 1, chunks=1)
+
+
+def test_handoff_under_uneven_load(engine):
+    """The in-launch record hand-off (write-through records, one flag per record, relaxed polls,
+    one agent acquire) under uneven load and with consumer caches warm from the previous launch
+    of the SAME workspace: two different panels alternate through one workspace while a second
+    stream streams 1 GB copies, 24 launches; every result equals its panel's eager result bit
+    for bit (a stale record line from the previous launch would change the fold)."""
+    pans = [_panel(5_000, 3_000, s, heavy=(s % 2 == 0)) for s in (41, 42)]
+    Ps = [_up(p["P"]) for p in pans]
+    mss = [_up(p["month_start"]) for p in pans]
+    maxd = max(int(np.diff(p["month_start"]).max()) for p in pans)
+    refs = []
+    for P, ms in zip(Ps, mss):
+        _, M, NR, I, _ = engine.signal_chunked(P, ms, maxd, 12, 1)
+        refs.append((M.clone(), NR.clone(), I.clone()))
+    ws = None
+    src = torch.empty(128 * 1024 * 1024, dtype=torch.float64, device="cuda:0").uniform_()
+    dst = torch.empty_like(src)
+    side = torch.cuda.Stream()
+    outs = []
+    for it in range(24):
+        k = it % 2
+        with torch.cuda.stream(side):   # bandwidth pressure on other CUs meanwhile
+            dst.copy_(src)
+        _, M, NR, I, ws = engine.signal_chunked(Ps[k], mss[k], maxd, 12, 1, workspace=ws)
+        outs.append((k, M, NR, I))
+    torch.cuda.synchronize()
+    assert not engine.signal_chunked_timed_out(ws)
+    for k, M, NR, I in outs:
+        assert bits_equal(M.cpu().numpy(), refs[k][0].cpu().numpy())
+        assert bits_equal(NR.cpu().numpy(), refs[k][1].cpu().numpy())
+        assert torch.equal(I, refs[k][2])
