@@ -379,6 +379,7 @@ def main(argv=None):
     tc = narrow_ids and not args.c2_unfused and max_days <= 23 and N % 2 == 0
     tc_ws = None
     if tc:
+        chunks = args.chunks or eng.signal_default_chunks(T_m, N, J, skip, eng.cus)
         nbytes = int(eng.lib.csm_signal_chunked_workspace(T_m, N, J, skip, min(chunks, 64)))
         tc_ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
     ws = None

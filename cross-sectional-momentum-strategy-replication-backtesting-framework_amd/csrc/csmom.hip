@@ -1227,9 +1227,14 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 // sync [0] ticket, [1] done, [2] timeout, [3] pad, [4 ..) flags [G][nbx].  Records
 // [G][nbx][SR][256] f64: one (chunk, column)'s record is whole cache lines of its own.
 // =====================================================================================
+#ifndef TC_THREADS
 #define TC_THREADS 512   // eight waves reduce months; the first four fold and scan
-#define TC_MONTH_WAVES (TC_THREADS / 128)   // month slots per asset half
-#define TC_COLS 256      // assets per workgroup
+#endif
+#ifndef TC_COLS
+#define TC_COLS 256      // assets per workgroup (a multiple of 128)
+#endif
+#define TC_HALVES (TC_COLS / 128)                    // 128-asset slices of a column
+#define TC_MONTH_WAVES (TC_THREADS / 64 / TC_HALVES)   // month slots per slice
 #define TC_MAXD 23       // day rows per month (a business month)
 #define TC_MAXG 64       // chunks
 #define TC_MAXC 32       // months per chunk
@@ -1528,11 +1533,11 @@ __global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
 
   // ---- 1. month prices of the chunk (k_signal's reduction), into LDS ----
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const int lm = 128 * (wv & 1) + 2 * lane;   // this lane's asset pair in phase 1
+  const int lm = 128 * (wv % TC_HALVES) + 2 * lane;   // this lane's asset pair in phase 1
   const int64_t am = (int64_t)x * TC_COLS + lm;
   const int voff = (int)((am < N ? am : 0) * 8);
   const int rowb = (int)(N * 8);
-  for (int m = m0 + (wv >> 1); m < m1; m += TC_MONTH_WAVES) {
+  for (int m = m0 + wv / TC_HALVES; m < m1; m += TC_MONTH_WAVES) {
     const int64_t f0 = month_start[m], nn = month_start[m + 1] - f0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(P + f0 * N), (short)0, (int)(nn * N * 8), 0x00020000);

@@ -106,6 +106,7 @@ class Engine:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.lib = load_library()
+        self.cus = int(torch.cuda.get_device_properties(self.device).multi_processor_count)
         h = ctypes.c_void_p()
         st = self.lib.csm_create(self.device.index, ctypes.byref(h))
         if st != 0:
@@ -263,6 +264,20 @@ class Engine:
                        _ptr(M), _ptr(NR), _ptr(next_pm), _ptr(workspace))
         return R, M, NR
 
+    @staticmethod
+    def signal_default_chunks(T_m, N, J=12, skip=1, cus=256):
+        """Chunks for csm_signal_chunked: as many as keep the grid (chunks x ceil(N / 256)
+        workgroups) within one workgroup per CU, chunks no shorter than one window, and never
+        fewer than the 32-months-per-chunk limit needs.  A second workgroup on a CU waits for
+        the first to leave (each holds ~80 KB of LDS and its month-end stream saturates the
+        CU), so the grid beyond the CU count serialises: C2 (20 column blocks) at 12 / 13 / 21
+        chunks 0.130 / 0.152 / 0.140 ms per step (profiles/r05/experiments/tc_chunks/)."""
+        if T_m <= 0:
+            return 1
+        nbx = max(1, -(-N // 256))
+        c = min(max(1, cus // nbx), max(1, T_m // max(J + skip + 1, 1)), 64)
+        return int(min(max(c, -(-T_m // 32)), 64))
+
     def signal_chunked(self, P, month_start, max_month_days, J=12, skip=1, chunks=None,
                        with_ret=False, with_ids=True, out=None, workspace=None):
         """csm_signal_chunked: month-end + time-chunked scan in one launch (narrow panels, C2):
@@ -274,7 +289,8 @@ class Engine:
         T_m = month_start.numel() - 1
         _need(P, "P", torch.float64, (T_d, N), self.device)
         _need(month_start, "month_start", torch.int64, (T_m + 1,), self.device)
-        C = self.default_chunks(T_m, N, J, skip) if chunks is None else int(chunks)
+        C = (self.signal_default_chunks(T_m, N, J, skip, self.cus) if chunks is None
+             else int(chunks))
         C = max(1, min(C, 64, max(T_m, 1)))
         if out is None:
             R = self.empty((T_m, N)) if with_ret else None

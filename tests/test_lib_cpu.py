@@ -102,3 +102,19 @@ def test_collective_entry_points_without_gpu():
     assert lib.csm_allgather(None, None, None, 8) == -1
     assert lib.csm_allgather_free(None) == -1
     assert lib.csm_comm_unique_id(None) == -1
+
+
+def test_signal_default_chunks():
+    """csm_signal_chunked's default chunk count: the grid (chunks x ceil(N / 256)) within one
+    workgroup per CU, chunks no shorter than one window, at least ceil(T_m / 32) chunks."""
+    from csmom import Engine
+    f = Engine.signal_default_chunks
+    assert f(310, 5_000, 12, 1, 256) == 12          # C2: 20 column blocks -> 240 workgroups
+    assert f(310, 1_000, 12, 1, 256) == 22          # narrow: one window per chunk binds
+    assert f(310, 5_000, 12, 1, 304) == 15
+    assert f(2_000, 60_000, 12, 1, 256) == 63       # wide: the 32-month limit binds
+    assert f(0, 5_000) == 1 and f(10, 512, 12, 1) == 1
+    for T_m in (1, 31, 32, 33, 700, 2_048):
+        for N in (2, 256, 5_000, 100_000):
+            C = f(T_m, N, 12, 1, 256)
+            assert 1 <= C <= 64 and -(-T_m // C) <= 32
