@@ -63,11 +63,16 @@ def test_c2_size_bits_and_chunked_path(engine):
 @pytest.mark.parametrize("N,T,J,skip,C", [(1_000, 2_600, 3, 0, None), (4_004, 1_500, 9, 2, 7),
                                           (2_002, 3_000, 12, 1, 64), (998, 800, 1, 1, 2),
                                           (600, 2_000, 24, 2, None), (514, 2_400, 12, 1, 13),
-                                          (256, 300, 12, 1, 1)])
+                                          (256, 300, 12, 1, 1), (2_050, 6_000, 12, 1, 10),
+                                          (1_000, 6_000, 12, 1, None), (770, 4_000, 12, 1, 7)])
 def test_gappy_panels_every_chunking(engine, N, T, J, skip, C):
     """30 % late listings, 30 % delistings, 5 % absent / all-NaN months and missing days: the
     pending next_ret rows that cross chunk boundaries (written by the chunk with the asset's
-    next present row, or NaN by the last chunk), assets absent for whole chunks, one chunk."""
+    next present row, or NaN by the last chunk), assets absent for whole chunks, one chunk.
+    J = 12 / skip = 1 with chunks longer than 14 months (the last three cases) take the
+    speculative scan of the idle waves: both of its outcomes -- states equal after month m0 + 13
+    (its outputs stand, plus next_ret of m0 + 13 and the last present month's NaN) and unequal
+    (the folding lane rescans over them) -- occur on these panels."""
     pan = _panel(N, T, 100 + N, heavy=True)
     _check(engine, _up(pan["P"]), _up(pan["month_start"]), J, skip, C)
 
