@@ -1241,6 +1241,9 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 #define TC_SYNC0 4       // sync words before the flags
 #define TC_SPINS (1u << 21)
 #define TC_NC 16         // chunk counts per load trip of the window search
+#ifndef TC_REC2
+#define TC_REC2 1        // the record's forward and backward fields by the two wave halves
+#endif
 // -DTC_TIMING (experiment builds, scripts/build_variant.py): per-workgroup phase stamps
 // (wall clock, 100 MHz) in 8 u64 words per ticket after the records (workspace grows)
 #ifdef TC_TIMING
@@ -1573,42 +1576,59 @@ __global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
   const int64_t hstride = (int64_t)nbx * SR * RS;   // chunk stride of a column's records
   double* cp = rec + (int64_t)x * SR * RS + la;     // this asset's column of records
   const int tm = m1 - m0;
-  if (worker) {
-    const double* col = pmL + la;
-    double* o = cp + (int64_t)g * hstride;
-    int n = 0, fv = -1, lvi = -1, lpm = -1;
-    double lv = NaN, first = absent_val();
-    for (int j = 0; j < tm; ++j) {
-      const double xv = col[j * RS];
-      if (is_absent(xv)) continue;
-      if (n == 0) first = xv;
-      if (!isnan_d(xv)) { if (fv < 0) fv = n; lvi = n; lv = xv; }
-      lpm = m0 + j;
-      ++n;
+  // the forward fields (count, first valid / last valid index, last valid price, first present
+  // price) by the folding waves, the backward ones (the newest T present prices, the head, the
+  // last present month) by the other waves at once (TC_REC2; else one wave does both)
+  constexpr bool REC2 = TC_REC2 && TC_THREADS == 2 * TC_COLS;
+  const int lr = worker ? la : tid - TC_COLS;   // the record column this lane writes
+  const bool fwd = worker, bwd = REC2 ? !worker : worker;
+  if (worker || REC2) {
+    const double* col = pmL + lr;
+    double* o = rec + (int64_t)x * SR * RS + lr + (int64_t)g * hstride;
+    if (fwd) {
+      int n = 0, fv = -1, lvi = -1;
+      double lv = NaN, first = absent_val();
+      for (int j0 = 0; j0 < tm; j0 += 8) {   // 8 months' LDS loads in flight per trip
+        double xs[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) xs[u] = j0 + u < tm ? col[(j0 + u) * RS] : absent_val();
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double xv = xs[u];
+          if (!is_absent(xv)) {
+            if (n == 0) first = xv;
+            if (!isnan_d(xv)) { if (fv < 0) fv = n; lvi = n; lv = xv; }
+            ++n;
+          }
+        }
+      }
+      tc_put(o + 0 * RS, (double)n);
+      tc_put(o + 1 * RS, (double)fv);
+      tc_put(o + 2 * RS, (double)lvi);
+      tc_put(o + 3 * RS, lv);
+      tc_put(o + 5 * RS, first);
     }
-    const int k = n < T ? n : T;
-    for (int j = 0; j < T - k; ++j) tc_put(o + (SUM_SCALARS + j) * RS, absent_val());
-    int got = 0;
-    double head = NaN;
-    int j = tm - 1;
-    for (; j >= 0 && got < k; --j) {
-      const double xv = col[j * RS];
-      if (is_absent(xv)) continue;
-      tc_put(o + (SUM_SCALARS + T - 1 - got) * RS, xv);
-      ++got;
+    if (bwd) {
+      // the newest min(n, T) present prices into the tail rows, absent fill below them
+      int got = 0, lpm = -1;
+      double head = NaN;
+      int j = tm - 1;
+      for (; j >= 0 && got < T; --j) {
+        const double xv = col[j * RS];
+        if (is_absent(xv)) continue;
+        if (got == 0) lpm = m0 + j;
+        tc_put(o + (SUM_SCALARS + T - 1 - got) * RS, xv);
+        ++got;
+      }
+      for (int i = 0; i < T - got; ++i) tc_put(o + (SUM_SCALARS + i) * RS, absent_val());
+      for (; j >= 0; --j) {
+        const double xv = col[j * RS];
+        if (is_absent(xv)) continue;
+        if (!isnan_d(xv)) { head = xv; break; }
+      }
+      tc_put(o + 4 * RS, head);
+      tc_put(o + (int64_t)(SR - 1) * RS, (double)lpm);
     }
-    for (; j >= 0; --j) {
-      const double xv = col[j * RS];
-      if (is_absent(xv)) continue;
-      if (!isnan_d(xv)) { head = xv; break; }
-    }
-    tc_put(o + 0 * RS, (double)n);
-    tc_put(o + 1 * RS, (double)fv);
-    tc_put(o + 2 * RS, (double)lvi);
-    tc_put(o + 3 * RS, lv);
-    tc_put(o + 4 * RS, head);
-    tc_put(o + 5 * RS, first);
-    tc_put(o + (int64_t)(SR - 1) * RS, (double)lpm);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
   __syncthreads();
