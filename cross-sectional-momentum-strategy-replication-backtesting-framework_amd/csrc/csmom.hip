@@ -1261,8 +1261,9 @@ __device__ __forceinline__ void tc_put(double* p, double v) {   // write-through
 }
 
 // scan_step with the ring in registers, oldest first (the same factors, product order and
-// stores as scan_step's LDS ring)
-template <int WR>
+// stores as scan_step's LDS ring).  JC > 0: J is the compile-time JC (the product's factor
+// count folds: no per-factor select).
+template <int WR, int JC = 0>
 __device__ __forceinline__ double scan_step_reg(ScanLane& s, double x, int m, double (&fr)[WR],
                                                 int J, int64_t N, int64_t a,
                                                 double* __restrict__ R, double* __restrict__ M,
@@ -1285,7 +1286,7 @@ __device__ __forceinline__ double scan_step_reg(ScanLane& s, double x, int m, do
   double acc = fr[0];
 #pragma unroll
   for (int k = 1; k < WR; ++k)
-    if (k < J) acc = acc * fr[k];
+    if (k < (JC > 0 ? JC : J)) acc = acc * fr[k];
   const double mom = acc - 1.0;
   const bool ranked = !isnan_d(mom);
   const double ps_new = xv ? x : s.psff;
@@ -1504,7 +1505,7 @@ __device__ __forceinline__ bool tc_fold_fast(const double* cp, int64_t hs, int g
   return true;
 }
 
-template <int WR>
+template <int WR, int JC = 0>
 __global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, int G, int nbx, double* __restrict__ R, double* __restrict__ M,
@@ -1685,12 +1686,14 @@ __global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
   }
   TC_STAMP(4);
 
-  // ---- 5. scan the chunk's months from LDS ----
+  // ---- 5. scan the chunk's months from LDS (the next month's price read a step ahead) ----
   if (live) {
+    double xn = pmL[la];
     for (int m = m0; m < m1; ++m) {
-      const double xv = pmL[(m - m0) * RS + la];
+      const double xv = xn;
+      if (m + 1 < m1) xn = pmL[(m + 1 - m0) * RS + la];
       double mom;
-      if constexpr (WR > 0) mom = scan_step_reg<WR>(sl, xv, m, fr, J, N, a, R, M, NR);
+      if constexpr (WR > 0) mom = scan_step_reg<WR, JC>(sl, xv, m, fr, J, N, a, R, M, NR);
       else mom = scan_step(sl, xv, m, ring + la, RS, W, J, N, a, R, M, NR);
       if (IDS) IDS[(int64_t)m * N + a] = (uint16_t)csm_fid(mom);
     }
@@ -3133,10 +3136,16 @@ int csm_signal_chunked(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
   double* rec = (double*)((char*)workspace + tc_sync_bytes(C, nbx));
   const size_t lds = (size_t)(W + 1 + maxc) * TC_COLS * sizeof(double);
   // the C2 look-back (J = 12, skip = 1) with its ring in registers; any other, from LDS
-  const void* kfn = W == 13 ? (const void*)k_signal_tc<13> : (const void*)k_signal_tc<0>;
+  // (and the C2 window J = 12 with its product length fixed at compile time)
+  const void* kfn = W == 13 ? (J == 12 ? (const void*)k_signal_tc<13, 12> : (const void*)k_signal_tc<13>)
+                            : (const void*)k_signal_tc<0>;
   if (lds > 65536)
     HIP_CHECK(ctx, hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  if (W == 13)
+  if (W == 13 && J == 12)
+    hipLaunchKernelGGL((k_signal_tc<13, 12>), dim3((unsigned)(C * nbx)), dim3(TC_THREADS), lds,
+                       ctx->stream, P, month_start, T_m, N, J, skip, C, nbx, R, M, NR, ids, rec,
+                       sync);
+  else if (W == 13)
     hipLaunchKernelGGL(k_signal_tc<13>, dim3((unsigned)(C * nbx)), dim3(TC_THREADS), lds,
                        ctx->stream, P, month_start, T_m, N, J, skip, C, nbx, R, M, NR, ids, rec,
                        sync);
