@@ -232,6 +232,7 @@ __device__ __forceinline__ double scan_step(ScanLane& s, double x, int m, double
 // (and ret_1m) as one 16-B store per row, next_ret as one 16-B store when both assets write
 // the same row (the steady state), so a wave issues half the store instructions.  Same
 // arithmetic in the same order as two scan_step calls: bit-identical outputs.
+template <int JC = 0>   // JC > 0: J fixed at compile time (the product's ring reads unrolled)
 __device__ __forceinline__ void scan_step_pair(ScanLane (&s)[2], const double (&x)[2], int m,
                                                double* ring0, int RS, int W, int J, int64_t N,
                                                int64_t a0, double* __restrict__ R,
@@ -259,9 +260,20 @@ __device__ __forceinline__ void scan_step_pair(ScanLane (&s)[2], const double (&
     s[c].head = (s[c].head + 1 == W) ? 0 : s[c].head + 1;
     double acc = ring[s[c].head * RS];
     int idx = s[c].head;
-    for (int k = 1; k < J; ++k) {
-      idx = (idx + 1 == W) ? 0 : idx + 1;
-      acc = acc * ring[idx * RS];
+    if constexpr (JC > 0) {
+      double f[JC];   // the ring reads all issued before the product
+#pragma unroll
+      for (int k = 1; k < JC; ++k) {
+        idx = (idx + 1 == W) ? 0 : idx + 1;
+        f[k] = ring[idx * RS];
+      }
+#pragma unroll
+      for (int k = 1; k < JC; ++k) acc = acc * f[k];
+    } else {
+      for (int k = 1; k < J; ++k) {
+        idx = (idx + 1 == W) ? 0 : idx + 1;
+        acc = acc * ring[idx * RS];
+      }
     }
     mom[c] = acc - 1.0;
     const bool ranked = !isnan_d(mom[c]);
@@ -762,7 +774,7 @@ __device__ __forceinline__ bool shard_pm_kept(int m, int T_m, int W) {
 // price, and the first / last present month (-1 none) -- for k_shard_summary_state and
 // k_shard_repair.
 // BL (VEC 2): day rows by raw buffer loads (see load_month).
-template <int MAXD, int VEC, int NBUF, int BW, bool SH, bool BL>
+template <int MAXD, int VEC, int NBUF, int BW, bool SH, bool BL, int JC = 0>
 __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
@@ -846,7 +858,7 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
       }
       double mom[VEC];
       if constexpr (VEC == 2) {   // paired 16-B stores (R / M / NR are 16-B aligned)
-        scan_step_pair(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
+        scan_step_pair<JC>(reinterpret_cast<ScanLane (&)[2]>(sl), reinterpret_cast<const double (&)[2]>(pm),
                        m, ring_lds + VEC * tid, RS, W, J, N, a0, R, M, NR,
                        reinterpret_cast<double (&)[2]>(mom));
       } else {
@@ -2156,6 +2168,7 @@ __global__ __launch_bounds__(UNION_THREADS) void k_shard_union(const uint64_t* _
 // lost their A/B (profiles/r0*/experiments) are not in the library.
 static int g_tune_signal_vec = 2;      // k_signal assets per lane: 2 (paired 16-B rows) | 1 (odd N)
 static int g_tune_signal_bwf = 0;      // k_signal blocks: 0 auto | 1 one wave | 4 four barrier-free waves x 2 month buffers (buffer loads)
+static int g_tune_signal_j12 = 1;      // wide shard k_signal: J = 12 with its product length fixed at compile time (0: runtime J)
 #define SIGNAL_BWF_MIN_N (180 * 512)   // auto: 4-wave blocks once the grid still covers >= 180 CUs
 static int64_t* g_dec_timing = nullptr;
 // PRE decile pass (csm_deciles_ids): 1 the merged sweep, then the general kernel for the rows it
@@ -2188,6 +2201,7 @@ int csm_tune(const char* key, int value) {
     return csm_tune_portfolio(key, value);
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_bwf") && (value == 0 || value == 1 || value == 4)) { g_tune_signal_bwf = value; return CSM_OK; }
+  if (!strcmp(key, "signal_j12") && (value == 0 || value == 1)) { g_tune_signal_j12 = value; return CSM_OK; }
   if (!strcmp(key, "dec_merge") && (value == 0 || value == 1)) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
@@ -2426,7 +2440,13 @@ static int signal_launch(csm_ctx* ctx, const char* who, const double* P, int64_t
   (max_month_days <= 23 && V == 2 ? (const void*)k_signal<23, V, 4, 1, SH_, false>              \
    : max_month_days <= 24         ? (const void*)k_signal<24, V, 4, 1, SH_, false>              \
                                   : (const void*)k_signal<32, V, 4, 1, SH_, false>)
-  if (wide4)
+  // date shards: the default look-back J = 12 with its product length fixed at compile time
+  // (8-way halo rank: shard kernel 0.237 -> 0.231 ms; the full C4 pass measured 0.3 % slower
+  // with it, so the one-GPU kernel keeps the runtime J)
+  const bool j12 = sh && J == 12 && g_tune_signal_j12;
+  if (wide4 && j12)
+    fn = (const void*)k_signal<23, 2, 2, 4, true, true, 12>;
+  else if (wide4)
     fn = sh ? (const void*)k_signal<23, 2, 2, 4, true, true> : (const void*)k_signal<23, 2, 2, 4, false, true>;
   else if (vec == 2)
     fn = sh ? SIG1(2, true) : SIG1(2, false);

@@ -382,7 +382,10 @@ def test_halo_shards_sparse_panel(engine, G, H):
 
 
 @pytest.mark.parametrize("G", [2, 7])
-def test_halo_shards_four_wave_blocks(engine, G):
+@pytest.mark.parametrize("j12", [1, 0])
+def test_halo_shards_four_wave_blocks(engine, G, j12):
+    """The halo rank's shard kernel in the C4 block shape, J = 12 with its product length fixed
+    at compile time (the default) and with the runtime J: the one-GPU pass's bits."""
     from oracle.synth_np import make_panel
     from csmom.distributed import virtual_shards_halo
     pan = make_panel(1_000, 2600, seed=13, nan_day=0.05, absent_month=0.2, nan_month=0.1,
@@ -392,9 +395,11 @@ def test_halo_shards_four_wave_blocks(engine, G):
     lib = engine.lib
     try:
         assert lib.csm_tune(b"signal_bwf", 4) == 0
+        assert lib.csm_tune(b"signal_j12", j12) == 0
         res = virtual_shards_halo(engine, P, ms, G, 12, 1, 10)
     finally:
         lib.csm_tune(b"signal_bwf", 0)
+        lib.csm_tune(b"signal_j12", 1)
     _halo_equal(out, res, ew=False)
 
 
