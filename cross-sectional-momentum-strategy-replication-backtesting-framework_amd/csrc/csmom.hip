@@ -1230,8 +1230,8 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 // bit-identical R / M / NR / ids.
 // Hand-off (MI355X_MICROARCH.md, visibility, row 1): records stored write-through (agent
 // relaxed atomic stores), every storing wave drains (vmcnt 0), a barrier, ONE lane stores the
-// flag; the consumer polls each flag with relaxed agent loads, ONE agent acquire, a barrier,
-// plain loads.  Workgroups take tickets in arrival order and ticket t is chunk t / nbx, so
+// flag; the consumer polls the flags with relaxed agent loads (one wave, a lane per flag: all
+// of them in one load per trip), ONE agent acquire, a barrier, plain loads.  Workgroups take tickets in arrival order and ticket t is chunk t / nbx, so
 // every record a workgroup waits for belongs to an earlier ticket -- a workgroup already
 // running: no residency assumption.  Spins are bounded (timeout word).  The last workgroup to
 // finish zeroes the flags; the ticket and done counters wrap to 0 themselves, so the sync
@@ -1652,19 +1652,20 @@ __global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
 
   // ---- 3. wait for the records of chunks 0..g-1 of this column ----
   if (g > 0) {
-    if (tid == 0) {
-      bool ok = true;
-      for (int h = 0; h < g && ok; ++h) {
-        const tc_gu32* f = (const tc_gu32*)(sync + TC_SYNC0 + (int64_t)h * nbx + x);
-        unsigned spins = 0;
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > TC_SPINS) {   // never expected: give up, mark the launch
+    if (tid < 64) {   // wave 0: lane h polls chunk h's flag, all g flags in one load per trip
+      bool got = lane >= g;
+      unsigned spins = 0;
+      while (true) {
+        if (!got)
+          got = __hip_atomic_load((const tc_gu32*)(sync + TC_SYNC0 + (int64_t)lane * nbx + x),
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        if (__ballot(!got) == 0ull) break;   // (wave-uniform)
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > TC_SPINS) {   // never expected: give up, mark the launch
+          if (lane == 0)
             __hip_atomic_store((tc_gu32*)(sync + 2), 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-            ok = false;
-            break;
-          }
+          break;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
