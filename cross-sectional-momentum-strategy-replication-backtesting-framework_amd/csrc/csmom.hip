@@ -1253,6 +1253,12 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
 #define TC_SYNC0 4       // sync words before the flags
 #define TC_SPINS (1u << 21)
 #define TC_NC 16         // chunk counts per load trip of the window search
+#ifndef TC_GW
+#define TC_GW 4          // chunks per load trip of the general fold walk
+#endif
+#ifndef TC_LBW
+#define TC_LBW 4         // launch bound: waves per SIMD the VGPR budget must allow
+#endif
 #ifndef TC_REC2
 #define TC_REC2 1        // the record's forward and backward fields by the two wave halves
 #endif
@@ -1328,16 +1334,16 @@ __device__ __forceinline__ void tc_fold_general(const double* cp, int64_t hs, in
   bool hasf = false, haslv = false, below = false;
   double lvlast = NaN, lvbelow = NaN;
   int lpm = -1, nv = 0, src_h = -1, src_j = -1;
-  for (int hb = g - 1; hb >= 0; hb -= 4) {   // one backward pass, four chunks per trip
-    double n4[4], f4[4], li4[4], lv4[4], lp4[4];
+  for (int hb = g - 1; hb >= 0; hb -= TC_GW) {   // one backward pass, TC_GW chunks per trip
+    double n4[TC_GW], f4[TC_GW], li4[TC_GW], lv4[TC_GW], lp4[TC_GW];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < TC_GW; ++u) {
       const int h = hb - u >= 0 ? hb - u : 0;
       n4[u] = at(h, 0); f4[u] = at(h, 1); li4[u] = at(h, 2); lv4[u] = at(h, 3);
       lp4[u] = at(h, SR - 1);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < TC_GW; ++u) {
       const int h = hb - u;
       if (h < 0) break;
       const int64_t n = (int64_t)n4[u];
@@ -1518,7 +1524,7 @@ __device__ __forceinline__ bool tc_fold_fast(const double* cp, int64_t hs, int g
 }
 
 template <int WR, int JC = 0>
-__global__ __launch_bounds__(TC_THREADS, 4) void k_signal_tc(
+__global__ __launch_bounds__(TC_THREADS, TC_LBW) void k_signal_tc(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, int G, int nbx, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, uint16_t* __restrict__ IDS, double* __restrict__ rec,
