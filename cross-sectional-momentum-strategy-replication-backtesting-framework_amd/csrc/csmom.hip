@@ -1816,36 +1816,23 @@ __device__ __forceinline__ void shard_pm_chunk(const double* __restrict__ PM,
 // idx (the halo pass's fallback columns): output column j < ncol is asset idx[j] (record rows
 // ncol apart); columns past the list's length *cnt get the record of an asset with no present
 // month (a neutral column for k_fold_carry).
-__global__ __launch_bounds__(256) void k_shard_summary_state(const double* __restrict__ PM,
-                                                             const double* __restrict__ P,
-                                                             const int64_t* __restrict__ ms,
-                                                             int T_m, int64_t N, int T,
-                                                             const double* __restrict__ st,
-                                                             double* __restrict__ out,
-                                                             const int32_t* __restrict__ idx,
-                                                             const int32_t* __restrict__ cnt,
-                                                             int64_t ncol) {
-  const int W = T - 1;
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= (idx ? ncol : N)) return;
-  const int64_t os = idx ? ncol : N;   // output row stride
-  out += j;
-  const bool listed = !idx || j < (int64_t)*cnt;
-  const int64_t a = idx ? (listed ? (int64_t)idx[j] : 0) : j;
-  const int64_t n = listed ? (int64_t)st[a] : 0;
-  const int fm = listed ? (int)st[3 * N + a] : -1, lm = listed ? (int)st[4 * N + a] : -1;
+// The record body over a month source: chunk(m0, dm, lo, hi, buf) fills WALK_CHUNK month
+// prices (ABSENT outside [lo, hi]) and one(m) gives one month's price.
+template <class Chunk, class One>
+__device__ __forceinline__ void shard_summary_body(Chunk chunk, One one, int64_t n, int fm, int lm,
+                                                   int T, int64_t os, double* __restrict__ out) {
   int64_t fv = -1, lvi = -1;
   double lv = qnan(), head = qnan(), first = absent_val();
   const int k = (int)(n < T ? n : T);
   for (int q = 0; q < T - k; ++q) out[(int64_t)(SUM_SCALARS + q) * os] = absent_val();
   if (n > 0) {
     // forward from the first present month: first price, index of the first valid row
-    first = shard_pm_at(PM, P, ms, fm, T_m, W, N, a);
+    first = one(fm);
     int64_t ix = 0;
     bool found = false;
     for (int m0 = fm; m0 <= lm && !found; m0 += WALK_CHUNK) {
       double buf[WALK_CHUNK];
-      shard_pm_chunk(PM, P, ms, m0, 1, fm, lm, T_m, W, N, a, buf);
+      chunk(m0, 1, fm, lm, buf);
 #pragma unroll
       for (int q = 0; q < WALK_CHUNK; ++q) {
         const double x = buf[q];
@@ -1860,7 +1847,7 @@ __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __res
     bool have_lv = false, done = false;
     for (int m0 = lm; m0 >= fm && !done; m0 -= WALK_CHUNK) {
       double buf[WALK_CHUNK];
-      shard_pm_chunk(PM, P, ms, m0, -1, fm, lm, T_m, W, N, a, buf);
+      chunk(m0, -1, fm, lm, buf);
 #pragma unroll
       for (int q = 0; q < WALK_CHUNK; ++q) {
         const double x = buf[q];
@@ -1884,6 +1871,66 @@ __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __res
   out[3 * os] = lv;
   out[4 * os] = head;
   out[5 * os] = first;
+}
+
+// Same record as k_shard_summary (n, fv, lvi, lv, head, first; tail of the last T present
+// month prices, ABSENT-padded at the front) from the SH state's n / first / last month.
+// idx (the halo pass's fallback columns): output column j < ncol is asset idx[j] (record rows
+// ncol apart); columns past the list's length *cnt get the record of an asset with no present
+// month (a neutral column for k_fold_carry).
+__global__ __launch_bounds__(256) void k_shard_summary_state(const double* __restrict__ PM,
+                                                             const double* __restrict__ P,
+                                                             const int64_t* __restrict__ ms,
+                                                             int T_m, int64_t N, int T,
+                                                             const double* __restrict__ st,
+                                                             double* __restrict__ out,
+                                                             const int32_t* __restrict__ idx,
+                                                             const int32_t* __restrict__ cnt,
+                                                             int64_t ncol) {
+  const int W = T - 1;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (idx ? ncol : N)) return;
+  const int64_t os = idx ? ncol : N;   // output row stride
+  const bool listed = !idx || j < (int64_t)*cnt;
+  const int64_t a = idx ? (listed ? (int64_t)idx[j] : 0) : j;
+  const int64_t n = listed ? (int64_t)st[a] : 0;
+  const int fm = listed ? (int)st[3 * N + a] : -1, lm = listed ? (int)st[4 * N + a] : -1;
+  shard_summary_body(
+      [&](int m0, int dm, int lo, int hi, double (&buf)[WALK_CHUNK]) {
+        shard_pm_chunk(PM, P, ms, m0, dm, lo, hi, T_m, W, N, a, buf);
+      },
+      [&](int m) { return shard_pm_at(PM, P, ms, m, T_m, W, N, a); }, n, fm, lm, T, os, out + j);
+}
+
+// The listed columns of the halo pass, ONE WORKGROUP PER COLUMN (grid ncol, COLS_THREADS): its
+// threads derive the column's T_m month prices together (PM where kept, else the month-end of
+// the daily rows: one round trip for all months instead of one per re-derived month), into
+// LDS; one lane then builds the record from LDS exactly as k_shard_summary_state does.
+#define COLS_THREADS 64
+__global__ __launch_bounds__(COLS_THREADS) void k_shard_summary_cols(
+    const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
+    int T_m, int64_t N, int T, const double* __restrict__ st, double* __restrict__ out,
+    const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int64_t ncol) {
+  extern __shared__ __attribute__((aligned(16))) double pmc[];   // [T_m]
+  const int W = T - 1;
+  const int64_t j = blockIdx.x;
+  const bool listed = j < (int64_t)*cnt;   // (workgroup-uniform)
+  const int64_t a = listed ? (int64_t)idx[j] : 0;
+  if (listed)
+    for (int m = threadIdx.x; m < T_m; m += COLS_THREADS) pmc[m] = shard_pm_at(PM, P, ms, m, T_m, W, N, a);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const int64_t n = listed ? (int64_t)st[a] : 0;
+  const int fm = listed ? (int)st[3 * N + a] : -1, lm = listed ? (int)st[4 * N + a] : -1;
+  shard_summary_body(
+      [&](int m0, int dm, int lo, int hi, double (&buf)[WALK_CHUNK]) {
+#pragma unroll
+        for (int q = 0; q < WALK_CHUNK; ++q) {
+          const int m = m0 + q * dm;
+          buf[q] = (m >= lo && m <= hi) ? pmc[m] : absent_val();
+        }
+      },
+      [&](int m) { return pmc[m]; }, n, fm, lm, T, ncol, out + j);
 }
 
 // F's step: scan_step without outputs (the state transition only).
@@ -1918,22 +1965,16 @@ __device__ __forceinline__ bool same_bits(double x, double y) {
 // fcarry: F's initial state (the halo pass's carry, [W+2][N]); NULL = empty (the speculative
 // pass).  idx (the halo pass's fallback columns): thread j repairs asset idx[j] for j < *cnt,
 // with carry / next_pm column j (rows ncol apart); NULL = every asset, carry / next_pm [.][N].
-__global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
-    const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
-    int T_m, int64_t N, int J, int skip,
-    const double* __restrict__ carry, const double* __restrict__ next_pm,
-    const double* __restrict__ st, double* __restrict__ R, double* __restrict__ M,
-    double* __restrict__ NR, uint16_t* __restrict__ IDS, const double* __restrict__ fcarry,
-    const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int64_t ncol) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][W][REPAIR_THREADS]
-  const int W = J + skip, RS = REPAIR_THREADS;
-  const int tid = threadIdx.x;
-  const int64_t j = (int64_t)blockIdx.x * REPAIR_THREADS + tid;
-  if (idx ? (j >= ncol || j >= (int64_t)*cnt) : j >= N) return;  // no barriers below
-  const int64_t a = idx ? (int64_t)idx[j] : j;
-  const int64_t cs = idx ? ncol : N, cj = idx ? j : a;   // carry / next_pm stride and column
-  double* rt = lds + tid;
-  double* rf = lds + W * RS + tid;
+// The repair body for asset a over a month source chunk(m0, buf) (REPAIR_CHUNK months from m0,
+// ABSENT past T_m - 1); rt / rf: T's and F's rings (stride RS).
+template <class Chunk>
+__device__ __forceinline__ void shard_repair_body(
+    Chunk chunk, int T_m, int64_t N, int J, int skip, const double* __restrict__ carry,
+    const double* __restrict__ next_pm, const double* __restrict__ st, double* __restrict__ R,
+    double* __restrict__ M, double* __restrict__ NR, uint16_t* __restrict__ IDS,
+    const double* __restrict__ fcarry, int64_t a, int64_t cs, int64_t cj, double* rt,
+    double* rf, int RS) {
+  const int W = J + skip;
   ScanLane t, f;
   scan_init(t, rt, RS, W, carry, cs, cj, true);
   scan_init(f, rf, RS, W, fcarry, N, a, true);
@@ -1951,7 +1992,7 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
   static_assert(REPAIR_CHUNK == WALK_CHUNK, "the repair walks months in shard_pm_chunk's batches");
   for (int m0 = fm < 0 ? 0 : fm; m0 < T_m && !done; m0 += REPAIR_CHUNK) {
     double buf[REPAIR_CHUNK];
-    shard_pm_chunk(PM, P, ms, m0, 1, 0, T_m - 1, T_m, W, N, a, buf);
+    chunk(m0, buf);
 #pragma unroll
     for (int q = 0; q < REPAIR_CHUNK; ++q) {
       const int m = m0 + q;
@@ -1977,6 +2018,55 @@ __global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
     }
     NR[(int64_t)prev * N + a] = nr;
   }
+}
+
+__global__ __launch_bounds__(REPAIR_THREADS) void k_shard_repair(
+    const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
+    int T_m, int64_t N, int J, int skip,
+    const double* __restrict__ carry, const double* __restrict__ next_pm,
+    const double* __restrict__ st, double* __restrict__ R, double* __restrict__ M,
+    double* __restrict__ NR, uint16_t* __restrict__ IDS, const double* __restrict__ fcarry,
+    const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int64_t ncol) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][W][REPAIR_THREADS]
+  const int W = J + skip, RS = REPAIR_THREADS;
+  const int tid = threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * REPAIR_THREADS + tid;
+  if (idx ? (j >= ncol || j >= (int64_t)*cnt) : j >= N) return;  // no barriers below
+  const int64_t a = idx ? (int64_t)idx[j] : j;
+  const int64_t cs = idx ? ncol : N, cj = idx ? j : a;   // carry / next_pm stride and column
+  shard_repair_body(
+      [&](int m0, double (&buf)[REPAIR_CHUNK]) {
+        shard_pm_chunk(PM, P, ms, m0, 1, 0, T_m - 1, T_m, W, N, a, buf);
+      },
+      T_m, N, J, skip, carry, next_pm, st, R, M, NR, IDS, fcarry, a, cs, cj, lds + tid,
+      lds + W * RS + tid, RS);
+}
+
+// The listed columns of the halo pass, one workgroup per column (k_shard_summary_cols' month
+// prices into LDS by all its threads, then one lane repairs from them; rings in LDS too).
+__global__ __launch_bounds__(COLS_THREADS) void k_shard_repair_cols(
+    const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
+    int T_m, int64_t N, int J, int skip,
+    const double* __restrict__ carry, const double* __restrict__ next_pm,
+    const double* __restrict__ st, double* __restrict__ R, double* __restrict__ M,
+    double* __restrict__ NR, uint16_t* __restrict__ IDS, const double* __restrict__ fcarry,
+    const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int64_t ncol) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // pm [T_m], rings [2][W]
+  const int W = J + skip;
+  const int64_t j = blockIdx.x;
+  if (j >= (int64_t)*cnt) return;   // (workgroup-uniform: before the barrier)
+  const int64_t a = (int64_t)idx[j];
+  double* pmc = lds;
+  for (int m = threadIdx.x; m < T_m; m += COLS_THREADS) pmc[m] = shard_pm_at(PM, P, ms, m, T_m, W, N, a);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  shard_repair_body(
+      [&](int m0, double (&buf)[REPAIR_CHUNK]) {
+#pragma unroll
+        for (int q = 0; q < REPAIR_CHUNK; ++q) buf[q] = m0 + q < T_m ? pmc[m0 + q] : absent_val();
+      },
+      T_m, N, J, skip, carry, next_pm, st, R, M, NR, IDS, fcarry, a, ncol, j, lds + T_m,
+      lds + T_m + W, 1);
 }
 
 // =====================================================================================
@@ -2176,6 +2266,7 @@ __global__ __launch_bounds__(UNION_THREADS) void k_shard_union(const uint64_t* _
 static int g_tune_signal_vec = 2;      // k_signal assets per lane: 2 (paired 16-B rows) | 1 (odd N)
 static int g_tune_signal_bwf = 0;      // k_signal blocks: 0 auto | 1 one wave | 4 four barrier-free waves x 2 month buffers (buffer loads)
 static int g_tune_signal_j12 = 1;      // wide shard k_signal: J = 12 with its product length fixed at compile time (0: runtime J)
+static int g_tune_cols_wg = 1;          // halo pass's listed columns: one workgroup per column (month prices into LDS) | 0 one thread per column
 #define SIGNAL_BWF_MIN_N (180 * 512)   // auto: 4-wave blocks once the grid still covers >= 180 CUs
 static int64_t* g_dec_timing = nullptr;
 // PRE decile pass (csm_deciles_ids): 1 the merged sweep, then the general kernel for the rows it
@@ -2209,6 +2300,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "signal_vec") && (value == 1 || value == 2)) { g_tune_signal_vec = value; return CSM_OK; }
   if (!strcmp(key, "signal_bwf") && (value == 0 || value == 1 || value == 4)) { g_tune_signal_bwf = value; return CSM_OK; }
   if (!strcmp(key, "signal_j12") && (value == 0 || value == 1)) { g_tune_signal_j12 = value; return CSM_OK; }
+  if (!strcmp(key, "cols_wg") && (value == 0 || value == 1)) { g_tune_cols_wg = value; return CSM_OK; }
   if (!strcmp(key, "dec_merge") && (value == 0 || value == 1)) { g_tune_dec_merge = value; return CSM_OK; }
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
@@ -2964,6 +3056,14 @@ int csm_shard_summary_cols(csm_ctx* ctx, const double* P, const int64_t* month_s
   if (!P || !month_start || !PM || !state || !idx || !count || !out || N <= 0 || T_m < 1 ||
       cap < 1 || J < 1 || skip < 0 || J + skip > 256)
     return set_err(ctx, CSM_E_INVAL, "csm_shard_summary_cols: bad arguments");
+  // one workgroup per listed column, its month prices derived together into LDS
+  if (g_tune_cols_wg && (size_t)T_m * sizeof(double) <= 65536 && cap <= 0x7FFFFFFF) {
+    hipLaunchKernelGGL(k_shard_summary_cols, dim3((unsigned)cap), dim3(COLS_THREADS),
+                       (size_t)T_m * sizeof(double), ctx->stream, PM, P, month_start, T_m, N,
+                       J + skip + 1, state, out, idx, count, cap);
+    LAUNCH_CHECK(ctx, "k_shard_summary_cols");
+    return CSM_OK;
+  }
   hipLaunchKernelGGL(k_shard_summary_state, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0,
                      ctx->stream, PM, P, month_start, T_m, N, J + skip + 1, state, out, idx,
                      count, cap);
@@ -2982,6 +3082,14 @@ int csm_shard_repair_cols(csm_ctx* ctx, const double* P, const int64_t* month_st
       !M || !NR || N <= 0 || T_m < 1 || cap < 1 || J < 1 || skip < 0 || J + skip > 128)
     return set_err(ctx, CSM_E_INVAL, "csm_shard_repair_cols: bad arguments (J + skip <= 128)");
   const int W = J + skip;
+  const size_t ldsc = (size_t)(T_m + 2 * W) * sizeof(double);
+  if (g_tune_cols_wg && ldsc <= 65536 && cap <= 0x7FFFFFFF) {
+    hipLaunchKernelGGL(k_shard_repair_cols, dim3((unsigned)cap), dim3(COLS_THREADS), ldsc,
+                       ctx->stream, PM, P, month_start, T_m, N, J, skip, carry, next_pm, state,
+                       R, M, NR, ids, fcarry, idx, count, cap);
+    LAUNCH_CHECK(ctx, "k_shard_repair_cols");
+    return CSM_OK;
+  }
   const size_t lds = (size_t)2 * W * REPAIR_THREADS * sizeof(double);
   if (lds > 65536)
     HIP_CHECK(ctx, hipFuncSetAttribute((const void*)k_shard_repair,

@@ -44,7 +44,9 @@ int csm_abi_version(void);
  * drive the fallbacks on inputs that would not reach them): "signal_vec" (2 paired 16-B rows |
  * 1 one asset per lane, the odd-N path), "signal_bwf" (0 auto | 1 one-wave blocks | 4 the wide
  * panels' four barrier-free waves with buffer loads), "signal_j12" (1 the wide date-shard kernel's
- * J = 12 with the product length fixed at compile time | 0 runtime J), "dec_merge" (1 the merged decile sweep on
+ * J = 12 with the product length fixed at compile time | 0 runtime J), "cols_wg" (1 the halo pass's listed
+ * columns summarised / repaired one workgroup per column, month prices derived together in LDS |
+ * 0 one thread per column), "dec_merge" (1 the merged decile sweep on
  * ids, the general kernel for the rows it leaves | 0 the general kernel only), "dec_split" (2
  * auto: wide rows on ids take the split pass -- plan, chunked sweep, finish -- in launches of
  * fewer rows than half the CUs (short date shards) | 1 always | 0 the merged pass with one

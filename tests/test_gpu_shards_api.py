@@ -367,17 +367,26 @@ def test_halo_shards_long_windows(engine, J, skip, G):
 
 @pytest.mark.parametrize("G", [2, 7])
 @pytest.mark.parametrize("H", [None, 0, 2])
-def test_halo_shards_sparse_panel(engine, G, H):
+@pytest.mark.parametrize("cols_wg", [1, 0])
+def test_halo_shards_sparse_panel(engine, G, H, cols_wg):
     """Gappy panel (25 % absent months, 15 % NaN months): most assets are flagged and go
     through the exchange; H = 0 (no halo at all) and H = 2 (shorter than the window) flag
-    every asset with history -- still bit for bit."""
+    every asset with history -- still bit for bit.  The listed columns' summary and repair one
+    workgroup per column (month prices derived together into LDS; the default) and one thread
+    per column (tune cols_wg 0)."""
     from oracle.synth_np import make_panel
     from csmom.distributed import virtual_shards_halo
     pan = make_panel(512, 2600, seed=11, nan_day=0.05, absent_month=0.25, nan_month=0.15,
                      cents=True)
     P, ms = _up(pan["P"]), pan["month_start"].astype(np.int64)
     out = engine.run(P, _up(ms), 12, 1, 10, with_ret=True)
-    cnt = _halo_equal(out, virtual_shards_halo(engine, P, ms, G, 12, 1, 10, H=H), ew=False)
+    lib = engine.lib
+    try:
+        assert lib.csm_tune(b"cols_wg", cols_wg) == 0
+        res = virtual_shards_halo(engine, P, ms, G, 12, 1, 10, H=H)
+    finally:
+        lib.csm_tune(b"cols_wg", 1)
+    cnt = _halo_equal(out, res, ew=False)
     assert cnt > 0
 
 
