@@ -423,7 +423,7 @@ def main(argv=None):
             eng.signal(panel.P, panel.month_start, max_days, J, skip, out=(None, None, M, NR))
         elif tc:
             eng.signal_chunked(panel.P, panel.month_start, max_days, J, skip, chunks=chunks,
-                               out=(None, M, NR, IDS), workspace=tc_ws)
+                               out=(None, M, NR, IDS), workspace=tc_ws, check=False)
         else:
             eng.month_end(panel.P, panel.month_start, PM=PM)
             i += 1
@@ -482,6 +482,13 @@ def main(argv=None):
             step(step_events[k])
         torch.cuda.synchronize()
     elapsed = allreduce_host([elapsed], dist.ReduceOp.MAX if world > 1 else None, dev)[0]
+    if tc_ws is not None and hasattr(eng.lib, "csm_signal_chunked_status"):   # (A/B base builds)
+        # k_signal_tc's in-launch hand-off: a workgroup that gave up a wait marks the workspace;
+        # any mark left by the timed (or staging) launches invalidates the line
+        try:
+            eng.signal_chunked_status(tc_ws)
+        except Exception as e:
+            raise SystemExit(f"C2 signal: {e}; the timed passes are invalid, no line printed")
 
     if world == 1:
         for ev in step_events:

@@ -36,6 +36,11 @@ struct csm_ctx {
   size_t dsplit_bytes;
   void* comm;             // RCCL communicator of csm_allgather_init (collective.hip), or NULL
   int comm_rank, comm_size;
+  // portfolio workspaces whose last cohort pass wrote the leg bitplanes (portfolio.hip): the
+  // turnover pass reads bitplanes only from a workspace recorded here, whatever the tune knobs
+  // say by then (a knob changed between the two calls falls back to the label bytes)
+  void* planes_ws[32];
+  int planes_next;
 };
 
 static inline int set_err(csm_ctx* c, int code, const char* fmt, ...) {
@@ -134,10 +139,14 @@ __device__ __forceinline__ uint32_t csm_fid(double x) {
 }
 
 // The split decile pass on ids (deciles.inc, wide rows): device workspace of the plan / sweep /
-// finish launches, carved from the context's split buffer (csmom.hip dsplit_layout).
-#define SPLIT_CELLS 16384   // default cells per sweep chunk (csm_tune "dec_split_cells"; the
+// finish launches, carved from the context's split buffer (csmom.hip dsplit_layout).  A chunk is
+// a whole number of the merged pass's sweep trips (SPLIT_TRIP cells: 512 lanes x 4 groups x 4
+// cells), and a sweep workgroup's lane owns the cells the merged pass's lane of that index owns
+// there, so both passes sum next_ret in the same order (deciles.inc DEC_CHUNK_ORDER).
+#define SPLIT_CELLS 32768   // default cells per sweep chunk (csm_tune "dec_split_cells"; the
                             // chunking depends on N and that knob only, never on the launch)
-#define SPLIT_THREADS 256
+#define SPLIT_TRIP 8192     // cells of one merged-sweep trip: chunks are multiples of it
+#define SPLIT_THREADS 512
 #define SPLIT_WAVES (SPLIT_THREADS / 64)
 #define SPLIT_FL 1024       // uncertain cells a sweep wave can list per chunk
 #define DSPLAN_BYTES 4096   // one row's DsPlan
@@ -145,13 +154,13 @@ __device__ __forceinline__ uint32_t csm_fid(double x) {
 struct DecSplit {
   char* plan;        // [T_m] DsPlan (slots, targets, ranked count)
   int8_t* tab;       // [T_m][8192] bucket -> label (-1 NaN, >= 0 certain, <= -2 uncertain)
-  double* ph;        // [T_m][C][NB] the certain cells' next_ret sums per label (two-sum high,
-  double* pl;        //   low) and counts, per chunk
-  int32_t* pc;
+  double* lp;        // [T_m][C][MAXQ - 1][SPLIT_THREADS] each lane's certain-cell next_ret sum
+                     //   per label, per chunk (the merged pass's per-lane chunk partials)
+  int32_t* pc;       // [T_m][C][MAXQ] certain-cell counts per label, per chunk
   int32_t* ucnt;     // [T_m][C][SPLIT_WAVES] uncertain cells listed per (chunk, wave)
   uint32_t* ulist;   // [T_m][C][SPLIT_WAVES][SPLIT_FL] their cell indices
   int C;             // chunks per row: ceil(N / cells)
-  int64_t cells;     // cells per chunk (a multiple of 4 * SPLIT_THREADS)
+  int64_t cells;     // cells per chunk (a multiple of SPLIT_TRIP)
 };
 
 // narrow-row decile launcher (deciles_narrow.hip), NB in {0,2,3,4,5,10,20}
@@ -168,7 +177,7 @@ template <int NB>
 void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
                         int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg, double* LS,
-                        int32_t* ticket);
+                        int32_t* ticket, int64_t cells);
 
 // the split pass (plan, chunked sweep, finish + the general path for the rows it leaves) on
 // wide rows of short date shards; flg (T_m ints) required

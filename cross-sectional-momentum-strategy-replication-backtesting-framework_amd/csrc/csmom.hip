@@ -1528,7 +1528,7 @@ __global__ __launch_bounds__(TC_THREADS, TC_LBW) void k_signal_tc(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, int G, int nbx, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, uint16_t* __restrict__ IDS, double* __restrict__ rec,
-    unsigned* __restrict__ sync) {
+    unsigned* __restrict__ sync, unsigned spin_limit) {
   extern __shared__ __attribute__((aligned(16))) double tc_lds[];   // ring [T][256], pm [C][256]
   __shared__ int s_t, s_last;
   const int tid = threadIdx.x;
@@ -1651,6 +1651,14 @@ __global__ __launch_bounds__(TC_THREADS, TC_LBW) void k_signal_tc(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
   __syncthreads();
+  // Publication.  Every record word is itself an agent-scope atomic store (tc_put: written
+  // through to the agent coherence point, never left dirty in this XCD's L2), and every storing
+  // wave has waited for its stores to complete (vmcnt(0)) before the barrier, so the records are
+  // visible at agent scope before the flag is issued.  That is all a release would add for
+  // atomic stores on gfx950; an __ATOMIC_RELEASE store also emits buffer_wbl2 (an L2 write-back
+  // of every dirty line of the XCD, the other workgroups' M / NR among them): measured +3.5 us
+  // per C2 launch (k_signal_tc 76.5 -> 80.0 us, same box, round 6), so the flag stays relaxed.
+  // The consumer acquires (agent fence) after it sees every flag.
   if (tid == 0)
     __hip_atomic_store((tc_gu32*)(sync + TC_SYNC0 + (int64_t)g * nbx + x), 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1662,17 +1670,20 @@ __global__ __launch_bounds__(TC_THREADS, TC_LBW) void k_signal_tc(
       bool got = lane >= g;
       unsigned spins = 0;
       while (true) {
-        if (!got)
-          got = __hip_atomic_load((const tc_gu32*)(sync + TC_SYNC0 + (int64_t)lane * nbx + x),
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        if (__ballot(!got) == 0ull) break;   // (wave-uniform)
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > TC_SPINS) {   // never expected: give up, mark the launch
+        // never expected (spin_limit 0 forces it: the tests of the failure report): give up and
+        // mark the launch; csm_signal_chunked_status reports the mark as CSM_E_TIMEOUT
+        if (spins >= spin_limit) {
           if (lane == 0)
             __hip_atomic_store((tc_gu32*)(sync + 2), 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
+        if (!got)
+          got = __hip_atomic_load((const tc_gu32*)(sync + TC_SYNC0 + (int64_t)lane * nbx + x),
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        if (__ballot(!got) == 0ull) break;   // (wave-uniform)
+        __builtin_amdgcn_s_sleep(2);
+        ++spins;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2283,6 +2294,9 @@ static int64_t g_tune_dec_split_cells = SPLIT_CELLS;   // cells per split-sweep 
 static int g_tune_mj_reg = 2;
 // rows with at most this many assets take the narrow-row decile kernels
 static int64_t g_tune_dec_narrow_max = 16384;
+// k_signal_tc: polling trips a waiting workgroup makes before it gives up and marks the launch
+// (0: give up at once -- only the tests of the failure report set it)
+static unsigned g_tune_tc_spins = TC_SPINS;
 
 extern "C" {
 
@@ -2305,7 +2319,8 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
   if (!strcmp(key, "dec_split") && value >= 0 && value <= 2) { g_tune_dec_split = value; return CSM_OK; }
-  if (!strcmp(key, "dec_split_cells") && value >= 4 * SPLIT_THREADS && value % (4 * SPLIT_THREADS) == 0) {
+  if (!strcmp(key, "tc_spins") && value >= 0) { g_tune_tc_spins = (unsigned)value; return CSM_OK; }
+  if (!strcmp(key, "dec_split_cells") && value >= SPLIT_TRIP && value % SPLIT_TRIP == 0) {
     g_tune_dec_split_cells = value;
     return CSM_OK;
   }
@@ -2618,7 +2633,7 @@ static void launch_deciles(bool v2, int T_m, hipStream_t st, const double* M, co
                                     g_tune_dec_merge ? flg : nullptr, LS, ticket);
     else
       launch_deciles_pre<NB>(T_m, st, M, NR, N, nbins, q, L, EW, CNT, NV, tm, ids,
-                             g_tune_dec_merge ? flg : nullptr, LS, ticket);
+                             g_tune_dec_merge ? flg : nullptr, LS, ticket, g_tune_dec_split_cells);
     return;
   }
   if (N <= g_tune_dec_narrow_max) {   // rows of a few thousand assets (C2/C3/C5)
@@ -2685,16 +2700,14 @@ static size_t dsplit_layout(int32_t T_m, int64_t N, DecSplit* sp, char* base) {
   size_t o = 0;
   const size_t plan = o; o = al(o + (size_t)T_m * DSPLAN_BYTES);
   const size_t tab = o;  o = al(o + (size_t)T_m * CSM_FB_BUCKETS);
-  const size_t ph = o;   o = al(o + (size_t)T_m * C * MAXQ * 8);
-  const size_t pl = o;   o = al(o + (size_t)T_m * C * MAXQ * 8);
+  const size_t lp = o;   o = al(o + (size_t)T_m * C * (MAXQ - 1) * SPLIT_THREADS * 8);
   const size_t pc = o;   o = al(o + (size_t)T_m * C * MAXQ * 4);
   const size_t uc = o;   o = al(o + (size_t)T_m * C * SPLIT_WAVES * 4);
   const size_t ul = o;   o = al(o + (size_t)T_m * C * SPLIT_WAVES * SPLIT_FL * 4);
   if (sp) {
     sp->plan = base + plan;
     sp->tab = (int8_t*)(base + tab);
-    sp->ph = (double*)(base + ph);
-    sp->pl = (double*)(base + pl);
+    sp->lp = (double*)(base + lp);
     sp->pc = (int32_t*)(base + pc);
     sp->ucnt = (int32_t*)(base + uc);
     sp->ulist = (uint32_t*)(base + ul);
@@ -3279,17 +3292,40 @@ int csm_signal_chunked(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
   if (W == 13 && J == 12)
     hipLaunchKernelGGL((k_signal_tc<13, 12>), dim3((unsigned)(C * nbx)), dim3(TC_THREADS), lds,
                        ctx->stream, P, month_start, T_m, N, J, skip, C, nbx, R, M, NR, ids, rec,
-                       sync);
+                       sync, g_tune_tc_spins);
   else if (W == 13)
     hipLaunchKernelGGL(k_signal_tc<13>, dim3((unsigned)(C * nbx)), dim3(TC_THREADS), lds,
                        ctx->stream, P, month_start, T_m, N, J, skip, C, nbx, R, M, NR, ids, rec,
-                       sync);
+                       sync, g_tune_tc_spins);
   else
     hipLaunchKernelGGL(k_signal_tc<0>, dim3((unsigned)(C * nbx)), dim3(TC_THREADS), lds,
                        ctx->stream, P, month_start, T_m, N, J, skip, C, nbx, R, M, NR, ids, rec,
-                       sync);
+                       sync, g_tune_tc_spins);
   LAUNCH_CHECK(ctx, "k_signal_tc");
   return CSM_OK;
+}
+
+int csm_signal_chunked_status(csm_ctx* ctx, void* workspace) {
+  int r = prep(ctx);
+  if (r) return r;
+  if (!workspace || ((uintptr_t)workspace & 255u) != 0)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_chunked_status: null or unaligned workspace");
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_CHECK(ctx, hipStreamIsCapturing(ctx->stream, &cs));
+  if (cs != hipStreamCaptureStatusNone)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_chunked_status: the stream is capturing (read "
+                   "the status after the graph's replay)");
+  unsigned w = 0;
+  unsigned* word = (unsigned*)workspace + 2;
+  HIP_CHECK(ctx, hipMemcpyAsync(&w, word, sizeof(w), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (w == 0u) return CSM_OK;
+  // reported once: cleared for the workspace's next launch
+  HIP_CHECK(ctx, hipMemsetAsync(word, 0, sizeof(unsigned), ctx->stream));
+  HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return set_err(ctx, CSM_E_TIMEOUT, "csm_signal_chunked: a workgroup gave up waiting for an "
+                 "earlier chunk's record (in-launch hand-off); the M / NR / R / ids of the "
+                 "launches since the last status check are invalid");
 }
 
 }  // extern "C"

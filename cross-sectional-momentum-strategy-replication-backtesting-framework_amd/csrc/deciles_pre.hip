@@ -18,6 +18,7 @@
 #define HB DEC_PRE_HB
 #define CAP DEC_PRE_CAP
 #define DEC_LU 8
+#define DEC_CHUNK_ORDER 1   // merged pass summed in the split pass's order (deciles.inc)
 namespace dec_pre {
 #include "deciles.inc"
 }  // namespace dec_pre
@@ -26,16 +27,20 @@ template <int NB>
 void launch_deciles_pre(int T_m, hipStream_t st, const double* M, const double* NR, int64_t N,
                         int nbins, const QTab& q, int8_t* L, double* EW, int32_t* CNT,
                         int32_t* NV, int64_t* tim, uint16_t* ids, int32_t* flg, double* LS,
-                        int32_t* ticket) {
+                        int32_t* ticket, int64_t cells) {
   // merged pass first (flg): one sweep of ids + next_ret per row (deciles.inc, MG); then the
   // general kernel takes the rows it left (all rows without flg) -- and, LS given, its last
   // workgroup forms the long-short (csmom.hip launches k_long_short instead for these rows).
   // (The merged pass with the general path as an in-workgroup fallback needs more than the 128
   // VGPRs of two 512-thread workgroups per CU at this width.)
-  if (flg)
+  // (the merged pass sums in the split pass's order: its chunks of `cells` cells)
+  if (flg) {
+    DecSplit sp{};
+    sp.cells = cells;
     hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, true>), dim3(T_m),
                        dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
-                       ids, flg, (double*)nullptr, (int32_t*)nullptr);
+                       ids, flg, (double*)nullptr, (int32_t*)nullptr, sp);
+  }
   hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, false>), dim3(T_m),
                      dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim,
                      ids, flg, LS, ticket);
@@ -67,7 +72,7 @@ void launch_deciles_split(int T_m, hipStream_t st, const double* M, const double
                                          const DecSplit&, double*, int32_t*);                 \
   template void launch_deciles_pre<NB>(int, hipStream_t, const double*, const double*, int64_t, \
                                        int, const QTab&, int8_t*, double*, int32_t*, int32_t*,  \
-                                       int64_t*, uint16_t*, int32_t*, double*, int32_t*);
+                                       int64_t*, uint16_t*, int32_t*, double*, int32_t*, int64_t);
 INST(0)
 INST(2)
 INST(3)

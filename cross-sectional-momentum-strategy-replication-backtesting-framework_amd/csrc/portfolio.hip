@@ -2126,6 +2126,9 @@ int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bin
   return pf_layout(T_m, B, N, n_bins, K).bytes;
 }
 
+static bool legs_masks(const PfLayout& lay, bool legs, int64_t N, int Kmax, int n_bins);
+static void planes_note(csm_ctx* ctx, void* ws, bool wrote);
+
 static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,
                        int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
                        void* workspace, bool legs, const PanAddr& pa) {
@@ -2147,6 +2150,7 @@ static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const do
       return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: n_bins=%d unsupported (2,3,4,5,10,20,30)", n_bins);
   }
   LAUNCH_CHECK(ctx, "k_cohort");
+  planes_note(ctx, workspace, !W && legs_masks(lay, legs, N, Kmax, n_bins));
   if (lay.p.C > 1) {
     hipLaunchKernelGGL(k_fw_fold, dim3((unsigned)((2 * lay.rows + 255) / 256)), dim3(256), 0, st,
                        (const double*)(ws + lay.fw), lay.rows, lay.p.C, ws + lay.fwt);
@@ -2200,6 +2204,7 @@ int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const d
 #undef PJ_CASE
   }
   LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret)");
+  for (int q = 0; q < nJ; ++q) planes_note(ctx, ws[q], legs_masks(lay, legs != 0, N, Kmax, n_bins));
   // (the shared path has one cohort chunk: each J's partials are its folded totals)
   return CSM_OK;
 }
@@ -2233,6 +2238,7 @@ int csm_cohort_sums_js_grouped(csm_ctx* ctx, int32_t nJ, const int8_t* L, const 
 #undef PJ_CASE
   }
   LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret, grouped)");
+  planes_note(ctx, workspace, legs_masks(lay, legs != 0, N, Kmax, n_bins));
   return CSM_OK;
 }
 
@@ -2258,6 +2264,25 @@ static bool legs_masks(const PfLayout& lay, bool legs, int64_t N, int Kmax, int 
   return g_tune_turn_mask && legs && (N & 3) == 0 && lay.seg && g_tune_cohort_seg &&
          !lay.p.kpar && (int64_t)Kmax * (n_bins + 1) <= SEG_MAXKD &&
          (lay.p.Ct == 1 || lay.p.CHt % 256 == 0);
+}
+
+// The cohort pass records, per workspace, whether it wrote the leg bitplanes (the
+// turnover pass must not infer it from knobs that may have changed in between)
+static void planes_note(csm_ctx* ctx, void* ws, bool wrote) {
+  int hit = -1;
+  for (int i = 0; i < 32; ++i)
+    if (ctx->planes_ws[i] == ws) { hit = i; break; }
+  if (wrote && hit < 0) {
+    ctx->planes_ws[ctx->planes_next] = ws;
+    ctx->planes_next = (ctx->planes_next + 1) % 32;
+  } else if (!wrote && hit >= 0) {
+    ctx->planes_ws[hit] = nullptr;
+  }
+}
+static bool planes_have(const csm_ctx* ctx, const void* ws) {
+  for (int i = 0; i < 32; ++i)
+    if (ws && ctx->planes_ws[i] == ws) return true;
+  return false;
 }
 
 static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W,
@@ -2331,7 +2356,8 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
         }
         // equal-weight legs after the legs label sort: the steady rows' member counts from the
         // leg bitplanes it wrote (k_turnover_ew_mask), not from label bytes
-        if (!gen && !W && !imp && legs_masks(lay, legs, N, Kmax, n_bins)) {
+        if (!gen && !W && !imp && legs_masks(lay, legs, N, Kmax, n_bins) &&
+            planes_have(ctx, workspace)) {
           hipLaunchKernelGGL(k_turnover_ew_mask, dim3((unsigned)((nblk + TM_WAVES - 1) / TM_WAVES)),
                              dim3(64 * TM_WAVES), 0, st,
                              (const uint64_t*)((char*)workspace + lay.lm_b), lay.nwm, T_m, B, N, ks,

@@ -279,12 +279,16 @@ class Engine:
         return int(min(max(c, -(-T_m // 32)), 64))
 
     def signal_chunked(self, P, month_start, max_month_days, J=12, skip=1, chunks=None,
-                       with_ret=False, with_ids=True, out=None, workspace=None):
+                       with_ret=False, with_ids=True, out=None, workspace=None, check=True):
         """csm_signal_chunked: month-end + time-chunked scan in one launch (narrow panels, C2):
         the same R / M / NR / ids bits as month_end -> momentum_chunked(_ids).  Even N, months
         of <= 23 day rows.  workspace: a zero-filled uint8 buffer of
         csm_signal_chunked_workspace bytes (kept by the caller across calls: each launch leaves
-        its sync words zero).  Returns (R, M, NR, IDS, workspace)."""
+        its sync words zero).  check (default): unless the stream is capturing, read the
+        launch's give-up mark (csm_signal_chunked_status; synchronises) and raise CsmError
+        (CSM_E_TIMEOUT) if a workgroup gave up a wait.  check=False (timed loops, graph capture):
+        the caller calls signal_chunked_status(workspace) itself afterwards.
+        Returns (R, M, NR, IDS, workspace)."""
         T_d, N = P.shape
         T_m = month_start.numel() - 1
         _need(P, "P", torch.float64, (T_d, N), self.device)
@@ -303,15 +307,27 @@ class Engine:
         nbytes = int(self.lib.csm_signal_chunked_workspace(T_m, N, int(J), int(skip), C))
         if workspace is None or workspace.numel() * workspace.element_size() < nbytes:
             workspace = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+        if R is not None:
+            _need(R, "R", torch.float64, (T_m, N), self.device)
+        _need(M, "M", torch.float64, (T_m, N), self.device)
+        _need(NR, "NR", torch.float64, (T_m, N), self.device)
         self._call("csm_signal_chunked", _ptr(P), T_d, N, _ptr(month_start), T_m,
                    int(max_month_days), int(J), int(skip), C, _ptr(R), _ptr(M), _ptr(NR),
                    _ptr(IDS), _ptr(workspace))
+        if check and not torch.cuda.is_current_stream_capturing():
+            self.signal_chunked_status(workspace)
         return R, M, NR, IDS, workspace
+
+    def signal_chunked_status(self, workspace):
+        """csm_signal_chunked_status: synchronise, raise CsmError (CSM_E_TIMEOUT) if a
+        csm_signal_chunked launch on this workspace gave up a wait since the last check (its
+        outputs are invalid; the mark is cleared)."""
+        self._call("csm_signal_chunked_status", _ptr(workspace))
 
     @staticmethod
     def signal_chunked_timed_out(workspace):
-        """Whether a csm_signal_chunked launch on this workspace gave up a wait (sync word 2;
-        never set by a correct launch).  Synchronises."""
+        """Whether the workspace holds an unreported give-up mark (sync word 2; never set by a
+        correct launch).  Synchronises; does not clear it."""
         return bool(workspace[8:12].view(torch.int32).item() != 0)
 
     def signal(self, P, month_start, max_month_days, J=12, skip=1, with_pm=False,

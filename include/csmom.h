@@ -34,6 +34,7 @@ extern "C" {
 #define CSM_E_INVAL (-1)   /* bad argument (null pointer, size, unsupported parameter) */
 #define CSM_E_HIP (-2)     /* HIP runtime / launch failure */
 #define CSM_E_RCCL (-3)    /* RCCL missing or a collective failed */
+#define CSM_E_TIMEOUT (-4) /* an in-launch hand-off gave up a wait: that launch's outputs are invalid */
 #define CSM_UNIQUE_ID_BYTES 128
 
 typedef struct csm_ctx csm_ctx;
@@ -50,7 +51,7 @@ int csm_abi_version(void);
  * ids, the general kernel for the rows it leaves | 0 the general kernel only), "dec_split" (2
  * auto: wide rows on ids take the split pass -- plan, chunked sweep, finish -- in launches of
  * fewer rows than half the CUs (short date shards) | 1 always | 0 the merged pass with one
- * workgroup per row; same labels and counts, means in another fixed order), "mj_reg"
+ * workgroup per row; the same labels, counts and means bit for bit), "mj_reg"
  * (csm_momentum_multi: 2 register ring, two assets per lane | 1 one asset | 0 the LDS ring),
  * "dec_narrow_max" (widest row for the narrow-row decile kernels), "cohort_seg" / "cohort_lds"
  * (portfolio cohort-sum kernel: label-sorted segments (rows <= 7168) | per-wave LDS sums |
@@ -64,8 +65,11 @@ int csm_abi_version(void);
  * rows by one workgroup per weight panel | 0 one per row), "turn_mask" (1 steady equal-weight
  * legs turnover rows counted from the legs label sort's leg bitplanes | 0 from the label
  * bytes), "ls_opt" (1 the one-wave legs label sort's prefix ranks by v_mbcnt | 0 masked
- * popcounts), "dec_split_cells" (cells per chunk of the split decile sweep, default 16384, a
- * multiple of 1024; the split workspace is the context's).
+ * popcounts), "dec_split_cells" (cells per chunk of the split decile sweep, default 32768, a
+ * multiple of 8192 -- the merged pass's sweep trip -- so the merged and split passes sum every
+ * row's decile means in the same order; the split workspace is the context's), "tc_spins" (polling trips a
+ * csm_signal_chunked workgroup makes before it gives up a wait, default 2^21; 0 gives up at
+ * once, which only the tests of the CSM_E_TIMEOUT report set).
  * Returns CSM_E_INVAL for an unknown key or value. */
 int csm_tune(const char* key, int value);
 /* Profiling aids: "dec_timing" = device int64 buffer [T_m][9] that k_deciles fills with
@@ -165,12 +169,20 @@ int csm_momentum_chunked_ids(csm_ctx* ctx, const double* PM, int32_t T_m, int64_
  * its first use (a launch leaves its sync words zero again; word 2 is set if a wait gave up,
  * which no correct launch does).  One launch at a time per workspace: two launches in flight
  * on different streams must not share one (their tickets and flags would mix).
+ * A give-up is never silent: csm_signal_chunked_status reports it.
  */
 int64_t csm_signal_chunked_workspace(int32_t T_m, int64_t N, int32_t J, int32_t skip, int32_t C);
 int csm_signal_chunked(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                        const int64_t* month_start, int32_t T_m, int32_t max_month_days,
                        int32_t J, int32_t skip, int32_t C, double* R, double* M, double* NR,
                        uint16_t* ids, void* workspace);
+/*
+ * Synchronises the context's stream and reads the workspace's give-up mark: CSM_OK, or
+ * CSM_E_TIMEOUT when a csm_signal_chunked launch on it since the last check gave up a wait (its
+ * outputs are invalid); the mark is then cleared.  CSM_E_INVAL while the stream is capturing
+ * (check after the graph's replay).
+ */
+int csm_signal_chunked_status(csm_ctx* ctx, void* workspace);
 /*
  * The two together for narrow sweep panels (C3): every look-back Js[q] (1 <= nJ <= 4, host
  * arrays as csm_momentum_multi) from ONE time-chunked scan -- one summary / fold for max(J) (plus

@@ -14,7 +14,7 @@ for i in $(seq 1 "$rounds"); do
     if [ "$v" = base ] && [ -n "${BASE_ARGS:-}" ]; then
       timeout -k 10 300 python -u bench.py --config "$cfg" --no-cpu-baseline "$@" $BASE_ARGS > "$log" 2>&1 || { echo "run $v $i failed"; tail -5 "$log"; exit 1; }
     elif [ "$v" = base ]; then
-      CSMOM_LIB=ab/libcsmom_base.so timeout -k 10 300 python -u bench.py --config "$cfg" --no-cpu-baseline "$@" > "$log" 2>&1 || { echo "run $v $i failed"; tail -5 "$log"; exit 1; }
+      CSMOM_AB_BASE=1 CSMOM_LIB=ab/libcsmom_base.so timeout -k 10 300 python -u bench.py --config "$cfg" --no-cpu-baseline "$@" > "$log" 2>&1 || { echo "run $v $i failed"; tail -5 "$log"; exit 1; }
     else
       timeout -k 10 300 python -u bench.py --config "$cfg" --no-cpu-baseline "$@" > "$log" 2>&1 || { echo "run $v $i failed"; tail -5 "$log"; exit 1; }
     fi

@@ -96,6 +96,30 @@ def test_c4_labels_every_date_and_means(c4, c4_oracle):
     assert np.array_equal(np.isnan(ls), np.isnan(LS_r)) and max_rel(ls, LS_r) <= REL
 
 
+def test_c4_halo_shards_bench_geometry(engine, c4):
+    """The benched 8-way date-shard geometry on the C4 bench panel itself (bench.py --gpus 8
+    --shard-mode halo, run here as virtual shards on one device with the collectives replaced
+    by stacks): every rank's halo state + k_signal<SH>, the need bits / union list, the listed
+    columns' records, fold and repair, and the decile pass of its ~58 rows -- which takes the
+    split pass (plan / chunked sweep / finish), while the one-GPU pipeline's 461 rows take the
+    merged pass.  M, NR, labels, counts, decile means and long-short bit for bit the one-GPU
+    csm_pipeline (features.py:44-52, run_demo.py:18-29,46-67); the listed columns fit the list
+    width the rank pass sizes (no fallback)."""
+    from csmom.distributed import fallback_cap, halo_slices, halo_months, virtual_shards_halo
+    N, T_d, ms_h, pan, out = c4
+    G = 8
+    rows = [m1 - m0 for (_, _, _, _, _, m0, m1) in halo_slices(np.asarray(ms_h), G,
+                                                                 halo_months(12, 1))]
+    assert max(rows) * 2 <= engine.cus < 2 * out.L.shape[0]   # split on ranks, merged whole
+    M, NR, L, EW, CNT, LS, cnt = virtual_shards_halo(engine, pan.P, ms_h, G, 12, 1, 10)
+    assert 1 <= cnt <= fallback_cap(N), cnt                    # the listed-column path ran
+    assert bits_equal(M.cpu().numpy(), out.M.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), out.NR.cpu().numpy())
+    assert torch.equal(L, out.L) and torch.equal(CNT, out.CNT)
+    assert bits_equal(EW.cpu().numpy(), out.EW.cpu().numpy())
+    assert bits_equal(LS.cpu().numpy(), out.LS.cpu().numpy())
+
+
 def test_c4_default_decile_kernel_agrees(engine, c4):
     """The streaming decile kernel (no ids) on the same mom_J: identical labels and counts."""
     N, T_d, ms_h, pan, out = c4
@@ -183,6 +207,43 @@ def test_c3_sweep_runner_summary(engine, c3):
         c = lambda x: x.contiguous()
         one = engine.summary(c(o.LS), c(o.TURN), c(o.COST), c(o.NET))[0, 0]
         assert bits_equal(summ[0, s].cpu().numpy(), one.cpu().numpy()), (J, K)
+
+
+def test_c3_bench_step_vs_oracle(engine, c3):
+    """The C3 step bench.py times, exactly (bench.py sweep_main's step_defer): month prices ->
+    value weights / dollar ADV -> SweepRunner(SweepConfig(Js=Ks=(3, 6, 9, 12), skip=1,
+    aum=1e8)).run_batch(PM, 1, W, ADV, defer=True) on its defaults -- the four look-backs
+    joined, the chunked multi-J scan with ids, the legs-mode decile pass on ids, the legs-only
+    grouped value-weight accounting (k_turnover_vwg) and the device summary.  Every (J, K) row
+    of the summary table against the oracle chain (features.py:44-52 scan, run_demo.py:18-29
+    qcut, portfolio_oracle's overlapping K-month value-weighted legs with the square-root-impact
+    cost of execution_models.py:4-12, the summary of utils.py:8-16): months exact, every other
+    field within 1e-10 relative (fp64 sums in another fixed order)."""
+    import csmom
+    PM, W, ADV = c3
+    cfg = csmom.SweepConfig(Js=(3, 6, 9, 12), Ks=(3, 6, 9, 12), skip=1, aum=1e8)
+    runner = csmom.SweepRunner(engine, cfg)
+    summ, _, flag = runner.run_batch(PM, 1, W=W, ADV=ADV, defer=True)
+    torch.cuda.synchronize()
+    assert flag is not None and int(flag.item()) == 0   # the legs-only branch the bench times
+    got_all = summ.cpu().numpy()
+    assert got_all.shape == (1, 16, 7)
+    PM_h, W_h, ADV_h = PM.cpu().numpy(), W.cpu().numpy(), ADV.cpu().numpy()
+    T_m = PM_h.shape[0]
+    for J in cfg.Js:
+        _, M_r, NR_r, _ = O.momentum_scan(PM_h, J, cfg.skip)
+        L_r = O.assign_deciles(M_r, cfg.n_bins)
+        for K in cfg.Ks:
+            r = PO.portfolio(L_r, NR_r, cfg.n_bins, K=K, W=W_h, half_spread=cfg.half_spread,
+                             k_impact=cfg.k_impact, aum=cfg.aum, ADV=ADV_h)
+            x = lambda f: r[f].reshape(1, T_m, 1)
+            ref = _summary_rows(x("LS"), x("TURN"), x("COST"), x("NET"))[0, 0]
+            got = got_all[0, cfg.strategies.index((J, K))]
+            assert np.array_equal(np.isnan(got), np.isnan(ref)), (J, K)
+            assert got[0] == ref[0], (J, K, got[0], ref[0])          # months
+            m = ~np.isnan(ref)
+            err = np.abs(got[m] - ref[m]) / np.maximum(np.abs(ref[m]), 1e-12)
+            assert err.max() <= REL, (J, K, float(err.max()))
 
 
 # ------------------------------------------------------------------------------------ C5

@@ -283,8 +283,9 @@ def tune_split(engine):
 @pytest.mark.parametrize("case", MERGE_CASES)
 def test_deciles_ids_split_equals_merged(engine, tune_split, case):
     """The split decile pass (plan -> chunked sweep -> finish, the general kernel for the rows
-    it leaves) against the one-workgroup-per-row merged pass: labels, counts and ranked rows bit
-    for bit, means within 1e-13 (another fixed summation order); labels equal the oracle's."""
+    it leaves) against the one-workgroup-per-row merged pass: labels, counts, ranked rows AND
+    decile means bit for bit (the merged pass sums in the split pass's chunk order,
+    DEC_CHUNK_ORDER); labels equal the oracle's."""
     rng = np.random.default_rng(11)
     x = np.stack([_stress_row(case), _stress_row("lognormal_mild"), _stress_row(case)])
     nr = rng.normal(0.01, 0.1, x.shape)
@@ -296,8 +297,7 @@ def test_deciles_ids_split_equals_merged(engine, tune_split, case):
         got[v] = engine.deciles_ids(M, NR, IDS, 10, with_nv=True)
     (L1, EW1, C1, N1), (L0, EW0, C0, N0) = got[1], got[0]
     assert torch.equal(L1, L0) and torch.equal(C1, C0) and torch.equal(N1, N0), case
-    a, b = EW1.cpu().numpy(), EW0.cpu().numpy()
-    assert np.array_equal(np.isnan(a), np.isnan(b)) and max_rel(a, b) <= 1e-13, case
+    assert bits_equal(EW1.cpu().numpy(), EW0.cpu().numpy()), case
     for r in range(x.shape[0]):
         assert np.array_equal(L1.cpu().numpy()[r], _oracle_labels(x[r])), (case, r)
     L2, _, _, _ = engine.deciles_ids(M, None, IDS, 10)          # labels only (no next_ret)
@@ -307,8 +307,8 @@ def test_deciles_ids_split_equals_merged(engine, tune_split, case):
 @pytest.mark.parametrize("N,T", [(40_000, 2_200), (16_388, 900), (65_536, 700)])
 def test_pipeline_split_equals_merged(engine, tune_split, N, T):
     """The C4 path (csm_pipeline: signal + ids -> decile pass -> long-short) with the split and
-    the merged decile pass: labels / counts bit for bit, means and long-short within 1e-13, and
-    the split pass's labels equal the oracle's qcut; rows of one, several and a partial chunk."""
+    the merged decile pass: labels / counts / means / long-short bit for bit, and the split
+    pass's labels equal the oracle's qcut; rows of one, several and a partial chunk."""
     pan = _panel(N=N, T=T, seed=N % 97)
     P, ms = _up(pan["P"]), _up(pan["month_start"])
     got = {}
@@ -318,9 +318,38 @@ def test_pipeline_split_equals_merged(engine, tune_split, N, T):
     a, b = got[1], got[0]
     assert torch.equal(a.L, b.L) and torch.equal(a.CNT, b.CNT) and torch.equal(a.NV, b.NV)
     for k in ("EW", "LS"):
-        x, y = getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy()
-        assert np.array_equal(np.isnan(x), np.isnan(y)) and max_rel(x, y) <= 1e-13, k
+        assert bits_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy()), k
     assert np.array_equal(a.L.cpu().numpy(), O.assign_deciles(a.M.cpu().numpy(), 10))
+
+
+@pytest.mark.parametrize("cells", [32768, 8192])
+def test_chunk_order_merged_equals_split_any_row_count(engine, tune_split, cells):
+    """The pass is chosen by the launch's row count (auto: the split pass below n_CU / 2 rows),
+    so a long one-GPU panel (merged pass) and its short date slices (split pass) must still give
+    the same decile means bit for bit: the 150-month panel ranked in one launch against its
+    rows ranked 20 at a time, under the default auto choice, at the default and a small chunk
+    width (more chunks per row, odd chunk counts)."""
+    lib = engine.lib
+    pan = _panel(N=24_000, T=3_300, seed=29)
+    P, ms = _up(pan["P"]), _up(pan["month_start"])
+    _, _, M, NR, IDS = engine.signal_ids(P, ms, int(np.diff(pan["month_start"]).max()), 12, 1)
+    T_m = M.shape[0]
+    assert 2 * T_m > engine.cus and 2 * 20 <= engine.cus   # merged whole, split in slices
+    try:
+        assert lib.csm_tune(b"dec_split_cells", cells) == 0
+        assert tune_split(2) == 0
+        L, EW, CNT, _ = engine.deciles_ids(M, NR, IDS, 10)
+        parts = []
+        for t0 in range(0, T_m, 20):
+            sl = slice(t0, min(T_m, t0 + 20))
+            parts.append(engine.deciles_ids(M[sl].contiguous(), NR[sl].contiguous(),
+                                            IDS[sl].contiguous(), 10))
+    finally:
+        lib.csm_tune(b"dec_split_cells", 32768)
+    assert torch.equal(L, torch.cat([p[0] for p in parts]))
+    assert torch.equal(CNT, torch.cat([p[2] for p in parts]))
+    assert bits_equal(EW.cpu().numpy(), torch.cat([p[1] for p in parts]).cpu().numpy())
+    assert np.array_equal(L.cpu().numpy(), O.assign_deciles(M.cpu().numpy(), 10))
 
 
 def test_pipeline_deciles_repeatable(engine):

@@ -537,3 +537,40 @@ def test_turnover_mask_bit_identical(engine, B, Ks, ncols, key):
                 a = getattr(got[1][i][K], f).cpu().numpy()
                 b = getattr(got[0][i][K], f).cpu().numpy()
                 assert bits_equal(a, b), (i, K, f)
+
+
+def test_turnover_planes_follow_the_cohort_pass(engine):
+    """The steady legs turnover reads the leg bitplanes only from a workspace whose cohort pass
+    wrote them (recorded per workspace in the context), never because the knob says so at
+    accounting time: a cohort pass run with turn_mask 0 into a workspace full of garbage,
+    then the accounting with turn_mask back at 1, gives the default path's bits (the label
+    bytes are read instead of the never-written planes)."""
+    import ctypes
+    z = load_golden("c1")
+    PM, _ = engine.month_end(_up(z["P"]), _up(z["month_start"].astype(np.int64)))
+    T_m, N = PM.shape
+    _, M, NR = engine.momentum(PM, 12, 1)
+    L, _, _, _ = engine.deciles(M, None, 10)
+    B, Ks = 8, (3, 6, 9, 12)
+    rep = lambda x: _up(np.stack([np.roll(x.cpu().numpy(), 7 * i, axis=1) for i in range(B)],
+                                 axis=1).reshape(T_m, B * N))
+    L, NR = rep(L), rep(NR)
+    ref = engine.portfolio_multi(L, NR, 10, Ks=Ks, B=B, legs_only=True)
+    lib = engine.lib
+    nbytes = int(lib.csm_portfolio_workspace(T_m, B, N, 10, max(Ks)))
+    ws = torch.full((nbytes,), 0xFF, dtype=torch.uint8, device="cuda:0")
+    try:
+        assert lib.csm_tune(b"turn_mask", 0) == 0
+        engine._call("csm_cohort_sums_legs", ctypes.c_void_p(L.data_ptr()),
+                     ctypes.c_void_p(NR.data_ptr()), None, T_m, B, N, 10, max(Ks),
+                     ctypes.c_void_p(ws.data_ptr()))
+    finally:
+        assert lib.csm_tune(b"turn_mask", 1) == 0
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    res, _ = engine._from_cohorts(L, None, T_m, B, N, 10, list(Ks), 0.0005, 0.1, 0.0, None,
+                                  None, True, ws, True, flag)
+    assert int(flag.item()) == 0
+    for K in Ks:
+        for f in ("LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(res[K], f).cpu().numpy(),
+                              getattr(ref[K], f).cpu().numpy()), (K, f)

@@ -415,9 +415,9 @@ def test_halo_shards_four_wave_blocks(engine, G, j12):
 @pytest.mark.parametrize("G", [2, 5, 8])
 def test_halo_shards_bucket_ids(engine, G):
     """Wide rows: halo shards write bucket ids (the repair rewrites the ids of replayed cells)
-    and rank from them -- csm_pipeline's labels, counts and means bit for bit (both sides take
-    the split decile pass at these row counts), the oracle's labels; few assets need the
-    exchange on this panel."""
+    and rank from them -- csm_pipeline's labels, counts and means bit for bit (the split pass
+    on the shards, and on the whole panel too at these row counts), the oracle's labels; few
+    assets need the exchange on this panel."""
     from oracle.synth_np import make_panel
     from csmom.distributed import virtual_shards_halo
     pan = make_panel(20_000, 1_400, seed=17, with_volume=False, nan_day=0.03, absent_month=0.05,

@@ -169,11 +169,45 @@ def test_handoff_under_uneven_load(engine):
         k = it % 2
         with torch.cuda.stream(side):   # bandwidth pressure on other CUs meanwhile
             dst.copy_(src)
-        _, M, NR, I, ws = engine.signal_chunked(Ps[k], mss[k], maxd, 12, 1, workspace=ws)
+        _, M, NR, I, ws = engine.signal_chunked(Ps[k], mss[k], maxd, 12, 1, workspace=ws,
+                                                check=False)
         outs.append((k, M, NR, I))
     torch.cuda.synchronize()
     assert not engine.signal_chunked_timed_out(ws)
+    engine.signal_chunked_status(ws)   # (raises on a give-up mark)
     for k, M, NR, I in outs:
         assert bits_equal(M.cpu().numpy(), refs[k][0].cpu().numpy())
         assert bits_equal(NR.cpu().numpy(), refs[k][1].cpu().numpy())
         assert torch.equal(I, refs[k][2])
+
+
+def test_timeout_is_loud(engine):
+    """A workgroup that gives up waiting for an earlier chunk's record (forced here: the
+    "tc_spins" knob at 0 gives up at the first trip) must not pass as a correct launch:
+    Engine.signal_chunked raises CSM_E_TIMEOUT (csm_signal_chunked_status), an unchecked launch
+    leaves the mark for the status call, the report clears it, and the next launch on the same
+    workspace is correct bit for bit."""
+    import csmom
+    from csmom._lib import CSM_E_TIMEOUT
+    lib = engine.lib
+    pan = _panel(2_000, 1_500, 5)
+    P, ms = _up(pan["P"]), _up(pan["month_start"])
+    maxd = int(torch.diff(ms).max().item())
+    _, M0, NR0, I0, ws = engine.signal_chunked(P, ms, maxd, 12, 1, chunks=4)
+    try:
+        assert lib.csm_tune(b"tc_spins", 0) == 0
+        with pytest.raises(csmom.CsmError) as ei:
+            engine.signal_chunked(P, ms, maxd, 12, 1, chunks=4, workspace=ws)
+        assert ei.value.status == CSM_E_TIMEOUT
+        assert not engine.signal_chunked_timed_out(ws)   # reported once, then cleared
+        engine.signal_chunked(P, ms, maxd, 12, 1, chunks=4, workspace=ws, check=False)
+        assert engine.signal_chunked_timed_out(ws)       # unchecked: the mark stays
+        with pytest.raises(csmom.CsmError) as ei:
+            engine.signal_chunked_status(ws)
+        assert ei.value.status == CSM_E_TIMEOUT
+    finally:
+        assert lib.csm_tune(b"tc_spins", 1 << 21) == 0
+    _, M, NR, I, ws = engine.signal_chunked(P, ms, maxd, 12, 1, chunks=4, workspace=ws)
+    assert bits_equal(M.cpu().numpy(), M0.cpu().numpy())
+    assert bits_equal(NR.cpu().numpy(), NR0.cpu().numpy())
+    assert torch.equal(I, I0)
