@@ -797,6 +797,45 @@ def sweep_profile(config, N, T_d, stage, alg_bytes):
                         "box_note": "rocprofv3 run on another box than this line"}}
 
 
+def sweep_decile_match(config, eng, PM=None, R0=None, J=12, n_bins=10):
+    """Decile match % of a sweep line: one sampled panel (C3: the panel; C5:
+    bootstrap panel 0) and one look-back J, ranked by the bench's kernels -- the chunked multi-J
+    scan (C3) or csm_boot_scan (C5), then the decile pass on ids -- against the oracle's qcut of
+    the ORACLE's mom_J (oracle month-end + scan; C5: the oracle's bootstrap of the same base
+    returns).  Full labels (every decile) and the legs-mode labels the sweep's accounting reads
+    (deciles 0 / n_bins - 1 / NaN exact, the interior ones anywhere inside)."""
+    import torch
+    from oracle import csmom_oracle as O
+    from oracle import portfolio_oracle as PO
+    if config == "c3":
+        T_m, N = PM.shape
+        M, _, IDS = eng.momentum_multi(PM, (J,), 1, with_ids=True,
+                                       chunks=eng.default_chunks(T_m, N, J, 1))[0]
+        _, Mo, _, _ = O.momentum_scan(PM.cpu().numpy(), J, 1)
+        what = f"the C3 panel, J = {J}"
+    else:
+        T_m, N = R0.shape
+        _, outs, _, _ = eng.boot_scan(R0, 1, (3, 6, 9, 12), 1, b0=0, seed=5000, mean_block=6.0)
+        M, IDS = outs[(3, 6, 9, 12).index(J)]
+        src = PO.bootstrap_indices(T_m, 1, 5000, 6.0, b0=0)
+        pm = PO.bootstrap_panel(R0.cpu().numpy(), src).reshape(T_m, N)
+        _, Mo, _, _ = O.momentum_scan(pm, J, 1)
+        what = f"bootstrap panel 0 of the C5 draw, J = {J}"
+    L, _, _, _ = eng.deciles_ids(M, None, IDS, n_bins)
+    Lg, _, _, _ = eng.deciles_ids(M, None, IDS, n_bins, legs=True)
+    torch.cuda.synchronize()
+    Lo = O.assign_deciles(Mo, n_bins)
+    Lh, Lgh = L.cpu().numpy(), Lg.cpu().numpy()
+    mom_exact = float((M.cpu().numpy().view(np.uint64) == Mo.view(np.uint64)).mean()) * 100.0
+    edge = (Lo == 0) | (Lo == n_bins - 1) | (Lo < 0)
+    legs_ok = np.where(edge, Lgh == Lo, (Lgh >= 1) & (Lgh <= n_bins - 2))
+    return {"decile_match_pct": round(100.0 * float((Lh == Lo).mean()), 6),
+            "legs_match_pct": round(100.0 * float(legs_ok.mean()), 6),
+            "mom_bit_exact_pct": round(mom_exact, 6),
+            "sample": f"{what}: {T_m} dates x {N} assets, the oracle's qcut of the oracle's mom_J "
+                      f"(full labels; legs: the legs-mode labels the accounting reads)"}
+
+
 def sweep_main(args):
     """C3 / C5: the (J, K) sweep (SweepRunner) on one panel (C3: at N > 1 the 16 strategies are
     split across the ranks, SweepRunner.run_batch_sharded, strong scaling of the fixed grid) or
@@ -969,6 +1008,11 @@ def sweep_main(args):
             "result_means": res_summary,
             "cpu_baseline": None,
         }
+        if not args.no_oracle_mom:
+            line["decile_match"] = sweep_decile_match(args.config, eng,
+                                                      PM=PM if args.config == "c3" else None,
+                                                      R0=R0 if args.config == "c5" else None)
+            line["decile_match_pct"] = line["decile_match"]["decile_match_pct"]
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_sweep(args.config, 1500 if args.config == "c3" else 1000,
                                                       T_d, cfg["start"])

@@ -128,6 +128,10 @@ SIGNATURES = {
                                               _p, _i64, _p]),
     "csm_shard_repair_cols": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p,
                                              _p, _p, _p, _i64, _p, _p, _p, _p]),
+    "csm_signal_halo": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _i32,
+                                       _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "csm_shard_fix_cols": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _i32, _p, _i32, _i32,
+                                          _p, _p, _i64, _p, _p, _p, _p]),
     "csm_signal_ids": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i32, _i32, _i32, _i32, _i32, _p,
                                       _p, _p, _p, _p]),
     "csm_deciles_ids": (ctypes.c_int, [_p, _p, _p, _p, _i32, _i64, _i32, _p, _p, _p, _p, _p]),

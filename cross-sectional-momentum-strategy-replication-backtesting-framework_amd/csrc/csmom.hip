@@ -741,6 +741,56 @@ __global__ __launch_bounds__(256) void k_momentum_multi_reg2(const double* __res
 
 #define MJ_REG_W 16
 
+// F's step: scan_step without outputs (the state transition only).
+__device__ __forceinline__ void scan_shadow(ScanLane& s, double x, int m, double* ring, int RS,
+                                            int W, int J) {
+  if (is_absent(x)) return;
+  const bool xv = !isnan_d(x);
+  const double pnew = xv ? x : s.pff;
+  const double ret = pnew / s.pff - 1.0;
+  s.pff = pnew;
+  ring[s.head * RS] = 1.0 + ret;
+  s.head = (s.head + 1 == W) ? 0 : s.head + 1;
+  double acc = ring[s.head * RS];
+  int idx = s.head;
+  for (int k = 1; k < J; ++k) {
+    idx = (idx + 1 == W) ? 0 : idx + 1;
+    acc = acc * ring[idx * RS];
+  }
+  const bool ranked = !isnan_d(acc - 1.0);
+  if (ranked) {
+    s.psff = xv ? x : s.psff;
+    s.prev = m;
+  } else {
+    s.prev = -1;
+  }
+}
+
+#define HALO_WALK 24   // a business month's day rows in one batch of loads
+#define HALO_MAXG 64
+
+// Month-end of asset a over day rows [d0, d1) (k_signal's reduction: last valid price, NaN if
+// the month has rows but no price, ABSENT if none), walked back from the last row: one load for
+// the usual month whose last row holds a price, else rows HALO_WALK at a time in flight.
+__device__ __forceinline__ double halo_month_price(const double* __restrict__ P, int64_t d0,
+                                                   int64_t d1, int64_t N, int64_t a) {
+  if (d1 <= d0) return absent_val();
+  const double xl = P[(d1 - 1) * N + a];
+  if (xl == xl) return xl;
+  bool p = !is_absent(xl);
+  for (int64_t d = d1 - 2; d >= d0; d -= HALO_WALK) {
+    double xs[HALO_WALK];
+#pragma unroll
+    for (int u = 0; u < HALO_WALK; ++u) xs[u] = d - u >= d0 ? P[(d - u) * N + a] : absent_val();
+#pragma unroll
+    for (int u = 0; u < HALO_WALK; ++u) {
+      if (xs[u] == xs[u]) return xs[u];
+      p |= !is_absent(xs[u]);
+    }
+  }
+  return p ? qnan() : absent_val();
+}
+
 // =====================================================================================
 // Kernel AB (fused): month-end aggregation + scan in one stream over the daily panel, for
 // large N.  One wave per block, two assets per lane (16-B row loads, 1 KiB per wave-
@@ -774,12 +824,26 @@ __device__ __forceinline__ bool shard_pm_kept(int m, int T_m, int W) {
 // price, and the first / last present month (-1 none) -- for k_shard_summary_state and
 // k_shard_repair.
 // BL (VEC 2): day rows by raw buffer loads (see load_month).
-template <int MAXD, int VEC, int NBUF, int BW, bool SH, bool BL, int JC = 0>
+// HALO (with SH, the halo date-shard pass): month_start holds ha.H halo months, the shard's
+// T_m months and ha.F forward months; a prologue does k_halo_pm + k_shard_halo's work for the
+// lane's assets -- the halo months' and forward months' prices (the month's last day row, a walk
+// back where it holds no price), the scan state the halo leaves from an empty state, its flags
+// (ha.flags) -- and the shard's scan continues from that state in the same registers / LDS ring,
+// the forward price finishing the pending ranked row: the same state, so the same outputs, as
+// k_shard_halo -> k_signal<SH> (csm_signal_shard_halo), without two launches and their
+// dependent walks between them.
+struct HaloArgs {
+  int H, F, before, after;
+  uint8_t* flags;
+};
+#define HALO_BATCH 8   // halo / forward months per prologue batch (LDS: [8][RS] prices + lists)
+template <int MAXD, int VEC, int NBUF, int BW, bool SH, bool BL, int JC = 0, bool HALO = false>
 __global__ __launch_bounds__(64 * BW) void k_signal(
     const double* __restrict__ P, const int64_t* __restrict__ month_start, int T_m, int64_t N,
     int J, int skip, double* __restrict__ PMo, double* __restrict__ R, double* __restrict__ M,
     double* __restrict__ NR, const double* __restrict__ carry, const double* __restrict__ next_pm,
-    double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS) {
+    double* __restrict__ carry_out, int64_t T_d, uint16_t* __restrict__ IDS, HaloArgs ha) {
+  static_assert(!HALO || (SH && VEC == 2), "the halo prologue: shard passes, paired lanes");
   typedef typename RowT<VEC>::T VT;
   extern __shared__ __attribute__((aligned(16))) double ring_lds[];  // [W][64 * VEC * BW]
   const int W = J + skip;
@@ -793,12 +857,131 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   int* shc = reinterpret_cast<int*>(ring_lds + W * RS);
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
-    scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, carry, N, a0 + k, live);
+    scan_init(sl[k], ring_lds + VEC * tid + k, RS, W, HALO ? nullptr : carry, N, a0 + k, live);
     if (SH) {
       shc[VEC * tid + k] = 0;
       shc[RS + VEC * tid + k] = -1;
       shc[2 * RS + VEC * tid + k] = -1;
     }
+  }
+  double npmh[VEC];   // HALO: the forward price of each asset (csm_shard_halo's next_pm)
+  if constexpr (HALO) {
+    // Months in batches of HU: each lane loads its two assets' last day row of every month of
+    // the batch (one 16-B load a month, all in flight); the cells whose last day holds no price
+    // (a missing day, a listing, a delisting, an absent month) are listed per wave and walked
+    // back by the wave's lanes in parallel, a cell per lane (halo_month_price); then each lane
+    // scans its halo months from an empty state (k_shard_halo's scan_shadow) and takes the first
+    // forward month with a row as the forward price.  LDS after the ring and the SH counters:
+    // the batch's month prices [HU][RS] and each wave's list of cells to walk.
+    constexpr int HU = HALO_BATCH;
+    const int64_t* ms = month_start;
+    const int H = ha.H, F = ha.F, HF = H + F;
+    const int64_t as = live ? a0 : 0;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int64_t aw = a0 - 2 * lane;   // the wave's first asset
+    double* hpw = ring_lds + (size_t)W * RS + (size_t)(3 * RS) / 2;
+    uint16_t* wl = reinterpret_cast<uint16_t*>(hpw + HU * RS) + wv * (HU * 128);
+    int nh[VEC], fv[VEC], lv[VEC];
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) { nh[c] = 0; fv[c] = -1; lv[c] = -1; npmh[c] = absent_val(); }
+    for (int j0 = 0; j0 < HF; j0 += HU) {   // (block-uniform)
+      double2 xl[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int j = j0 + u;
+        const int m = j < H ? j : j + T_m;   // halo month j, or forward month j - H
+        xl[u] = make_double2(absent_val(), absent_val());
+        if (j < HF) {
+          const int64_t d0 = ms[m], d1 = ms[m + 1];
+          if (d1 > d0) xl[u] = *reinterpret_cast<const double2*>(P + (d1 - 1) * N + as);
+        }
+      }
+      int nit = 0;   // wave-uniform
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        *reinterpret_cast<double2*>(hpw + u * RS + 2 * tid) = xl[u];
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) {
+          const double x = comp(xl[u], c);
+          const bool need = live && j0 + u < HF && !(x == x);
+          const uint64_t mk = __ballot(need);
+          if (need) wl[nit + lane_prefix(mk)] = (uint16_t)(u * 128 + 2 * lane + c);
+          nit += __popcll(mk);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // the walks, a cell per lane and two cells per lane at once: the month's day rows before
+      // its last (known to hold no price) in one batch of loads per cell, all in flight
+      for (int it0 = 0; it0 < nit; it0 += 128) {   // (wave-uniform)
+        int item[2], u[2];
+        int64_t d0[2], d1[2];
+        double xs[2][HALO_WALK];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int it = it0 + 64 * h + lane;
+          item[h] = it < nit ? (int)wl[it] : -1;
+          u[h] = item[h] >> 7;
+          const int j = j0 + (item[h] < 0 ? 0 : u[h]);
+          const int m = j < H ? j : j + T_m;
+          d0[h] = ms[m];
+          d1[h] = ms[m + 1];
+          const int64_t a = aw + (item[h] & 127);
+#pragma unroll
+          for (int k = 0; k < HALO_WALK; ++k) {
+            const int64_t d = d1[h] - 2 - k;
+            xs[h][k] = (item[h] >= 0 && d >= d0[h]) ? P[d * N + a] : absent_val();
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (item[h] < 0) continue;
+          const int64_t a = aw + (item[h] & 127);
+          const double xlast = hpw[u[h] * RS + 128 * wv + (item[h] & 127)];
+          bool p = !is_absent(xlast), got = false;
+          double x = 0.0;
+#pragma unroll
+          for (int k = 0; k < HALO_WALK; ++k) {
+            if (!got && xs[h][k] == xs[h][k]) { x = xs[h][k]; got = true; }
+            p |= !is_absent(xs[h][k]);
+          }
+          if (!got && d1[h] - 1 - HALO_WALK > d0[h]) {   // months longer than the batch (rare)
+            const double y = halo_month_price(P, d0[h], d1[h] - 1 - HALO_WALK, N, a);
+            if (y == y) { x = y; got = true; }
+            p |= !is_absent(y);
+          }
+          hpw[u[h] * RS + 128 * wv + (item[h] & 127)] = got ? x : (p ? qnan() : absent_val());
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int j = j0 + u;
+        if (j >= HF) break;
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) {
+          const double x = hpw[u * RS + 2 * tid + c];
+          if (j < H) {
+            if (live && !is_absent(x)) {
+              if (!isnan_d(x)) { if (fv[c] < 0) fv[c] = nh[c]; lv[c] = nh[c]; }
+              ++nh[c];
+              scan_shadow(sl[c], x, j, ring_lds + VEC * tid + c, RS, W, J);
+            }
+          } else if (is_absent(npmh[c])) {
+            npmh[c] = x;
+          }
+        }
+      }
+      __syncthreads();   // (the batch's LDS is the next batch's)
+    }
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) {
+      sl[c].prev = -1;   // (the halo's pending row is the previous rank's: scan_init's state)
+      uint8_t fl = 0;
+      if (ha.before && !(fv[c] >= 0 && lv[c] - fv[c] >= W)) fl |= 1;
+      if (ha.after && is_absent(npmh[c])) fl |= 2;
+      if (live && ha.flags) ha.flags[a0 + c] = fl;
+    }
+    month_start += H;   // the shard's months from here on
   }
   const double* base = P + (live ? a0 : 0);
   const int64_t rstride = N;
@@ -907,8 +1090,20 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
   if (live) {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
-      scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm,
-                  SH ? nullptr : carry_out);
+      if constexpr (HALO) {   // scan_finish's pending row, with the prologue's forward price
+        if (sl[k].prev >= 0) {
+          double nr = qnan();
+          const double x = npmh[k];
+          if (!is_absent(x)) {
+            const double ps_new = isnan_d(x) ? sl[k].psff : x;
+            nr = ps_new / sl[k].psff - 1.0;
+          }
+          NR[(int64_t)sl[k].prev * N + a0 + k] = nr;
+        }
+      } else {
+        scan_finish(sl[k], ring_lds + VEC * tid + k, RS, W, N, a0 + k, NR, next_pm,
+                    SH ? nullptr : carry_out);
+      }
       if (SH) {
         const int* q = shc + VEC * tid + k;
         carry_out[a0 + k] = (double)q[0];
@@ -1092,20 +1287,15 @@ struct FoldJs {
   int n;
   int J[MJ_MAX];
 };
-__global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ sm, int G, int g,
-                                                    int64_t N, int J, int skip,
-                                                    double* __restrict__ carry,
-                                                    double* __restrict__ next_pm,
-                                                    const double* __restrict__ tail_pm,
-                                                    FoldJs jq, double* __restrict__ psq) {
-  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= N) return;
+// The fold of k_fold_carry for asset (column) a: the scan state at shard g's first month from
+// the exchange records of shards < g (ring factors oldest first, then pff, psff: rows 0..W + 1
+// through store(row, value)), and the first present price after shard g (returned).
+template <class Store>
+__device__ __forceinline__ double fold_body(const double* __restrict__ sm, int G, int g,
+                                            int64_t N, int64_t a, int J, int skip,
+                                            const double* __restrict__ tail_pm, Store store,
+                                            const FoldJs& jq, double* __restrict__ psq) {
   const int W = J + skip, T = W + 1, S = SUM_SCALARS + T;
-  if (g < 0) {  // batched over all chunks: chunk blockIdx.y, outputs stacked per chunk
-    g = blockIdx.y;
-    carry += (int64_t)g * (W + 2) * N;
-    next_pm += (int64_t)g * N;
-  }
   const double NaN = qnan();
   // the neighbours' scalars in one round trip (the walks below start there and usually end
   // there): chunk g - 1's record scalars, chunk g + 1's count and first price
@@ -1126,7 +1316,6 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
     else for (int h = g + 2; h < G; ++h) if (sc(h, 0) > 0.0) { npm = sc(h, 5); break; }
   }
   if (tail_pm && g < G - 1 && is_absent(npm)) npm = tail_pm[a];
-  next_pm[a] = npm;
   // locate the oldest of the last T present rows of shards < g
   int nv = 0, src_h = -1, src_j = -1;
   for (int h = g - 1; h >= 0 && nv < T; --h) {
@@ -1144,7 +1333,7 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
   }
   // replay oldest -> newest; the newest W rets become the ring (as factors fl(1+ret))
   double pff = pff_before;
-  for (int k = 0; k < W; ++k) carry[(int64_t)k * N + a] = NaN;
+  for (int k = 0; k < W; ++k) store(k, NaN);
   int c = 0;
   for (int h = src_h; h >= 0 && h < g; ++h) {
     const int kh = (int)fmin(sc(h, 0), (double)T);
@@ -1160,14 +1349,14 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
         const double ret = nx / pff - 1.0;
         pff = nx;
         const int pos = c - (nv - W);
-        if (pos >= 0) carry[(int64_t)pos * N + a] = 1.0 + ret;
+        if (pos >= 0) store(pos, 1.0 + ret);
         ++c;
       }
     }
   }
   double lastv = NaN;
   for (int h = g - 1; h >= 0; --h) if (!isnan_d(sc(h, 3))) { lastv = sc(h, 3); break; }
-  carry[(int64_t)W * N + a] = lastv;
+  store(W, lastv);
   int64_t off = 0, f = -1;
   for (int hb = 0; hb < g; hb += SUM_U) {   // every earlier chunk's counts, SUM_U in flight
     double cn[SUM_U], fi[SUM_U];
@@ -1199,9 +1388,28 @@ __global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ s
     }
     return ps;
   };
-  carry[(int64_t)(W + 1) * N + a] = psff_of(J);
+  store(W + 1, psff_of(J));
   if (psq)
     for (int q = 0; q < jq.n; ++q) psq[((int64_t)g * MJ_MAX + q) * N + a] = psff_of(jq.J[q]);
+  return npm;
+}
+
+__global__ __launch_bounds__(256) void k_fold_carry(const double* __restrict__ sm, int G, int g,
+                                                    int64_t N, int J, int skip,
+                                                    double* __restrict__ carry,
+                                                    double* __restrict__ next_pm,
+                                                    const double* __restrict__ tail_pm,
+                                                    FoldJs jq, double* __restrict__ psq) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  const int W = J + skip;
+  if (g < 0) {  // batched over all chunks: chunk blockIdx.y, outputs stacked per chunk
+    g = blockIdx.y;
+    carry += (int64_t)g * (W + 2) * N;
+    next_pm += (int64_t)g * N;
+  }
+  next_pm[a] = fold_body(sm, G, g, N, a, J, skip, tail_pm,
+                         [&](int k, double v) { carry[(int64_t)k * N + a] = v; }, jq, psq);
 }
 
 // =====================================================================================
@@ -1944,31 +2152,6 @@ __global__ __launch_bounds__(COLS_THREADS) void k_shard_summary_cols(
       [&](int m) { return pmc[m]; }, n, fm, lm, T, ncol, out + j);
 }
 
-// F's step: scan_step without outputs (the state transition only).
-__device__ __forceinline__ void scan_shadow(ScanLane& s, double x, int m, double* ring, int RS,
-                                            int W, int J) {
-  if (is_absent(x)) return;
-  const bool xv = !isnan_d(x);
-  const double pnew = xv ? x : s.pff;
-  const double ret = pnew / s.pff - 1.0;
-  s.pff = pnew;
-  ring[s.head * RS] = 1.0 + ret;
-  s.head = (s.head + 1 == W) ? 0 : s.head + 1;
-  double acc = ring[s.head * RS];
-  int idx = s.head;
-  for (int k = 1; k < J; ++k) {
-    idx = (idx + 1 == W) ? 0 : idx + 1;
-    acc = acc * ring[idx * RS];
-  }
-  const bool ranked = !isnan_d(acc - 1.0);
-  if (ranked) {
-    s.psff = xv ? x : s.psff;
-    s.prev = m;
-  } else {
-    s.prev = -1;
-  }
-}
-
 __device__ __forceinline__ bool same_bits(double x, double y) {
   return __double_as_longlong(x) == __double_as_longlong(y);
 }
@@ -2080,6 +2263,74 @@ __global__ __launch_bounds__(COLS_THREADS) void k_shard_repair_cols(
       lds + T_m + W, 1);
 }
 
+// The halo pass's listed columns after collective 1b, in ONE launch: a workgroup per listed
+// column (a grid-stride loop over the device-side count, so an empty list costs one wave per
+// workgroup) folds the column's exchange records (fold_body, k_fold_carry's walk) into the
+// true scan state at the shard's first month and the first present price after the shard,
+// derives the column's month prices into LDS (shard_pm_at, all lanes), and one lane replays
+// every month from that state -- the sequential scan itself, so every output of the column is
+// the unsharded pass's (no convergence test against the halo trajectory: nothing the halo
+// state wrote is trusted).  Replaces k_fold_carry + k_shard_repair_cols.
+template <int WR, int JC>
+__global__ __launch_bounds__(COLS_THREADS) void k_shard_fix_cols(
+    const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
+    int T_m, int64_t N, int J, int skip, const double* __restrict__ recs, int G, int g,
+    double* __restrict__ R, double* __restrict__ M, double* __restrict__ NR,
+    uint16_t* __restrict__ IDS, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt,
+    int64_t ncol) {
+  // LDS: pm [T_m], carry [W + 2], ring [W] (runtime W), the column's records [G][S]
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int W = J + skip, S = SUM_SCALARS + W + 1;
+  double* pmc = lds;
+  double* cy = lds + T_m;
+  double* ring = cy + W + 2;
+  double* rec = ring + W;
+  const int64_t n = (int64_t)*cnt < ncol ? (int64_t)*cnt : ncol;
+  for (int64_t j = blockIdx.x; j < n; j += gridDim.x) {   // (workgroup-uniform)
+    const int64_t a = (int64_t)idx[j];
+    for (int q = threadIdx.x; q < G * S; q += COLS_THREADS) rec[q] = recs[(int64_t)q * ncol + j];
+    for (int m = threadIdx.x; m < T_m; m += COLS_THREADS) pmc[m] = shard_pm_at(PM, P, ms, m, T_m, W, N, a);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double npm = fold_body(rec, G, g, 1, 0, J, skip, (const double*)nullptr,
+                                   [&](int k, double v) { cy[k] = v; }, FoldJs{0, {0, 0, 0, 0}},
+                                   (double*)nullptr);
+      ScanLane t;
+      if constexpr (WR > 0) {   // the ring in registers, oldest first (k_signal_tc's scan)
+        double fr[WR];
+#pragma unroll
+        for (int k = 0; k < WR; ++k) fr[k] = cy[k];
+        t.pff = cy[WR];
+        t.psff = cy[WR + 1];
+        t.head = 0;
+        t.prev = -1;
+        double xn = pmc[0];
+        for (int m = 0; m < T_m; ++m) {
+          const double x = xn;
+          if (m + 1 < T_m) xn = pmc[m + 1];
+          const double mom = scan_step_reg<WR, JC>(t, x, m, fr, J, N, a, R, M, NR);
+          if (IDS) IDS[(int64_t)m * N + a] = (uint16_t)csm_fid(mom);
+        }
+      } else {
+        scan_init(t, ring, 1, W, cy, 1, 0, true);
+        for (int m = 0; m < T_m; ++m) {
+          const double mom = scan_step(t, pmc[m], m, ring, 1, W, J, N, a, R, M, NR);
+          if (IDS) IDS[(int64_t)m * N + a] = (uint16_t)csm_fid(mom);
+        }
+      }
+      if (t.prev >= 0) {   // the pending ranked row at the shard's end (scan_finish)
+        double nr = qnan();
+        if (!is_absent(npm)) {
+          const double ps_new = isnan_d(npm) ? t.psff : npm;
+          nr = ps_new / t.psff - 1.0;
+        }
+        NR[(int64_t)t.prev * N + a] = nr;
+      }
+    }
+    __syncthreads();   // (the LDS is the next column's)
+  }
+}
+
 // =====================================================================================
 // Halo date shards (the default multi-GPU pass; north_star's "J + skip lookback
 // halo").  A rank holds its shard's daily rows plus H calendar months before it and the first
@@ -2094,31 +2345,6 @@ __global__ __launch_bounds__(COLS_THREADS) void k_shard_repair_cols(
 // =====================================================================================
 #define HALO_THREADS 256
 #define HALO_U 8
-#define HALO_WALK 24   // a business month's day rows in one batch of loads
-#define HALO_MAXG 64
-
-// Month-end of asset a over day rows [d0, d1) (k_signal's reduction: last valid price, NaN if
-// the month has rows but no price, ABSENT if none), walked back from the last row: one load for
-// the usual month whose last row holds a price, else rows HALO_WALK at a time in flight.
-__device__ __forceinline__ double halo_month_price(const double* __restrict__ P, int64_t d0,
-                                                   int64_t d1, int64_t N, int64_t a) {
-  if (d1 <= d0) return absent_val();
-  const double xl = P[(d1 - 1) * N + a];
-  if (xl == xl) return xl;
-  bool p = !is_absent(xl);
-  for (int64_t d = d1 - 2; d >= d0; d -= HALO_WALK) {
-    double xs[HALO_WALK];
-#pragma unroll
-    for (int u = 0; u < HALO_WALK; ++u) xs[u] = d - u >= d0 ? P[(d - u) * N + a] : absent_val();
-#pragma unroll
-    for (int u = 0; u < HALO_WALK; ++u) {
-      if (xs[u] == xs[u]) return xs[u];
-      p |= !is_absent(xs[u]);
-    }
-  }
-  return p ? qnan() : absent_val();
-}
-
 // The halo months' and the forward months' prices, one thread per (asset, month): PMh[j][N],
 // j < H halo month j, j = H + f forward month f < F.  A wave whose lanes walk a month back (no
 // price on its last day: listings, delistings, absent months) does not hold up the others.
@@ -2517,7 +2743,8 @@ static int signal_launch(csm_ctx* ctx, const char* who, const double* P, int64_t
                          int64_t N, const int64_t* month_start, int32_t T_m,
                          int32_t max_month_days, int32_t J, int32_t skip, double* PM, double* R,
                          double* M, double* NR, const double* carry, const double* next_pm,
-                         double* carry_out, bool sh = false, uint16_t* ids = nullptr) {
+                         double* carry_out, bool sh = false, uint16_t* ids = nullptr,
+                         const HaloArgs* halo = nullptr) {
   int r = prep(ctx);
   if (r) return r;
   // (a shard pass starts from an empty state, or -- the halo pass -- from the halo's carry
@@ -2546,7 +2773,9 @@ static int signal_launch(csm_ctx* ctx, const char* who, const double* P, int64_t
                                (g_tune_signal_bwf == 0 && N >= (int64_t)SIGNAL_BWF_MIN_N));
   const int bw = wide4 ? 4 : 1;
   const size_t lds = (size_t)W * 64 * vec * bw * sizeof(double) +
-                     (sh ? (size_t)3 * 64 * vec * bw * sizeof(int) : 0);
+                     (sh ? (size_t)3 * 64 * vec * bw * sizeof(int) : 0) +
+                     (halo ? (size_t)HALO_BATCH * 64 * vec * bw * sizeof(double) +
+                             (size_t)bw * HALO_BATCH * 128 * sizeof(uint16_t) : 0);
   const unsigned blocks = (unsigned)((N / vec + 64 * bw - 1) / (64 * bw));
   const void* fn = nullptr;
   // one-wave blocks, four month buffers: 23 / 24 / 32 day rows (the longest month)
@@ -2558,7 +2787,14 @@ static int signal_launch(csm_ctx* ctx, const char* who, const double* P, int64_t
   // (8-way halo rank: shard kernel 0.237 -> 0.231 ms; the full C4 pass measured 0.3 % slower
   // with it, so the one-GPU kernel keeps the runtime J)
   const bool j12 = sh && J == 12 && g_tune_signal_j12;
-  if (wide4 && j12)
+  if (halo && !(sh && wide4))
+    return set_err(ctx, CSM_E_INVAL, "%s: the fused halo prologue runs in the wide shard kernel "
+                   "(even N >= %d, months of <= 23 days); use csm_shard_halo + "
+                   "csm_signal_shard_halo", who, SIGNAL_BWF_MIN_N);
+  if (halo)
+    fn = j12 ? (const void*)k_signal<23, 2, 2, 4, true, true, 12, true>
+             : (const void*)k_signal<23, 2, 2, 4, true, true, 0, true>;
+  else if (wide4 && j12)
     fn = (const void*)k_signal<23, 2, 2, 4, true, true, 12>;
   else if (wide4)
     fn = sh ? (const void*)k_signal<23, 2, 2, 4, true, true> : (const void*)k_signal<23, 2, 2, 4, false, true>;
@@ -2572,9 +2808,10 @@ static int signal_launch(csm_ctx* ctx, const char* who, const double* P, int64_t
   {
     int T_m_ = T_m, J_ = J, skip_ = skip;
     int64_t N_ = N, T_d_ = T_d;
+    HaloArgs ha = halo ? *halo : HaloArgs{0, 0, 0, 0, nullptr};
     void* args[] = {(void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_, (void*)&PM, (void*)&R,
                     (void*)&M, (void*)&NR, (void*)&carry, (void*)&next_pm, (void*)&carry_out, &T_d_,
-                    (void*)&ids};
+                    (void*)&ids, (void*)&ha};
     HIP_CHECK(ctx, hipLaunchKernel(fn, dim3(blocks), dim3(64 * bw), args, lds, ctx->stream));
   }
   LAUNCH_CHECK(ctx, who);
@@ -3022,6 +3259,21 @@ int csm_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
   return CSM_OK;
 }
 
+int csm_signal_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                    const int64_t* month_start, int32_t H, int32_t T_m, int32_t F, int32_t before,
+                    int32_t after, int32_t max_month_days, int32_t J, int32_t skip, double* PM,
+                    double* R, double* M, double* NR, double* state, uint16_t* ids,
+                    uint8_t* flags) {
+  if (!flags || H < 0 || F < 0 || F > 8 || J + skip > 64)
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_halo: bad arguments (flags [N], H >= 0, "
+                   "0 <= F <= 8, J + skip <= 64)");
+  if (ids && ((N % 4) != 0 || ((uintptr_t)ids & 7u) != 0))
+    return set_err(ctx, CSM_E_INVAL, "csm_signal_halo: ids need N %% 4 == 0, 8-B alignment");
+  const HaloArgs ha{H, F, before ? 1 : 0, after ? 1 : 0, flags};
+  return signal_launch(ctx, "csm_signal_halo", P, T_d, N, month_start, T_m, max_month_days, J,
+                       skip, PM, R, M, NR, nullptr, nullptr, state, true, ids, &ha);
+}
+
 int csm_signal_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                           const int64_t* month_start, int32_t T_m, int32_t max_month_days,
                           int32_t J, int32_t skip, const double* carry, const double* next_pm,
@@ -3111,6 +3363,38 @@ int csm_shard_repair_cols(csm_ctx* ctx, const double* P, const int64_t* month_st
                      dim3(REPAIR_THREADS), lds, ctx->stream, PM, P, month_start, T_m, N, J, skip,
                      carry, next_pm, state, R, M, NR, ids, fcarry, idx, count, cap);
   LAUNCH_CHECK(ctx, "k_shard_repair (columns)");
+  return CSM_OK;
+}
+
+int csm_shard_fix_cols(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                       const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                       const double* records, int32_t G, int32_t g, const int32_t* idx,
+                       const int32_t* count, int64_t cap, double* R, double* M, double* NR,
+                       uint16_t* ids) {
+  int r = prep(ctx);
+  if (r) return r;
+  const int W = J + skip;
+  const size_t lds = (size_t)(T_m + 2 * W + 2 + (size_t)G * (SUM_SCALARS + W + 1)) * sizeof(double);
+  if (!P || !month_start || !PM || !records || !idx || !count || !M || !NR || N <= 0 ||
+      T_m < 1 || cap < 1 || cap > 0x7FFFFFFF || G < 1 || g < 0 || g >= G || J < 1 || skip < 0 ||
+      W > 128 || G > HALO_MAXG || lds > 65536)
+    return set_err(ctx, CSM_E_INVAL, "csm_shard_fix_cols: bad arguments (J + skip <= 128, "
+                   "0 <= g < G <= %d, months, rings and records within 64 KB of LDS)", HALO_MAXG);
+  // a workgroup per listed column, at most two per CU (the list is short; the rest exit at once)
+  const int64_t grid = cap < 2 * (int64_t)ctx->n_cu ? cap : 2 * (int64_t)ctx->n_cu;
+  // (C4's look-back J = 12, skip = 1: the ring in registers and the product length fixed)
+  const void* fn = (J == 12 && skip == 1) ? (const void*)k_shard_fix_cols<13, 12>
+                                          : (const void*)k_shard_fix_cols<0, 0>;
+  {
+    int T_m_ = T_m, J_ = J, skip_ = skip, G_ = G, g_ = g;
+    int64_t N_ = N, cap_ = cap;
+    void* args[] = {(void*)&PM, (void*)&P, (void*)&month_start, &T_m_, &N_, &J_, &skip_,
+                    (void*)&records, &G_, &g_, (void*)&R, (void*)&M, (void*)&NR, (void*)&ids,
+                    (void*)&idx, (void*)&count, &cap_};
+    HIP_CHECK(ctx, hipLaunchKernel(fn, dim3((unsigned)grid), dim3(COLS_THREADS), args, lds,
+                                   ctx->stream));
+  }
+  LAUNCH_CHECK(ctx, "k_shard_fix_cols");
   return CSM_OK;
 }
 

@@ -203,12 +203,18 @@ class DateShardPipeline:
         if H != min(self.halo, m0) or F != min(self.fwd, rest):
             raise ValueError(f"rank {self.rank}: P holds {H} halo / {F} forward months, the "
                              f"pipeline expects {min(self.halo, m0)} / {min(self.fwd, rest)}")
-        carry_h, npm_h, flags = st.shard_halo(P, month_start, H, F, J, s, before=m0 > H,
-                                              after=rest > F)
         msh = month_start[H:H + T_m + 1]
         ids = _shard_ids(st, P, msh)
-        PM, _, M, NR, state = st.signal_shard_halo(P, msh, max_month_days, J, s, carry_h, npm_h,
-                                                   **({} if ids is None else {"ids": ids}))
+        kw = {} if ids is None else {"ids": ids}
+        if _halo_fused(st, P.shape[1], max_month_days):   # one launch: halo prologue + shard
+            carry_h = None
+            PM, _, M, NR, state, flags = st.signal_halo(P, month_start, H, F, max_month_days, J,
+                                                        s, before=m0 > H, after=rest > F, **kw)
+        else:
+            carry_h, npm_h, flags = st.shard_halo(P, month_start, H, F, J, s, before=m0 > H,
+                                                  after=rest > F)
+            PM, _, M, NR, state = st.signal_shard_halo(P, msh, max_month_days, J, s, carry_h,
+                                                       npm_h, **kw)
         self.last_count = None
         if self.G > 1:
             cap = self.fallback_cap(N)
@@ -219,13 +225,23 @@ class DateShardPipeline:
             idx, cnt = st.shard_union(masks, N, cap)
             rec = st.shard_summary_cols(PM, state, idx, cnt, J, s)
             recs = self.gather(rec)                                    # collective 1b
-            carry_u, npm_u = st.fold_carry(recs, self.rank, J, s)
-            st.shard_repair_cols(PM, carry_u, npm_u, carry_h, state, idx, cnt, M, NR, J, s,
-                                 **({} if ids is None else {"ids": ids}))
+            self._fix_cols(PM, recs, carry_h, state, idx, cnt, M, NR, ids)
             self.last_count = (cnt, cap)
             if check and int(cnt.max().item()) > cap:   # every rank sees the same list
                 return self._run_allgather_fallback(P, month_start, H, F, max_month_days)
         return self._rank_and_gather(M, NR, ids)
+
+    def _fix_cols(self, PM, recs, carry_h, state, idx, cnt, M, NR, ids):
+        """The listed columns from the all-gathered records: fold + replay in one launch
+        (shard_fix_cols), or -- stages without it (the CPU oracle stages) -- fold_carry then
+        shard_repair_cols."""
+        st, J, s = self.st, self.J, self.skip
+        kw = {} if ids is None else {"ids": ids}
+        if hasattr(st, "shard_fix_cols"):
+            st.shard_fix_cols(PM, recs, self.rank, state, idx, cnt, M, NR, J, s, **kw)
+        else:
+            carry_u, npm_u = st.fold_carry(recs, self.rank, J, s)
+            st.shard_repair_cols(PM, carry_u, npm_u, carry_h, state, idx, cnt, M, NR, J, s, **kw)
 
     def _run_allgather_fallback(self, P, month_start, H, F, max_month_days):
         """The halo pass's list overflowed its width: the speculative all-gather pass on the
@@ -317,13 +333,20 @@ def halo_slices(month_start_host, G, H, fwd=None):
     return out
 
 
+def _halo_fused(stages, N, max_month_days):
+    """Whether the halo pass takes csm_signal_halo (halo prologue in the shard kernel)."""
+    return hasattr(stages, "signal_halo") and stages.halo_fused_ok(N, max_month_days)
+
+
 def virtual_shards_halo(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, H=None,
-                        cap=None):
+                        cap=None, fold_repair=False, fused_halo=True):
     """The halo pass's G-shard decomposition run sequentially on ONE device (the collectives
     replaced by stacks): every shard's halo state, fused pass, need mask, the union list, the
     listed records, fold and repair -- for single-GPU verification that a G-GPU halo run equals
     the 1-GPU run bit for bit.  Returns (M, NR, L, EW, CNT, LS, count) with count the union
-    list's length."""
+    list's length.  fold_repair: the listed columns by fold_carry + shard_repair_cols (the
+    convergence-tested repair) instead of the one-launch shard_fix_cols.  fused_halo=False:
+    shard_halo + signal_shard_halo even where signal_halo takes the panel."""
     import numpy as np
     H = halo_months(J, skip) if H is None else int(H)
     ms = np.asarray(month_start_host, dtype=np.int64)
@@ -334,13 +357,20 @@ def virtual_shards_halo(stages, P, month_start_host, G, J=12, skip=1, n_bins=10,
     for (d0, d1, hm, F, h0, m0, m1) in halo_slices(ms, G, H):
         Pg = P[d0:d1].contiguous()
         msg = torch.from_numpy(ms[h0:m1 + F + 1] - d0).to(dev)
-        carry_h, npm_h, flags = stages.shard_halo(Pg, msg, hm, F, J, skip, before=h0 > 0,
-                                                  after=m1 + F < len(ms) - 1)
         msh = msg[hm:hm + (m1 - m0) + 1]
         maxd = int(np.diff(ms[m0:m1 + 1]).max()) if m1 > m0 else 1
         ids = _shard_ids(stages, Pg, msh)
-        PM, _, M, NR, state = stages.signal_shard_halo(Pg, msh, maxd, J, skip, carry_h, npm_h,
-                                                       **({} if ids is None else {"ids": ids}))
+        kw = {} if ids is None else {"ids": ids}
+        if fused_halo and not fold_repair and _halo_fused(stages, N, maxd):
+            carry_h = None
+            PM, _, M, NR, state, flags = stages.signal_halo(Pg, msg, hm, F, maxd, J, skip,
+                                                            before=h0 > 0,
+                                                            after=m1 + F < len(ms) - 1, **kw)
+        else:
+            carry_h, npm_h, flags = stages.shard_halo(Pg, msg, hm, F, J, skip, before=h0 > 0,
+                                                      after=m1 + F < len(ms) - 1)
+            PM, _, M, NR, state = stages.signal_shard_halo(Pg, msh, maxd, J, skip, carry_h,
+                                                           npm_h, **kw)
         sh.append((PM, M, NR, state, ids, carry_h, flags))
     masks = torch.stack([stages.shard_need(x[6], x[3], min(H, m1))
                          for x, (_, _, _, _, _, _, m1) in zip(sh, halo_slices(ms, G, H))])
@@ -351,9 +381,13 @@ def virtual_shards_halo(stages, P, month_start_host, G, J=12, skip=1, n_bins=10,
     recs = torch.stack([stages.shard_summary_cols(x[0], x[3], idx, cnt, J, skip) for x in sh])
     Ms, NRs, Ls, EWs, CNTs = [], [], [], [], []
     for g, (PM, M, NR, state, ids, carry_h, _) in enumerate(sh):
-        carry_u, npm_u = stages.fold_carry(recs, g, J, skip)
-        stages.shard_repair_cols(PM, carry_u, npm_u, carry_h, state, idx, cnt, M, NR, J, skip,
-                                 **({} if ids is None else {"ids": ids}))
+        kw = {} if ids is None else {"ids": ids}
+        if hasattr(stages, "shard_fix_cols") and not fold_repair:
+            stages.shard_fix_cols(PM, recs, g, state, idx, cnt, M, NR, J, skip, **kw)
+        else:
+            carry_u, npm_u = stages.fold_carry(recs, g, J, skip)
+            stages.shard_repair_cols(PM, carry_u, npm_u, carry_h, state, idx, cnt, M, NR, J, skip,
+                                     **kw)
         if ids is not None:
             L, EW, CNT, _ = stages.deciles_ids(M, NR, ids, n_bins)
         else:

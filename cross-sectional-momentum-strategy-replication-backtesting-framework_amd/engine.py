@@ -909,6 +909,32 @@ class Engine:
                    _ptr(R), _ptr(M), _ptr(NR), _ptr(state), _ptr(ids))
         return PM, R, M, NR, ShardState(state, P, month_start)
 
+    @staticmethod
+    def halo_fused_ok(N, max_month_days):
+        """Whether csm_signal_halo (the halo prologue inside the wide shard kernel) takes this
+        panel: even N >= 92160 (the four-wave blocks), months of <= 23 day rows."""
+        return N % 2 == 0 and 92160 <= N < (1 << 31) // 256 and max_month_days <= 23
+
+    def signal_halo(self, P, month_start, H, F, max_month_days, J, skip, before=True, after=True,
+                    with_ret=False, ids=None):
+        """csm_signal_halo: shard_halo + signal_shard_halo in one launch (halo_fused_ok
+        panels).  month_start [H + T_m + F + 1] as shard_halo's.  Returns (PM, R, M, NR,
+        ShardState, flags) -- ShardState on the shard's month offsets, flags shard_halo's."""
+        T_d, N = P.shape
+        T_m = month_start.numel() - 1 - H - F
+        _need(P, "P", torch.float64, (T_d, N), self.device)
+        _need(month_start, "month_start", torch.int64, (H + T_m + F + 1,), self.device)
+        PM, M, NR = self.empty((T_m, N)), self.empty((T_m, N)), self.empty((T_m, N))
+        R = self.empty((T_m, N)) if with_ret else None
+        state = self.empty((5, N))
+        flags = self.empty((N,), torch.uint8)
+        if ids is not None:
+            _need(ids, "ids", torch.int16, (T_m, N), self.device)
+        self._call("csm_signal_halo", _ptr(P), T_d, N, _ptr(month_start), int(H), int(T_m), int(F),
+                   int(bool(before)), int(bool(after)), int(max_month_days), int(J), int(skip),
+                   _ptr(PM), _ptr(R), _ptr(M), _ptr(NR), _ptr(state), _ptr(ids), _ptr(flags))
+        return PM, R, M, NR, ShardState(state, P, month_start[H:H + T_m + 1]), flags
+
     def shard_need(self, flags, state, H, out=None):
         """csm_shard_need -> int64 [4][ceil(N / 64)]: this rank's exchange bits (H = the halo
         length the next rank holds)."""
@@ -954,6 +980,25 @@ class Engine:
                    T_m, N, int(J), int(skip), _ptr(carry), _ptr(next_pm), _ptr(fcarry),
                    _ptr(state.t), _ptr(idx), _ptr(cnt), cap, _ptr(R), _ptr(M), _ptr(NR),
                    _ptr(ids))
+        return M, NR
+
+    def shard_fix_cols(self, PM, records, g, state, idx, cnt, M, NR, J, skip, R=None, ids=None):
+        """csm_shard_fix_cols: fold the listed columns' all-gathered records [G][S][cap] (this
+        rank g) and replay every month of each listed column from its true carry, in one launch
+        (the halo pass's fold_carry + shard_repair_cols)."""
+        T_m, N = PM.shape
+        G, S, cap = records.shape
+        if S != 6 + J + skip + 1:
+            raise ValueError(f"records have {S} rows, expected {6 + J + skip + 1}")
+        _need(records, "records", torch.float64, (G, S, cap), self.device)
+        _need(idx, "idx", torch.int32, (cap,), self.device)
+        _need(M, "M", torch.float64, (T_m, N), self.device)
+        _need(NR, "NR", torch.float64, (T_m, N), self.device)
+        if ids is not None:
+            _need(ids, "ids", torch.int16, (T_m, N), self.device)
+        self._call("csm_shard_fix_cols", _ptr(state.P), _ptr(state.month_start), _ptr(PM),
+                   T_m, N, int(J), int(skip), _ptr(records), G, int(g), _ptr(idx), _ptr(cnt), cap,
+                   _ptr(R), _ptr(M), _ptr(NR), _ptr(ids))
         return M, NR
 
     def sync(self):

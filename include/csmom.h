@@ -372,11 +372,27 @@ int csm_shard_repair_ids(csm_ctx* ctx, const double* P, const int64_t* month_sta
  *   with csm_fold_carry (N = cap), and:
  * csm_shard_repair_cols: csm_shard_repair of the listed assets, their carry / next_pm columns
  *   from that fold ([.][cap]); fcarry = this rank's halo carry (the state the pass started from).
+ * csm_shard_fix_cols: the fold and the repair of the listed columns in ONE launch (the halo
+ *   pass's default): records = the all-gathered [G][S][cap] records, g = this rank; each listed
+ *   column's true carry and forward price are folded from them and every month of the column
+ *   is replayed from that carry (the sequential scan: the unsharded pass's R / M / NR / ids).
  */
 int csm_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                    const int64_t* month_start, int32_t H, int32_t T_m, int32_t F,
                    int32_t before, int32_t after, int32_t J, int32_t skip, double* halo_pm,
                    double* carry, double* next_pm, uint8_t* flags);
+/*
+ * csm_signal_halo: csm_shard_halo + csm_signal_shard_halo in ONE launch (the wide shard kernel:
+ * even N >= 92160, months of <= 23 day rows; else CSM_E_INVAL -- take the two calls): P and
+ * month_start [H + T_m + F + 1] as csm_shard_halo's; the halo state, the forward price and
+ * flags [N] (csm_shard_halo's) come from the kernel's prologue, the shard's PM / R / M / NR /
+ * state / ids are csm_signal_shard_halo's, bit for bit.
+ */
+int csm_signal_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
+                    const int64_t* month_start, int32_t H, int32_t T_m, int32_t F, int32_t before,
+                    int32_t after, int32_t max_month_days, int32_t J, int32_t skip, double* PM,
+                    double* R, double* M, double* NR, double* state, uint16_t* ids,
+                    uint8_t* flags);
 int csm_signal_shard_halo(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
                           const int64_t* month_start, int32_t T_m, int32_t max_month_days,
                           int32_t J, int32_t skip, const double* carry, const double* next_pm,
@@ -395,6 +411,11 @@ int csm_shard_repair_cols(csm_ctx* ctx, const double* P, const int64_t* month_st
                           const double* carry, const double* next_pm, const double* fcarry,
                           const double* state, const int32_t* idx, const int32_t* count,
                           int64_t cap, double* R, double* M, double* NR, uint16_t* ids);
+int csm_shard_fix_cols(csm_ctx* ctx, const double* P, const int64_t* month_start,
+                       const double* PM, int32_t T_m, int64_t N, int32_t J, int32_t skip,
+                       const double* records, int32_t G, int32_t g, const int32_t* idx,
+                       const int32_t* count, int64_t cap, double* R, double* M, double* NR,
+                       uint16_t* ids);
 
 /*
  * Portfolio accounting beyond the reference's K = 1 equal-weight case (SURVEY 8(f) rank 2;

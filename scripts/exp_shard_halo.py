@@ -10,6 +10,7 @@ Times, interleaved (median of `reps`): the halo pass, the speculative all-gather
 shard alone; per-stage HIP events of the halo pass; |U| (the assets this rank lists).
 Prints one JSON line.  Usage: exp_shard_halo.py [N] [days_per_rank] [reps] [G] [split_cells]"""
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -76,10 +77,17 @@ def main():
     def halo(ev=None):
         rec = (lambda i: ev[i].record()) if ev else (lambda i: None)
         rec(0)
-        carry_h, npm_h, flags = eng.shard_halo(P, ms, hp.H, hp.F, J, skip, before=True,
-                                               after=True)
-        rec(1)
-        PM, _, M, NR, st = eng.signal_shard_halo(P, msh, maxd, J, skip, carry_h, npm_h, ids=IDS)
+        if os.environ.get("CSM_HALO_SPLIT"):   # A/B: round 5's two launches
+            carry_h, npm_h, flags = eng.shard_halo(P, ms, hp.H, hp.F, J, skip, before=True,
+                                                   after=True)
+            rec(1)
+            PM, _, M, NR, st = eng.signal_shard_halo(P, msh, maxd, J, skip, carry_h, npm_h,
+                                                     ids=IDS)
+        else:   # the halo prologue inside the shard kernel (csm_signal_halo)
+            carry_h = None
+            rec(1)
+            PM, _, M, NR, st, flags = eng.signal_halo(P, ms, hp.H, hp.F, maxd, J, skip,
+                                                      ids=IDS)
         rec(2)
         mask = eng.shard_need(flags, st, H)
         masks = torch.stack([other[0], mask, other[2]])   # the 3 ranks' bits (the union's input)
@@ -88,8 +96,12 @@ def main():
         rcd = eng.shard_summary_cols(PM, st, idx, cnt, J, skip)
         recs = torch.stack([rcd] * G)
         rec(4)
-        carry_u, npm_u = eng.fold_carry(recs, 1, J, skip)
-        eng.shard_repair_cols(PM, carry_u, npm_u, carry_h, st, idx, cnt, M, NR, J, skip, ids=IDS)
+        if os.environ.get("CSM_FOLD_REPAIR") and carry_h is not None:   # A/B: round 5's repair
+            carry_u, npm_u = eng.fold_carry(recs, 1, J, skip)
+            eng.shard_repair_cols(PM, carry_u, npm_u, carry_h, st, idx, cnt, M, NR, J, skip,
+                                  ids=IDS)
+        else:
+            eng.shard_fix_cols(PM, recs, 1, st, idx, cnt, M, NR, J, skip, ids=IDS)
         rec(5)
         L, EW, CNT, _ = eng.deciles_ids(M, NR, IDS, nb)
         rec(6)
@@ -134,7 +146,7 @@ def main():
         t2 = time.perf_counter()
         pipelined.append(1e3 * (t2 - t0) / 20)
         enqueue.append(1e3 * (t1 - t0) / 20)
-    names = ["shard_halo", "signal_shard_halo", "need+union", "summary_cols", "fold+repair_cols",
+    names = ["shard_halo", "signal_shard_halo", "need+union", "summary_cols", "fix_cols",
              "deciles_ids", "gather_emul+long_short"]
     st_ms = {n: [] for n in names}
     for _ in range(reps):
@@ -163,7 +175,7 @@ def main():
         diag = dict(diag.most_common(12))
     print(json.dumps({
         "diag": diag,
-        "N": N, "days_per_rank": dpr, "split_cells": cells or 16384,
+        "N": N, "days_per_rank": dpr, "split_cells": cells or 32768,
         "dec_split": __import__("os").environ.get("CSM_DEC_SPLIT", "default (2: auto)"),
         "tune": __import__("os").environ.get("CSM_TUNE", ""), "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
         "F": hp.F, "G_emulated": G, "cap": cap, "listed_this_rank": int(cnt.item()),

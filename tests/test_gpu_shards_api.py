@@ -367,13 +367,14 @@ def test_halo_shards_long_windows(engine, J, skip, G):
 
 @pytest.mark.parametrize("G", [2, 7])
 @pytest.mark.parametrize("H", [None, 0, 2])
-@pytest.mark.parametrize("cols_wg", [1, 0])
-def test_halo_shards_sparse_panel(engine, G, H, cols_wg):
+@pytest.mark.parametrize("cols_wg,fold_repair", [(1, False), (1, True), (0, True)])
+def test_halo_shards_sparse_panel(engine, G, H, cols_wg, fold_repair):
     """Gappy panel (25 % absent months, 15 % NaN months): most assets are flagged and go
     through the exchange; H = 0 (no halo at all) and H = 2 (shorter than the window) flag
-    every asset with history -- still bit for bit.  The listed columns' summary and repair one
-    workgroup per column (month prices derived together into LDS; the default) and one thread
-    per column (tune cols_wg 0)."""
+    every asset with history -- still bit for bit.  The listed columns' fold and replay in one
+    launch (shard_fix_cols, the default), and the fold + convergence-tested repair with the
+    summary and repair one workgroup per column (month prices derived together into LDS) or one
+    thread per column (tune cols_wg 0)."""
     from oracle.synth_np import make_panel
     from csmom.distributed import virtual_shards_halo
     pan = make_panel(512, 2600, seed=11, nan_day=0.05, absent_month=0.25, nan_month=0.15,
@@ -383,7 +384,7 @@ def test_halo_shards_sparse_panel(engine, G, H, cols_wg):
     lib = engine.lib
     try:
         assert lib.csm_tune(b"cols_wg", cols_wg) == 0
-        res = virtual_shards_halo(engine, P, ms, G, 12, 1, 10, H=H)
+        res = virtual_shards_halo(engine, P, ms, G, 12, 1, 10, H=H, fold_repair=fold_repair)
     finally:
         lib.csm_tune(b"cols_wg", 1)
     cnt = _halo_equal(out, res, ew=False)
@@ -465,3 +466,51 @@ def test_halo_flags_and_union(engine):
     # one rank alone: no rank before or after it, so nothing needs the exchange
     idx, cnt = engine.shard_union(engine.shard_need(flags, st, H)[None], N, 2)
     assert int(cnt.item()) == 0
+
+
+@pytest.fixture(scope="module")
+def wide_gappy():
+    """A panel wide enough for the four-wave shard kernel (and so the fused halo prologue), with
+    late listings, delistings, NaN days, absent and all-NaN months (walks back in the halo)."""
+    from oracle.synth_np import make_panel
+    pan = make_panel(96_000, 1_300, seed=23, with_volume=False, late=0.1, delist=0.1,
+                     nan_day=0.03, absent_month=0.05, nan_month=0.05, cents=True)
+    return _up(pan["P"]), pan["month_start"].astype(np.int64)
+
+
+@pytest.mark.parametrize("G", [3, 8])
+def test_fused_halo_prologue_equals_two_launches(engine, wide_gappy, G):
+    """csm_signal_halo (the halo months' prices, state and flags computed in the shard kernel's
+    prologue) against csm_shard_halo + csm_signal_shard_halo on every rank of a G-way split:
+    flags, PM, M, NR, ids and the end-state record bit for bit; and the whole virtual halo pass
+    (fused prologue + shard_fix_cols) against the two-launch pass with the convergence repair
+    and against the one-GPU pipeline: M, NR, labels, counts, decile means and long-short."""
+    from csmom.distributed import halo_months, halo_slices, virtual_shards_halo
+    P, ms = wide_gappy
+    N = P.shape[1]
+    J, skip = 12, 1
+    H = halo_months(J, skip)
+    for (d0, d1, hm, F, h0, m0, m1) in halo_slices(ms, G, H):
+        Pg = P[d0:d1].contiguous()
+        msg = torch.from_numpy(ms[h0:m1 + F + 1] - d0).to("cuda:0")
+        msh = msg[hm:hm + (m1 - m0) + 1]
+        maxd = int(np.diff(ms[m0:m1 + 1]).max())
+        assert engine.halo_fused_ok(N, maxd)
+        before, after = h0 > 0, m1 + F < len(ms) - 1
+        ids_a = engine.empty((m1 - m0, N), torch.int16)
+        ids_b = engine.empty((m1 - m0, N), torch.int16)
+        carry, npm, fl_b = engine.shard_halo(Pg, msg, hm, F, J, skip, before=before, after=after)
+        PMb, _, Mb, NRb, stb = engine.signal_shard_halo(Pg, msh, maxd, J, skip, carry, npm,
+                                                        ids=ids_b)
+        PMa, _, Ma, NRa, sta, fl_a = engine.signal_halo(Pg, msg, hm, F, maxd, J, skip,
+                                                        before=before, after=after, ids=ids_a)
+        assert torch.equal(fl_a, fl_b)
+        for x, y in ((PMa, PMb), (Ma, Mb), (NRa, NRb), (sta.t, stb.t)):
+            assert bits_equal(x.cpu().numpy(), y.cpu().numpy())
+        assert torch.equal(ids_a, ids_b)
+    out = engine.pipeline(P, _up(ms), J, skip, 10)
+    a = virtual_shards_halo(engine, P, ms, G, J, skip, 10)
+    b = virtual_shards_halo(engine, P, ms, G, J, skip, 10, fold_repair=True, fused_halo=False)
+    assert a[6] > 0   # listed columns went through shard_fix_cols
+    for res in (a, b):
+        _halo_equal(out, res)
