@@ -1415,6 +1415,9 @@ __global__ __launch_bounds__(64 * TM_WAVES) void k_turnover_ew_mask(
 // are the same bits.  Rows that are not all-full go onto the general launch's work list as the
 // per-row launch's ids (tb * Ct + c).
 #define TO_MAXG 4
+#ifndef VWG_U
+#define VWG_U 1   // cells per lane in flight in k_turnover_vwg (2 / 4 measured slower: C3 portfolio 0.241 -> 0.266 / 0.342 ms)
+#endif
 template <bool IMP>
 __global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
     const int8_t* __restrict__ L, const double* __restrict__ W, int T_m, int B, int64_t N,
@@ -1453,27 +1456,46 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
   for (int g = 0; g < TO_MAXG; ++g)
 #pragma unroll
     for (int q = 0; q < TO_MAXQ; ++q) { turn[g][q] = 0.0; cost[g][q] = 0.0; }
-  for (int64_t a = a0 + tid; a < a1; a += PF_THREADS) {
-    // every load of the cell first: weights / ADV / vol once, then each row's labels
-    double x1, x0[TO_MAXQ], adv = 0.0, sg = 0.02;
-    int l1[TO_MAXG], l0[TO_MAXG][TO_MAXQ];
-    x1 = W[rtw + a];
+  // VWG_U cells of a lane in flight (every load of them first), then charged in the lane's cell
+  // order: the same per-lane sums as one cell at a time (the row is one latency chain per trip,
+  // and a C3 launch is ~1 workgroup per CU)
+  for (int64_t ab = a0 + tid; ab < a1; ab += VWG_U * PF_THREADS) {
+    double x1u[VWG_U], x0u[VWG_U][TO_MAXQ], advu[VWG_U], sgu[VWG_U];
+    int l1u[VWG_U][TO_MAXG], l0u[VWG_U][TO_MAXG][TO_MAXQ];
 #pragma unroll
-    for (int q = 0; q < TO_MAXQ; ++q)
-      x0[q] = q < nq ? W[rtw - (int64_t)ks.K[q] * pa.mw + a] : 1.0;
-    if (IMP) {
-      adv = ADV[rtw + a];
-      if (SIG) sg = SIG[rtw + a];
-    }
-#pragma unroll
-    for (int g = 0; g < TO_MAXG; ++g) {
-      const bool on = g < G && ((act >> g) & 1u);
-      const int64_t rt = pa.lrow(t, g * Bg + p);
-      l1[g] = on ? (int)L[rt + a] : -1;
+    for (int u = 0; u < VWG_U; ++u) {
+      const int64_t a = ab + (int64_t)u * PF_THREADS;
+      const bool in = a < a1;
+      const int64_t ai = in ? a : a0;
+      // every load of the cell first: weights / ADV / vol once, then each row's labels
+      x1u[u] = W[rtw + ai];
 #pragma unroll
       for (int q = 0; q < TO_MAXQ; ++q)
-        l0[g][q] = (on && q < nq) ? (int)L[rt - (int64_t)ks.K[q] * pa.ml + a] : -1;
+        x0u[u][q] = q < nq ? W[rtw - (int64_t)ks.K[q] * pa.mw + ai] : 1.0;
+      advu[u] = 0.0;
+      sgu[u] = 0.02;
+      if (IMP) {
+        advu[u] = ADV[rtw + ai];
+        if (SIG) sgu[u] = SIG[rtw + ai];
+      }
+#pragma unroll
+      for (int g = 0; g < TO_MAXG; ++g) {
+        const bool on = g < G && ((act >> g) & 1u);
+        const int64_t rt = pa.lrow(t, g * Bg + p);
+        l1u[u][g] = on ? (int)L[rt + ai] : -1;
+#pragma unroll
+        for (int q = 0; q < TO_MAXQ; ++q)
+          l0u[u][g][q] = (on && q < nq) ? (int)L[rt - (int64_t)ks.K[q] * pa.ml + ai] : -1;
+      }
     }
+#pragma unroll
+    for (int u = 0; u < VWG_U; ++u) {
+    if (ab + (int64_t)u * PF_THREADS >= a1) break;
+    const double x1 = x1u[u];
+    const double* x0 = x0u[u];
+    const double adv = advu[u], sg = sgu[u];
+    const int* l1 = l1u[u];
+    const int (*l0)[TO_MAXQ] = l0u[u];
     const double vw1 = valid_w(x1);
     const double unit_sig = sg == sg ? sg : 0.02;
     const double sra = (IMP && adv > 0.0) ? sqrt(aum / adv) : -1.0;
@@ -1505,6 +1527,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
           }
         }
       }
+    }
     }
   }
   __shared__ double red[TO_MAXG][PF_WAVES][2 * TO_MAXQ];
