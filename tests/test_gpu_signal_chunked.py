@@ -80,7 +80,8 @@ def test_gappy_panels_every_chunking(engine, N, T, J, skip, C):
 @pytest.mark.parametrize("name", ["edge", "c1", "small", "real_data", "longwin"])
 def test_fixtures(engine, name):
     """The reference-generated fixtures (tests/golden): M / NR of every tag with J + skip <= 32
-    bit for bit (odd N padded with an absent column, which changes no other asset)."""
+    bit for bit (odd N padded with an absent column, which changes no other asset); fixtures
+    that keep sampled cells and a digest of the whole panel (C1) are checked through both."""
     z = load_golden(name)
     P = z["P"]
     ms_h = z["month_start"].astype(np.int64)
@@ -95,14 +96,26 @@ def test_fixtures(engine, name):
     maxd = int(np.diff(ms_h).max())
     tags = golden_tags(z)
     done = 0
+    import hashlib
+    dig = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    canon = lambda a: np.where(np.isnan(a), np.nan, a)   # (pandas' canonical NaN payload)
     for tag in tags:
         J, s = parse_tag(tag)
-        if J + s > 32 or f"{tag}_M" not in z.files:
+        full = f"{tag}_M" in z.files
+        if J + s > 32 or not (full or f"{tag}_M_sha256" in z.files):
             continue
         _, M, NR, _, ws = engine.signal_chunked(Pd, ms, maxd, J, s)
         assert not engine.signal_chunked_timed_out(ws)
-        assert bits_equal(M.cpu().numpy()[:, :N], z[f"{tag}_M"]), tag
-        assert bits_equal(NR.cpu().numpy()[:, :N], z[f"{tag}_NR"]), tag
+        m, nr = M.cpu().numpy()[:, :N], NR.cpu().numpy()[:, :N]
+        if full:
+            assert bits_equal(m, z[f"{tag}_M"]), tag
+            assert bits_equal(nr, z[f"{tag}_NR"]), tag
+        else:
+            idx = z["sample_idx"]
+            assert bits_equal(m.reshape(-1)[idx], z[f"{tag}_M_sample"]), tag
+            assert bits_equal(nr.reshape(-1)[idx], z[f"{tag}_NR_sample"]), tag
+            assert dig(canon(m)) == str(z[f"{tag}_M_sha256"]), tag
+            assert dig(canon(nr)) == str(z[f"{tag}_NR_sha256"]), tag
         done += 1
     if not done:
         pytest.skip("no full-panel tag with J + skip <= 32")
