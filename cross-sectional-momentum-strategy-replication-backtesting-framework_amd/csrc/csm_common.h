@@ -161,6 +161,7 @@ struct DecSplit {
   uint32_t* ulist;   // [T_m][C][SPLIT_WAVES][SPLIT_FL] their cell indices
   int C;             // chunks per row: ceil(N / cells)
   int64_t cells;     // cells per chunk (a multiple of SPLIT_TRIP)
+  int pf;            // the sweep's prefetching variant (no more (chunk, date) pairs than CUs)
 };
 
 // narrow-row decile launcher (deciles_narrow.hip), NB in {0,2,3,4,5,10,20}

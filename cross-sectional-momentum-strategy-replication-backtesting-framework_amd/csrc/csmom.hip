@@ -2515,6 +2515,11 @@ static int g_tune_dec_merge = 1;
 // another fixed order
 static int g_tune_dec_split = 2;
 static int64_t g_tune_dec_split_cells = SPLIT_CELLS;   // cells per split-sweep chunk
+// the split sweep: 0 the two-workgroups-per-CU variant (no prefetch) | 1 the prefetching one
+// workgroup per CU | 2 prefetch when the launch has no more (chunk, date) pairs than CUs.
+// C4 rank rehearsals, deciles_ids ms: 4-way 0.1162 / 0.1338 / 0.1165, 8-way 0.0998 / 0.1019 /
+// 0.1014 (profiles/r06/experiments/split_pf)
+static int g_tune_dec_split_pf = 0;
 // csm_momentum_multi: 2 register shift ring, two assets per lane (even N, aligned) | 1 one asset
 // per lane | 0 the shared-memory ring (max(J) + skip > 16 always takes it)
 static int g_tune_mj_reg = 2;
@@ -2545,6 +2550,7 @@ int csm_tune(const char* key, int value) {
   if (!strcmp(key, "mj_reg") && value >= 0 && value <= 2) { g_tune_mj_reg = value; return CSM_OK; }
   if (!strcmp(key, "dec_narrow_max") && value >= 0) { g_tune_dec_narrow_max = value; return CSM_OK; }
   if (!strcmp(key, "dec_split") && value >= 0 && value <= 2) { g_tune_dec_split = value; return CSM_OK; }
+  if (!strcmp(key, "dec_split_pf") && value >= 0 && value <= 2) { g_tune_dec_split_pf = value; return CSM_OK; }
   if (!strcmp(key, "tc_spins") && value >= 0) { g_tune_tc_spins = (unsigned)value; return CSM_OK; }
   if (!strcmp(key, "dec_split_cells") && value >= SPLIT_TRIP && value % SPLIT_TRIP == 0) {
     g_tune_dec_split_cells = value;
@@ -3001,6 +3007,7 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
       }
       DecSplit sp;
       dsplit_layout(T_m, N, &sp, (char*)ctx->dsplit);
+      sp.pf = g_tune_dec_split_pf == 2 ? (C * T_m <= (int64_t)ctx->n_cu) : g_tune_dec_split_pf;
       int64_t* tm = g_dec_timing;
       double* lsx = NR ? LSw : nullptr;
       int32_t* tkx = lsx ? ctx->ticket : nullptr;

@@ -56,8 +56,12 @@ void launch_deciles_split(int T_m, hipStream_t st, const double* M, const double
   hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, true, false, 1>), dim3(T_m),
                      dim3(DEC_THREADS), 0, st, M, NR, N, nbins, q, L, EW, CNT, NV, tim, ids, flg,
                      (double*)nullptr, (int32_t*)nullptr, sp);
-  hipLaunchKernelGGL((dec_pre::k_dsplit_sweep<NB>), dim3((unsigned)sp.C, (unsigned)T_m),
-                     dim3(SPLIT_THREADS), 0, st, NR, (const uint16_t*)ids, N, L, flg, sp);
+  if (sp.pf)
+    hipLaunchKernelGGL((dec_pre::k_dsplit_sweep<NB, true>), dim3((unsigned)sp.C, (unsigned)T_m),
+                       dim3(SPLIT_THREADS), 0, st, NR, (const uint16_t*)ids, N, L, flg, sp);
+  else
+    hipLaunchKernelGGL((dec_pre::k_dsplit_sweep<NB, false>), dim3((unsigned)sp.C, (unsigned)T_m),
+                       dim3(SPLIT_THREADS), 0, st, NR, (const uint16_t*)ids, N, L, flg, sp);
   // the finish launch: the listed cells of the rows the plan and sweep took, the general path
   // for the rows they left; LS given, its last workgroup forms the long-short
   hipLaunchKernelGGL((dec_pre::k_deciles<NB, true, true, false, false, 2>), dim3(T_m),

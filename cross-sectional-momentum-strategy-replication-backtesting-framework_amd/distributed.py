@@ -18,6 +18,7 @@ CPU tests drive this orchestration with gloo and the oracle).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -206,7 +207,7 @@ class DateShardPipeline:
         msh = month_start[H:H + T_m + 1]
         ids = _shard_ids(st, P, msh)
         kw = {} if ids is None else {"ids": ids}
-        if _halo_fused(st, P.shape[1], max_month_days):   # one launch: halo prologue + shard
+        if _halo_fused(st, P, max_month_days):   # one launch: halo prologue + shard
             carry_h = None
             PM, _, M, NR, state, flags = st.signal_halo(P, month_start, H, F, max_month_days, J,
                                                         s, before=m0 > H, after=rest > F, **kw)
@@ -333,20 +334,31 @@ def halo_slices(month_start_host, G, H, fwd=None):
     return out
 
 
-def _halo_fused(stages, N, max_month_days):
+# csm_signal_halo (the halo prologue inside the shard kernel) is bit for bit the two-launch
+# csm_shard_halo + csm_signal_shard_halo, but its main loop runs slower on long shards (C4
+# ranks, ms: 2-way 0.976 vs 0.086 + 0.873, 4-way 0.527 vs 0.079 + 0.443, 8-way 0.315 vs
+# 0.091 + 0.232), so it is taken for shards of at most HALO_FUSED_MAX_DAYS days (halo and
+# forward months included; CSM_HALO_FUSED_MAX_DAYS, 0 never);
+# profiles/r06/experiments/negative_results.txt
+HALO_FUSED_MAX_DAYS = int(os.environ.get("CSM_HALO_FUSED_MAX_DAYS", "2048"))
+
+
+def _halo_fused(stages, P, max_month_days):
     """Whether the halo pass takes csm_signal_halo (halo prologue in the shard kernel)."""
-    return hasattr(stages, "signal_halo") and stages.halo_fused_ok(N, max_month_days)
+    return (P.shape[0] <= HALO_FUSED_MAX_DAYS and hasattr(stages, "signal_halo")
+            and stages.halo_fused_ok(P.shape[1], max_month_days))
 
 
 def virtual_shards_halo(stages, P, month_start_host, G, J=12, skip=1, n_bins=10, H=None,
-                        cap=None, fold_repair=False, fused_halo=True):
+                        cap=None, fold_repair=False, fused_halo=None):
     """The halo pass's G-shard decomposition run sequentially on ONE device (the collectives
     replaced by stacks): every shard's halo state, fused pass, need mask, the union list, the
     listed records, fold and repair -- for single-GPU verification that a G-GPU halo run equals
     the 1-GPU run bit for bit.  Returns (M, NR, L, EW, CNT, LS, count) with count the union
     list's length.  fold_repair: the listed columns by fold_carry + shard_repair_cols (the
-    convergence-tested repair) instead of the one-launch shard_fix_cols.  fused_halo=False:
-    shard_halo + signal_shard_halo even where signal_halo takes the panel."""
+    convergence-tested repair) instead of the one-launch shard_fix_cols.  fused_halo: True
+    takes csm_signal_halo where it applies, False shard_halo + signal_shard_halo, None the
+    run_halo choice (shards of at most HALO_FUSED_MAX_DAYS days)."""
     import numpy as np
     H = halo_months(J, skip) if H is None else int(H)
     ms = np.asarray(month_start_host, dtype=np.int64)
@@ -361,7 +373,11 @@ def virtual_shards_halo(stages, P, month_start_host, G, J=12, skip=1, n_bins=10,
         maxd = int(np.diff(ms[m0:m1 + 1]).max()) if m1 > m0 else 1
         ids = _shard_ids(stages, Pg, msh)
         kw = {} if ids is None else {"ids": ids}
-        if fused_halo and not fold_repair and _halo_fused(stages, N, maxd):
+        if fused_halo is None:
+            fh = _halo_fused(stages, Pg, maxd)
+        else:
+            fh = fused_halo and stages.halo_fused_ok(N, maxd)
+        if fh and not fold_repair:
             carry_h = None
             PM, _, M, NR, state, flags = stages.signal_halo(Pg, msg, hm, F, maxd, J, skip,
                                                             before=h0 > 0,

@@ -67,7 +67,10 @@ int csm_abi_version(void);
  * bytes), "ls_opt" (1 the one-wave legs label sort's prefix ranks by v_mbcnt | 0 masked
  * popcounts), "dec_split_cells" (cells per chunk of the split decile sweep, default 32768, a
  * multiple of 8192 -- the merged pass's sweep trip -- so the merged and split passes sum every
- * row's decile means in the same order; the split workspace is the context's), "tc_spins" (polling trips a
+ * row's decile means in the same order; the split workspace is the context's), "dec_split_pf"
+ * (the split sweep: 0 two workgroups per CU, the default | 1 one prefetching workgroup per CU |
+ * 2 the prefetching one when the launch has no more (chunk, date) pairs than CUs; the same
+ * bits either way), "tc_spins" (polling trips a
  * csm_signal_chunked workgroup makes before it gives up a wait, default 2^21; 0 gives up at
  * once, which only the tests of the CSM_E_TIMEOUT report set).
  * Returns CSM_E_INVAL for an unknown key or value. */

@@ -21,7 +21,7 @@ import torch
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 import csmom  # noqa: E402
-from csmom.distributed import fallback_cap, halo_months  # noqa: E402
+from csmom.distributed import _halo_fused, fallback_cap, halo_months  # noqa: E402
 from csmom.synth import make_halo_panel  # noqa: E402
 
 
@@ -74,10 +74,14 @@ def main():
     mss = (msh - d0).contiguous()
     torch.cuda.synchronize()
 
+    # run_halo's choice (distributed._halo_fused); CSM_HALO_FUSED=1 / 0 forces either
+    force = os.environ.get("CSM_HALO_FUSED")
+    fused = _halo_fused(eng, P, maxd) if force is None else force == "1"
+
     def halo(ev=None):
         rec = (lambda i: ev[i].record()) if ev else (lambda i: None)
         rec(0)
-        if os.environ.get("CSM_HALO_SPLIT"):   # A/B: round 5's two launches
+        if not fused:   # the two launches
             carry_h, npm_h, flags = eng.shard_halo(P, ms, hp.H, hp.F, J, skip, before=True,
                                                    after=True)
             rec(1)
@@ -177,6 +181,7 @@ def main():
         "diag": diag,
         "N": N, "days_per_rank": dpr, "split_cells": cells or 32768,
         "dec_split": __import__("os").environ.get("CSM_DEC_SPLIT", "default (2: auto)"),
+        "fused_halo": fused,
         "tune": __import__("os").environ.get("CSM_TUNE", ""), "T_d_with_halo": int(P.shape[0]), "T_m": T_m, "H": hp.H,
         "F": hp.F, "G_emulated": G, "cap": cap, "listed_this_rank": int(cnt.item()),
         "collective_bytes_per_rank": {"need_bits": 4 * 8 * ((N + 63) // 64),

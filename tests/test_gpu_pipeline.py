@@ -276,8 +276,9 @@ def test_narrow_fallback_rows_with_long_short(engine, case):
 @pytest.fixture
 def tune_split(engine):
     lib = engine.lib
-    yield lambda v: lib.csm_tune(b"dec_split", v)
+    yield lambda v, pf=0: lib.csm_tune(b"dec_split", v) or lib.csm_tune(b"dec_split_pf", pf)
     lib.csm_tune(b"dec_split", 2)
+    lib.csm_tune(b"dec_split_pf", 0)
 
 
 @pytest.mark.parametrize("case", MERGE_CASES)
@@ -285,19 +286,22 @@ def test_deciles_ids_split_equals_merged(engine, tune_split, case):
     """The split decile pass (plan -> chunked sweep -> finish, the general kernel for the rows
     it leaves) against the one-workgroup-per-row merged pass: labels, counts, ranked rows AND
     decile means bit for bit (the merged pass sums in the split pass's chunk order,
-    DEC_CHUNK_ORDER); labels equal the oracle's."""
+    DEC_CHUNK_ORDER), with either split sweep (prefetching / two workgroups per CU); labels
+    equal the oracle's."""
     rng = np.random.default_rng(11)
     x = np.stack([_stress_row(case), _stress_row("lognormal_mild"), _stress_row(case)])
     nr = rng.normal(0.01, 0.1, x.shape)
     nr[rng.random(x.shape) < 0.03] = np.nan
     M, NR, IDS = _up(x), _up(nr), _ids_dev(x)
     got = {}
-    for v in (1, 0):
-        assert tune_split(v) == 0
-        got[v] = engine.deciles_ids(M, NR, IDS, 10, with_nv=True)
-    (L1, EW1, C1, N1), (L0, EW0, C0, N0) = got[1], got[0]
+    for v, pf in ((1, 1), (1, 0), (0, 0)):
+        assert tune_split(v, pf) == 0
+        got[v, pf] = engine.deciles_ids(M, NR, IDS, 10, with_nv=True)
+    (L1, EW1, C1, N1), (L0, EW0, C0, N0) = got[1, 1], got[0, 0]
     assert torch.equal(L1, L0) and torch.equal(C1, C0) and torch.equal(N1, N0), case
     assert bits_equal(EW1.cpu().numpy(), EW0.cpu().numpy()), case
+    for a, b in zip(got[1, 0], got[1, 1]):
+        assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), case
     for r in range(x.shape[0]):
         assert np.array_equal(L1.cpu().numpy()[r], _oracle_labels(x[r])), (case, r)
     L2, _, _, _ = engine.deciles_ids(M, None, IDS, 10)          # labels only (no next_ret)

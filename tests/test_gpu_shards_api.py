@@ -509,7 +509,7 @@ def test_fused_halo_prologue_equals_two_launches(engine, wide_gappy, G):
             assert bits_equal(x.cpu().numpy(), y.cpu().numpy())
         assert torch.equal(ids_a, ids_b)
     out = engine.pipeline(P, _up(ms), J, skip, 10)
-    a = virtual_shards_halo(engine, P, ms, G, J, skip, 10)
+    a = virtual_shards_halo(engine, P, ms, G, J, skip, 10, fused_halo=True)
     b = virtual_shards_halo(engine, P, ms, G, J, skip, 10, fold_repair=True, fused_halo=False)
     assert a[6] > 0   # listed columns went through shard_fix_cols
     for res in (a, b):

@@ -77,7 +77,7 @@ def test_tune_keys_documented_in_header_are_accepted():
              b"turn_want": ([1, 65536], 4096), b"overlap_rows": ([0, 1], 1),
              b"turn_gen_grid": ([1, 2048], 8192), b"gen_reset": ([0, 1], 1), b"turn_vwg": ([0, 1], 1),
              b"dec_split": ([0, 1, 2], 2), b"dec_split_cells": ([8192, 65536], 32768),
-             b"tc_spins": ([0, 100], 1 << 21),
+             b"dec_split_pf": ([0, 1, 2], 0), b"tc_spins": ([0, 100], 1 << 21),
              b"turn_mask": ([0, 1], 1), b"ls_opt": ([0, 1], 1),
              b"signal_j12": ([0, 1], 1), b"cols_wg": ([0, 1], 1)}
     for key, (vals, default) in cases.items():
@@ -86,7 +86,7 @@ def test_tune_keys_documented_in_header_are_accepted():
         assert lib.csm_tune(key, default) == 0
     for key, v in ((b"signal_vec", 3), (b"signal_bwf", 2), (b"dec_merge", 2), (b"overlap_rows", 2),
                    (b"turn_want", 0), (b"gen_reset", 2), (b"signal_j12", 2), (b"cols_wg", 2), (b"dec_split", 3), (b"dec_split_cells", 1000),
-                   (b"dec_split_cells", 4096), (b"tc_spins", -1), (b"no_such_knob", 1)):
+                   (b"dec_split_cells", 4096), (b"dec_split_pf", 3), (b"tc_spins", -1), (b"no_such_knob", 1)):
         assert lib.csm_tune(key, v) != 0, (key, v)
     # result-corrupting profiling knobs and negative-result variants are gone
     for key in (b"dec_ablate", b"signal_store", b"signal_rr", b"signal_db", b"signal_mw",
