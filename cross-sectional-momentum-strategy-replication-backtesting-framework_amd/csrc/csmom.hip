@@ -766,6 +766,10 @@ __device__ __forceinline__ void scan_shadow(ScanLane& s, double x, int m, double
   }
 }
 
+#ifdef SIG_HIST
+__device__ uint32_t* g_sig_hist;   // A/B build only: csm_signal_ids' per-month id histogram
+#endif
+
 #define HALO_WALK 24   // a business month's day rows in one batch of loads
 #define HALO_MAXG 64
 
@@ -1050,6 +1054,17 @@ __global__ __launch_bounds__(64 * BW) void k_signal(
           mom[c] = scan_step(sl[c], pm[c], m, ring_lds + VEC * tid + c, RS, W, J, N, a0 + c, R, M, NR);
       }
       if (IDS) {   // fixed-map bucket ids for the decile pass (csm_signal_ids)
+#ifdef SIG_HIST
+        // A/B only (verdict r05 #4): the cost of a per-month id histogram built here by
+        // integer atomics ([T_m][8192] u32, the decile pass's bucket of each ranked id)
+        if (g_sig_hist) {
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) {
+            const uint32_t id = csm_fid(mom[c]);
+            if (id != CSM_FB_NAN) atomicAdd(g_sig_hist + (int64_t)m * 8192 + (id >> 3), 1u);
+          }
+        }
+#endif
         if (VEC == 2)
           *reinterpret_cast<uint32_t*>(IDS + (int64_t)m * N + a0) =
               csm_fid(mom[0]) | (csm_fid(mom[VEC - 1]) << 16);
@@ -2840,6 +2855,20 @@ int csm_signal_ids(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N,
     return set_err(ctx, CSM_E_INVAL, "csm_signal_ids: ids must be non-NULL and 8-B aligned, N %% 4 == 0 "
                    "(N=%lld)", (long long)N);
   (void)min_month_days;   // kept in the ABI (host hint for fixed day batches; no kernel uses it)
+#ifdef SIG_HIST
+  {   // A/B build only: a zeroed [T_m][8192] histogram per launch
+    static uint32_t* hist = nullptr;
+    static int64_t cap = 0;
+    const int64_t need = (int64_t)T_m * 8192;
+    if (need > cap) {
+      if (hist) hipFree(hist);
+      HIP_CHECK(ctx, hipMalloc(&hist, need * 4));
+      cap = need;
+      HIP_CHECK(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_sig_hist), &hist, sizeof(hist)));
+    }
+    HIP_CHECK(ctx, hipMemsetAsync(hist, 0, need * 4, ctx->stream));
+  }
+#endif
   return signal_launch(ctx, "csm_signal_ids", P, T_d, N, month_start, T_m, max_month_days, J,
                        skip, PM, R, M, NR, nullptr, nullptr, nullptr, false, ids);
 }

@@ -1520,7 +1520,11 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
           if (IMP) {   // turnover_body's charge, term for term
             double unit = half_spread;
             if (sra >= 0.0) {
+#ifdef VWG_NOSQRT   // A/B timing only (wrong costs): the charge without its square root
+              const double im = k_impact * unit_sig * (dw * sra);
+#else
               const double im = k_impact * unit_sig * (sqrt(dw) * sra);
+#endif
               unit = unit + ((im == im) ? im : 0.0);
             }
             cost[g][q] += dw * unit;

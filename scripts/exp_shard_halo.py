@@ -150,6 +150,35 @@ def main():
         t2 = time.perf_counter()
         pipelined.append(1e3 * (t2 - t0) / 20)
         enqueue.append(1e3 * (t1 - t0) / 20)
+    # CSM_HALO_GRAPH=1: the whole rank pass captured as ONE hipGraph (no host enqueue), replayed
+    # back to back; its long-short and listed count checked bit for bit against an eager pass
+    graph = None
+    if os.environ.get("CSM_HALO_GRAPH") == "1":
+        LSe, cnte = [x.clone() for x in halo()[:2]]
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):   # (warm the capture stream's engine binding)
+            halo()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            LSg, cntg = halo()[:2]
+        g.replay()
+        torch.cuda.synchronize()
+        same = bool(torch.equal(LSg.view(torch.int64), LSe.view(torch.int64)) and
+                    torch.equal(cntg, cnte))
+        rep = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(20):
+                g.replay()
+            torch.cuda.synchronize()
+            rep.append(1e3 * (time.perf_counter() - t0) / 20)
+        graph = {"replay_ms_median": round(float(np.median(rep)), 4),
+                 "replay_ms_min": round(float(np.min(rep)), 4), "bits_equal_eager": same}
+        del g
     names = ["shard_halo", "signal_shard_halo", "need+union", "summary_cols", "fix_cols",
              "deciles_ids", "gather_emul+long_short"]
     st_ms = {n: [] for n in names}
@@ -191,6 +220,7 @@ def main():
         "ms_min": {k: round(float(np.min(v)), 4) for k, v in times.items()},
         "halo_back_to_back_ms_median": round(float(np.median(pipelined)), 4),
         "halo_host_enqueue_ms_median": round(float(np.median(enqueue)), 4),
+        "halo_graph": graph,
         "halo_stages_ms_median": {n: round(float(np.median(v)), 4) for n, v in st_ms.items()},
     }), flush=True)
 
