@@ -2136,10 +2136,13 @@ __global__ __launch_bounds__(256) void k_shard_summary_state(const double* __res
       [&](int m) { return shard_pm_at(PM, P, ms, m, T_m, W, N, a); }, n, fm, lm, T, os, out + j);
 }
 
-// The listed columns of the halo pass, ONE WORKGROUP PER COLUMN (grid ncol, COLS_THREADS): its
-// threads derive the column's T_m month prices together (PM where kept, else the month-end of
-// the daily rows: one round trip for all months instead of one per re-derived month), into
-// LDS; one lane then builds the record from LDS exactly as k_shard_summary_state does.
+// The listed columns of the halo pass, ONE WORKGROUP PER COLUMN (COLS_THREADS): its threads
+// derive the column's T_m month prices together (PM where kept, else the month-end of the
+// daily rows: one round trip for all months instead of one per re-derived month), into LDS; one
+// lane then builds the record from LDS exactly as k_shard_summary_state does.  The grid is
+// min(ncol, 2 n_CU) workgroups striding over the ncol columns (the listed count is on the
+// device): a listed column as above, a column past the list gets the neutral record (no present
+// month: k_shard_summary_state's, written by the workgroup's first T + SUM_SCALARS lanes).
 #define COLS_THREADS 64
 __global__ __launch_bounds__(COLS_THREADS) void k_shard_summary_cols(
     const double* __restrict__ PM, const double* __restrict__ P, const int64_t* __restrict__ ms,
@@ -2147,24 +2150,36 @@ __global__ __launch_bounds__(COLS_THREADS) void k_shard_summary_cols(
     const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int64_t ncol) {
   extern __shared__ __attribute__((aligned(16))) double pmc[];   // [T_m]
   const int W = T - 1;
-  const int64_t j = blockIdx.x;
-  const bool listed = j < (int64_t)*cnt;   // (workgroup-uniform)
-  const int64_t a = listed ? (int64_t)idx[j] : 0;
-  if (listed)
+  const int64_t nl = *cnt;
+  for (int64_t j = blockIdx.x; j < ncol; j += gridDim.x) {   // (workgroup-uniform)
+    if (j >= nl) {   // the neutral record: shard_summary_body with n = 0
+      const int r = threadIdx.x;
+      if (r < SUM_SCALARS + T) {
+        double v = absent_val();   // the tail rows and `first`
+        if (r == 0) v = 0.0;
+        else if (r == 1 || r == 2) v = -1.0;
+        else if (r == 3 || r == 4) v = qnan();
+        out[(int64_t)r * ncol + j] = v;
+      }
+      continue;
+    }
+    const int64_t a = (int64_t)idx[j];
+    __syncthreads();   // (the previous column's lane 0 is done with pmc)
     for (int m = threadIdx.x; m < T_m; m += COLS_THREADS) pmc[m] = shard_pm_at(PM, P, ms, m, T_m, W, N, a);
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  const int64_t n = listed ? (int64_t)st[a] : 0;
-  const int fm = listed ? (int)st[3 * N + a] : -1, lm = listed ? (int)st[4 * N + a] : -1;
-  shard_summary_body(
-      [&](int m0, int dm, int lo, int hi, double (&buf)[WALK_CHUNK]) {
+    __syncthreads();
+    if (threadIdx.x != 0) continue;
+    const int64_t n = (int64_t)st[a];
+    const int fm = (int)st[3 * N + a], lm = (int)st[4 * N + a];
+    shard_summary_body(
+        [&](int m0, int dm, int lo, int hi, double (&buf)[WALK_CHUNK]) {
 #pragma unroll
-        for (int q = 0; q < WALK_CHUNK; ++q) {
-          const int m = m0 + q * dm;
-          buf[q] = (m >= lo && m <= hi) ? pmc[m] : absent_val();
-        }
-      },
-      [&](int m) { return pmc[m]; }, n, fm, lm, T, ncol, out + j);
+          for (int q = 0; q < WALK_CHUNK; ++q) {
+            const int m = m0 + q * dm;
+            buf[q] = (m >= lo && m <= hi) ? pmc[m] : absent_val();
+          }
+        },
+        [&](int m) { return pmc[m]; }, n, fm, lm, T, ncol, out + j);
+  }
 }
 
 __device__ __forceinline__ bool same_bits(double x, double y) {
@@ -3359,7 +3374,8 @@ int csm_shard_summary_cols(csm_ctx* ctx, const double* P, const int64_t* month_s
     return set_err(ctx, CSM_E_INVAL, "csm_shard_summary_cols: bad arguments");
   // one workgroup per listed column, its month prices derived together into LDS
   if (g_tune_cols_wg && (size_t)T_m * sizeof(double) <= 65536 && cap <= 0x7FFFFFFF) {
-    hipLaunchKernelGGL(k_shard_summary_cols, dim3((unsigned)cap), dim3(COLS_THREADS),
+    const int64_t grid = std::min<int64_t>(cap, 2 * (int64_t)ctx->n_cu);
+    hipLaunchKernelGGL(k_shard_summary_cols, dim3((unsigned)grid), dim3(COLS_THREADS),
                        (size_t)T_m * sizeof(double), ctx->stream, PM, P, month_start, T_m, N,
                        J + skip + 1, state, out, idx, count, cap);
     LAUNCH_CHECK(ctx, "k_shard_summary_cols");
