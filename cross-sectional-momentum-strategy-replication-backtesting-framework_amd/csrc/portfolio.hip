@@ -1735,49 +1735,73 @@ __global__ __launch_bounds__(256) void k_ls(const double* __restrict__ PR, int T
   }
 }
 
-#define LS_PB 64   // panels per workgroup (a wave's lanes: 64 consecutive panels, coalesced rows)
-#define LS_TP 16   // month phases per workgroup
-__global__ __launch_bounds__(LS_PB * LS_TP) void k_ls_wide(const double* __restrict__ PR, int T_m, int B,
-                                                     int nb, double* __restrict__ LS,
-                                                     const double* __restrict__ COST,
-                                                     double* __restrict__ NET,
-                                                     int32_t* __restrict__ need_full) {
-  // thread (j, p): panel blockIdx.x * LS_PB + p, months t = j (mod LS_TP) -- a wave reads the
-  // same month of 64 adjacent panels (one workgroup per panel read one panel's column, a row
-  // stride apart per lane)
-  const int p = (int)threadIdx.x % LS_PB, j = (int)threadIdx.x / LS_PB;
-  const int b = (int)blockIdx.x * LS_PB + p;
+// Wide batches (C5: B = 800 panels of a grouped launch) in two launches instead of one
+// workgroup per 64 panels walking every month twice (52 workgroups, 140 us per launch):
+// k_ls_flags -- per (panel b, holding period q) whether some month has a decile-0 value
+// (bit 0) and some month a decile-(nb-1) value (bit 1), from blocks of LS_FM months in
+// parallel (64 panels x 4 month phases per workgroup, an atomicOr per panel into a zeroed
+// [nK][B] word array) -- then k_ls_rows, one thread per (q, t, b) output with k_ls's rule.
+// The same flags and the same per-output arithmetic as k_ls, so the same bits.
+#define LS_PB 64   // batches of at least this many panels take the two-launch form
+#define LS_FM 32   // months per k_ls_flags workgroup (8 per thread, loads in flight)
+__global__ __launch_bounds__(256) void k_ls_flags(const double* __restrict__ PR, int T_m, int B,
+                                                  int nb, int32_t* __restrict__ flags) {
+  const int p = (int)threadIdx.x & 63, j = (int)threadIdx.x >> 6;
+  const int b = (int)blockIdx.x * 64 + p;
+  const int q = (int)blockIdx.y;
+  const int t0 = (int)blockIdx.z * LS_FM;
   const bool on = b < B;
-  const int64_t qo = (int64_t)blockIdx.y * T_m * B;
-  PR += qo * nb;
-  LS += qo;
-  if (NET) { NET += qo; COST += qo; }
-  __shared__ int fl[LS_TP][LS_PB];
-  int lo = 0, hi = 0;
-  for (int t = j; on && t < T_m; t += LS_TP) {
-    const double* e = PR + ((int64_t)t * B + b) * nb;
-    lo |= e[0] == e[0];
-    hi |= e[nb - 1] == e[nb - 1];
+  const double* P0 = PR + (int64_t)q * T_m * B * nb;
+  constexpr int TK = LS_FM / 4;
+  double lo[TK], hi[TK];
+#pragma unroll
+  for (int k = 0; k < TK; ++k) {
+    const int t = t0 + j + 4 * k;
+    const bool ok = on && t < T_m;
+    const double* e = P0 + ((int64_t)(ok ? t : 0) * B + (on ? b : 0)) * nb;
+    lo[k] = ok ? e[0] : qnan();
+    hi[k] = ok ? e[nb - 1] : qnan();
   }
-  fl[j][p] = lo | (hi << 1);
-  __syncthreads();
   int f = 0;
 #pragma unroll
-  for (int jj = 0; jj < LS_TP; ++jj) f |= fl[jj][p];
-  const bool both = f == 3;
-  if (need_full && on && !both && j == 0) atomicOr(need_full, 1);
-  for (int t = j; on && t < T_m; t += LS_TP) {
-    const int64_t tb = (int64_t)t * B + b;
-    const double* e = PR + tb * nb;
+  for (int k = 0; k < TK; ++k) f |= (lo[k] == lo[k] ? 1 : 0) | (hi[k] == hi[k] ? 2 : 0);
+  __shared__ int fl[4][64];
+  fl[j][p] = f;
+  __syncthreads();
+  if (j == 0 && on) {
+    const int g = fl[0][p] | fl[1][p] | fl[2][p] | fl[3][p];
+    if (g) atomicOr(flags + (int64_t)q * B + b, g);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ls_rows(const double* __restrict__ PR, int T_m, int B,
+                                                 int nb, int nq, const int32_t* __restrict__ flags,
+                                                 double* __restrict__ LS,
+                                                 const double* __restrict__ COST,
+                                                 double* __restrict__ NET,
+                                                 int32_t* __restrict__ need_full) {
+  const int64_t rows = (int64_t)T_m * B;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)nq * rows) return;
+  const int q = (int)(g / rows);
+  const int64_t tb = g - (int64_t)q * rows;
+  const int b = (int)(tb % B);
+  const bool both = flags[(int64_t)q * B + b] == 3;
+  if (need_full && !both && tb < B) atomicOr(need_full, 1);   // (month 0's thread of the panel)
+  const double* e = PR + g * nb;
+  const double lo = e[0], hi = e[nb - 1];
+  double v = qnan();
+  if (both && lo == lo && hi == hi) {   // (some decile holds a value: k_ls's D(n-1) - D0)
+    v = hi - lo;
+  } else {   // the interior deciles decide (any value at all; max - min without both legs)
     bool any = false;
     double mx = -INFINITY, mn = INFINITY;
     for (int d = 0; d < nb; ++d)
       if (e[d] == e[d]) { any = true; mx = fmax(mx, e[d]); mn = fmin(mn, e[d]); }
-    double v = qnan();
-    if (any) v = both ? (e[nb - 1] - e[0]) : (mx - mn);
-    LS[tb] = v;
-    if (NET) NET[tb] = v - COST[tb];
+    if (any) v = both ? (hi - lo) : (mx - mn);
   }
+  LS[g] = v;
+  if (NET) NET[g] = v - COST[g];
 }
 
 // ---------------------------------------------------------------------------------- E6
@@ -2065,6 +2089,7 @@ struct PfLayout {
   bool seg;                          // label-sort buffers present (N <= SEG_MAXN)
   int64_t perm_b, off_b, wsrt_b;     // byte offsets: uint16 [rows][N], int32 [rows][nb+1], f64 [rows][N]
   int64_t lm_b, nwm;                 // leg bitplanes uint64 [rows][2][nwm] (k_label_sort_legs_ew)
+  int64_t lsf_b;                     // byte offset: int32 [TO_MAXQ][B] long-short leg flags (k_ls_flags)
 };
 static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax) {
   PfLayout l;
@@ -2095,6 +2120,8 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
     l.lm_b = al(l.wsrt_b + l.rows * seg_stride(N) * 8);
     l.bytes = al(l.lm_b + l.rows * 2 * l.nwm * 8);
   }
+  l.lsf_b = (l.bytes + 255) / 256 * 256;
+  l.bytes = l.lsf_b + (int64_t)TO_MAXQ * B * 4 + 256;
   return l;
 }
 
@@ -2423,11 +2450,18 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
                        (const double*)(ws + lay.cost), lay.p.Ct, (int64_t)lay.rows, PRq, TURNq,
                        COSTq, legs ? 1 : 0);
     LAUNCH_CHECK(ctx, "k_overlap");
-    if (B >= LS_PB)   // wide batches (C5: 227 -> 140 us per 800-panel launch)
-      hipLaunchKernelGGL(k_ls_wide, dim3((unsigned)((B + LS_PB - 1) / LS_PB), (unsigned)ks.n),
-                         dim3(LS_PB * LS_TP), 0, st, (const double*)PRq, T_m, B, n_bins,
-                         LS + q0 * rb, (const double*)COSTq, NETq, legs ? need_full : nullptr);
-    else
+    if (B >= LS_PB && T_m > 0) {   // wide batches (C5): flags over month blocks, then one
+      // thread per output (one workgroup per 64 panels: 227 -> 140 us per 800-panel launch)
+      int32_t* lsf = (int32_t*)((char*)workspace + lay.lsf_b);
+      HIP_CHECK(ctx, hipMemsetAsync(lsf, 0, (size_t)ks.n * B * sizeof(int32_t), st));
+      hipLaunchKernelGGL(k_ls_flags, dim3((unsigned)((B + 63) / 64), (unsigned)ks.n,
+                                          (unsigned)((T_m + LS_FM - 1) / LS_FM)),
+                         dim3(256), 0, st, (const double*)PRq, T_m, B, n_bins, lsf);
+      hipLaunchKernelGGL(k_ls_rows, dim3((unsigned)(((int64_t)ks.n * T_m * B + 255) / 256)),
+                         dim3(256), 0, st, (const double*)PRq, T_m, B, n_bins, ks.n,
+                         (const int32_t*)lsf, LS + q0 * rb, (const double*)COSTq, NETq,
+                         legs ? need_full : nullptr);
+    } else
       hipLaunchKernelGGL(k_ls, dim3((unsigned)B, (unsigned)ks.n), dim3(256), 0, st,
                          (const double*)PRq, T_m, B, n_bins, LS + q0 * rb, (const double*)COSTq,
                          NETq, legs ? need_full : nullptr);

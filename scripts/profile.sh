@@ -22,9 +22,9 @@ case "$CFG" in
   c4) N=100000; TD=10000; RUN="--steps 20 --warmup 5"; NT=25; PMC="--steps 2 --warmup 1"; NP=3; STAGE="" ;;
   c2) N=5000; TD=6522; RUN="--steps 50 --warmup 5"; NT=106; PMC="--steps 2 --warmup 1"; NP=6; STAGE="" ;;
   c3) N=5000; TD=6522; RUN="--steps 10 --warmup 2"; NT=22; PMC="--steps 3 --warmup 1"; NP=7
-      STAGE="--stage portfolio(k_cohort+k_turnover+k_overlap+k_ls)=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turn_prep,k_turnover,k_overlap,k_overlap_rows,k_ls,k_ls_wide,k_turnover_vwg,k_turnover_ew_mask" ;;
+      STAGE="--stage portfolio(k_cohort+k_turnover+k_overlap+k_ls)=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turn_prep,k_turnover,k_overlap,k_overlap_rows,k_ls,k_ls_wide,k_ls_flags,k_ls_rows,k_turnover_vwg,k_turnover_ew_mask" ;;
   c5) N=5000; TD=6522; RUN="--steps 2 --warmup 1"; NT=5; PMC="--steps 1 --warmup 1"; NP=3
-      STAGE="--stage portfolio(k_cohort+k_turnover+k_overlap+k_ls)=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turn_prep,k_turnover,k_overlap,k_overlap_rows,k_ls,k_ls_wide,k_turnover_vwg,k_turnover_ew_mask" ;;
+      STAGE="--stage portfolio(k_cohort+k_turnover+k_overlap+k_ls)=k_label_sort,k_label_sort_legs_ew,k_cohort_seg,k_cohort_lds,k_cohort,k_fw_fold,k_turn_prep,k_turnover,k_overlap,k_overlap_rows,k_ls,k_ls_wide,k_ls_flags,k_ls_rows,k_turnover_vwg,k_turnover_ew_mask" ;;
   *) echo "unknown config $CFG"; exit 2 ;;
 esac
 BENCH="bench.py --gpus 1 --config $CFG --no-cpu-baseline $EXTRA"

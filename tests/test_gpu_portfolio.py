@@ -574,3 +574,54 @@ def test_turnover_planes_follow_the_cohort_pass(engine):
         for f in ("LS", "TURN", "COST", "NET"):
             assert bits_equal(getattr(res[K], f).cpu().numpy(),
                               getattr(ref[K], f).cpu().numpy()), (K, f)
+
+
+def _ls_rule(PR):
+    """run_demo.py:57-67 per (month, panel) on the engine's own PR [T_m][B][nb]: D(n-1) - D0 when
+    the panel has both legs in some month, else max - min over the deciles holding a value."""
+    T_m, B, nb = PR.shape
+    LS = np.full((T_m, B), np.nan)
+    for b in range(B):
+        col = PR[:, b, :]
+        both = bool((~np.isnan(col[:, 0])).any() and (~np.isnan(col[:, nb - 1])).any())
+        for t in range(T_m):
+            e = col[t]
+            ok = ~np.isnan(e)
+            if not ok.any():
+                continue
+            LS[t, b] = (e[nb - 1] - e[0]) if both else (e[ok].max() - e[ok].min())
+    return LS, both
+
+
+@pytest.mark.parametrize("legs", [False, True])
+def test_long_short_wide_batch_rule(engine, legs):
+    """Batches of >= 64 panels form the long-short in two launches (k_ls_flags over month
+    blocks, k_ls_rows per output): LS / NET equal the reference rule applied to the engine's
+    own PR, bit for bit, on 80 panels where some lack the top or the bottom leg in every month
+    (max - min there) or have empty months; legs-only accounting sets the rerun flag for them
+    and its rerun is the full path's, bit for bit."""
+    rng = np.random.default_rng(5)
+    T_m, B, N, nb = 40, 80, 120, 10
+    Lh = rng.integers(-1, nb, size=(T_m, B, N)).astype(np.int8)
+    Lh[:, 3, :][Lh[:, 3, :] == nb - 1] = nb - 2       # panel 3: no top decile ever
+    Lh[:, 11, :][Lh[:, 11, :] == 0] = 1               # panel 11: no bottom decile ever
+    Lh[5:9, 17, :] = -1                               # panel 17: four empty months
+    NRh = rng.normal(0.01, 0.08, size=(T_m, B, N))
+    NRh[rng.random(NRh.shape) < 0.02] = np.nan
+    L, NR = _up(Lh.reshape(T_m, B * N)), _up(NRh.reshape(T_m, B * N))
+    full = engine.portfolio_multi(L, NR, nb, Ks=(1, 3), B=B)
+    for K in (1, 3):
+        PR = full[K].PR.cpu().numpy().reshape(T_m, B, nb)
+        ref, _ = _ls_rule(PR)
+        assert bits_equal(full[K].LS.cpu().numpy().reshape(T_m, B), ref), K
+        net = full[K].LS.cpu().numpy() - full[K].COST.cpu().numpy()
+        assert bits_equal(full[K].NET.cpu().numpy(), net), K
+    if legs:
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+        engine.portfolio_multi(L, NR, nb, Ks=(1, 3), B=B, legs_only=True, need_full=flag)
+        assert int(flag.item()) == 1
+        got = engine.portfolio_multi(L, NR, nb, Ks=(1, 3), B=B, legs_only=True)
+        for K in (1, 3):
+            for f in ("PR", "LS", "TURN", "COST", "NET"):
+                assert bits_equal(getattr(got[K], f).cpu().numpy(),
+                                  getattr(full[K], f).cpu().numpy()), (K, f)
