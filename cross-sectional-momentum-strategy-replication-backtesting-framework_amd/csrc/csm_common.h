@@ -36,10 +36,12 @@ struct csm_ctx {
   size_t dsplit_bytes;
   void* comm;             // RCCL communicator of csm_allgather_init (collective.hip), or NULL
   int comm_rank, comm_size;
-  // portfolio workspaces whose last cohort pass wrote the leg bitplanes (portfolio.hip): the
-  // turnover pass reads bitplanes only from a workspace recorded here, whatever the tune knobs
-  // say by then (a knob changed between the two calls falls back to the label bytes)
+  // portfolio workspaces and what their last cohort pass wrote (portfolio.hip): bit 0 the leg
+  // bitplanes -- the turnover pass reads bitplanes only from a workspace recorded here, whatever
+  // the tune knobs say by then (a knob changed between the two calls falls back to the label
+  // bytes) -- bit 1 legs-only cohort partials in the two-leg layout ([rows][K][C][2])
   void* planes_ws[32];
+  unsigned char planes_bits[32];
   int planes_next;
 };
 

@@ -542,6 +542,10 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     int64_t N, int K, int C, int Cs, int xcd, int stage2, PanAddr pa, int Bo) {
   constexpr int ND = LEGS ? 2 : NB;   // segments per age
   auto dec_of = [](int e) { return LEGS ? (e ? NB - 1 : 0) : e; };
+  // LEGS: the partials in the two-leg layout [rows][K][C][2] (leg 0 = decile 0, leg 1 = decile
+  // NB - 1): the accounting reads 2 of every 2 values, not 2 of every NB, and the leg partials
+  // of a (row, age) are one 16-B pair instead of two stores NB * 8 B apart
+  constexpr int SW_W = LEGS ? 2 : NB;   // partials per (row, age, chunk)
   // the return row of month t (N values), NaN at slot N
   extern __shared__ __attribute__((aligned(16))) double rl[];
   // then each J's K * (NB + 1) segment offsets, in the same dynamic allocation: sized to the
@@ -580,8 +584,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   if (c >= Cs) {   // chunks beyond the Cs working ones only hold zeros
     for (int jq = 0; jq < sj.n; ++jq)
       for (int g = tid; g < K * ND; g += PF_THREADS) {
-        const int k = g / ND, d = dec_of(g - k * ND);
-        const int64_t ob = ((tbo * K + k) * C + c) * NB + d;
+        const int k = g / ND, e = g - k * ND;
+        const int64_t ob = ((tbo * K + k) * C + c) * SW_W + (LEGS ? e : dec_of(e));
         sj.SWR[jq][ob] = 0.0;
         sj.SW[jq][ob] = 0.0;
       }
@@ -629,8 +633,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   // whole return row, so Cs stays small
   for (int g = tid; g < K * ND && Cs > 1; g += PF_THREADS) {
     if (g % Cs == c) continue;
-    const int k = g / ND, d = dec_of(g - k * ND);
-    const int64_t ob = ((tbo * K + k) * C + c) * NB + d;
+    const int k = g / ND, e = g - k * ND;
+    const int64_t ob = ((tbo * K + k) * C + c) * SW_W + (LEGS ? e : dec_of(e));
     SWRp[ob] = 0.0;
     SWp[ob] = 0.0;
   }
@@ -648,7 +652,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   auto seg_at = [&](int g) {
     Seg q;
     const int k = g / ND, d = dec_of(g - k * ND);
-    q.ob = ((tbo * K + k) * C + c) * NB + d;
+    q.ob = ((tbo * K + k) * C + c) * SW_W + (LEGS ? g - k * ND : d);
     q.live = k < kmax;
     const int64_t srow = tbo - (int64_t)(q.live ? k : 0) * Bo;
     const int oi = LEGS ? k * 4 + (d == 0 ? 0 : 2) : k * (NB + 1) + d;
@@ -1598,7 +1602,7 @@ __global__ __launch_bounds__(256) void k_overlap(
     const double* __restrict__ SWRp, const double* __restrict__ SWp, KSet ks, int Kmax, int C,
     int nb, const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
     int64_t rows, double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST,
-    int legs) {
+    int legs, const int32_t* __restrict__ lwp) {
   // one thread per output (q, t, b, d), in PR's layout (flat grid: the one-workgroup-per-row
   // version was 64-lane workgroups with nb lanes busy, dispatch-bound at sweep sizes)
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1611,6 +1615,10 @@ __global__ __launch_bounds__(256) void k_overlap(
   if (legs && d != 0 && d != nb - 1) {   // legs-only cohort sums: not computed
     PR[(q * rows + tb) * nb + d] = qnan();
   } else {
+    // the partials' layout: n_bins per (row, age, chunk), or the legs-only two-leg layout (any
+    // other word reads as n_bins: never an index past the n_bins layout)
+    const int lw = *lwp == 2 ? 2 : nb;
+    const int ds = lw == 2 ? (d == 0 ? 0 : 1) : d;
     double acc = 0.0;
     int n = 0;
     for (int k = 0; k < K; ++k) {
@@ -1620,7 +1628,7 @@ __global__ __launch_bounds__(256) void k_overlap(
         double xr[8], yr[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int64_t o = ((tb * Kmax + k) * C + (c0 + u < C ? c0 + u : 0)) * nb + d;
+          const int64_t o = ((tb * Kmax + k) * C + (c0 + u < C ? c0 + u : 0)) * lw + ds;
           xr[u] = c0 + u < C ? SWRp[o] : 0.0;
           yr[u] = c0 + u < C ? SWp[o] : 0.0;
         }
@@ -1655,7 +1663,7 @@ __global__ __launch_bounds__(256) void k_overlap_rows(
     const double* __restrict__ SWRp, const double* __restrict__ SWp, KSet ks, int Kmax,
     int nb, const double* __restrict__ TURNp, const double* __restrict__ COSTp, int Ct,
     int64_t rows, double* __restrict__ PR, double* __restrict__ TURN, double* __restrict__ COST,
-    int legs) {
+    int legs, const int32_t* __restrict__ lwp) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= rows * nb) return;
   const int d = (int)(g % nb);
@@ -1663,13 +1671,15 @@ __global__ __launch_bounds__(256) void k_overlap_rows(
   if (legs && d != 0 && d != nb - 1) {   // legs-only cohort sums: not computed
     for (int q = 0; q < ks.n; ++q) PR[((int64_t)q * rows + tb) * nb + d] = qnan();
   } else {
+    const int lw = *lwp == 2 ? 2 : nb;   // the partials' layout (k_overlap)
+    const int ds = lw == 2 ? (d == 0 ? 0 : 1) : d;
     double acc = 0.0;
     int n = 0;
     for (int k0 = 0; k0 < Kmax; k0 += OV_TRIP) {
       double xs[OV_TRIP], ys[OV_TRIP];
 #pragma unroll
       for (int u = 0; u < OV_TRIP; ++u) {   // one partial per (age, decile): loads first
-        const int64_t o = (tb * Kmax + (k0 + u < Kmax ? k0 + u : 0)) * nb + d;
+        const int64_t o = (tb * Kmax + (k0 + u < Kmax ? k0 + u : 0)) * lw + ds;
         xs[u] = k0 + u < Kmax ? 0.0 + SWRp[o] : 0.0;   // 0.0 + x: k_overlap's chunk sum of one
         ys[u] = k0 + u < Kmax ? 0.0 + SWp[o] : 0.0;
       }
@@ -1894,6 +1904,16 @@ static int32_t* g_gen_probe = nullptr;
 __global__ void k_copy_i32(const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
   if (threadIdx.x == 0) dst[0] = *(volatile const int32_t*)src;
 }
+// n int32 words set to v (a kernel node under capture, as the work-list counter's reset)
+__global__ __launch_bounds__(256) void k_fill_i32(int32_t* __restrict__ p, int64_t n, int32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+static void fill_i32(hipStream_t st, int32_t* p, int64_t n, int32_t v) {
+  const int64_t g = std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)(g > 0 ? g : 1)), dim3(256), 0, st, p, n, v);
+}
 
 struct PfPlan {
   int C, kpar, Ct;
@@ -1955,8 +1975,9 @@ __global__ __launch_bounds__(256) void k_fw_fold(const double* __restrict__ FWp,
   FWt[i] = tot;
 }
 
+// Returns whether the legs-only segment pass ran (its partials in the two-leg layout).
 template <int NB>
-static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
+static bool launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, const double* NR,
                           const double* W, int T_m, int B, int64_t N, int K, double* SWRp,
                           double* SWp, double* FWp, char* segws, int64_t perm_b, int64_t off_b,
                           int64_t wsrt_b, bool legs, const PanAddr& pa, int64_t lm_b = 0) {
@@ -2003,7 +2024,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
       hipLaunchKernelGGL((k_cohort_seg<NB, false>), g2, dim3(PF_THREADS), lds, st, NR, sj,
                          (const double*)WSRT, T_m, B, N, K, pl.C, Cs, xcd, 1, pa, B);
     }
-    return;
+    return legs;
   }
   if (g_tune_cohort_lds && !pl.kpar && K * NB <= AC_MAXKD) {
     const dim3 g2((unsigned)(pl.C * T_m * B));
@@ -2013,7 +2034,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
     else
       hipLaunchKernelGGL((k_cohort_lds<NB, false>), g2, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B,
                          N, K, pl.C, pl.CH, SWRp, SWp, FWp, pa);
-    return;
+    return false;
   }
   if (W)
     hipLaunchKernelGGL((k_cohort<NB, true>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
@@ -2021,6 +2042,7 @@ static void launch_cohort(hipStream_t st, const PfPlan& pl, const int8_t* L, con
   else
     hipLaunchKernelGGL((k_cohort<NB, false>), g, dim3(PF_THREADS), 0, st, L, NR, W, T_m, B, N, K,
                        pl.C, pl.CH, pl.kpar, SWRp, SWp, FWp, pa);
+  return false;
 }
 
 // Equal-weight cohort sums of nJ look-backs sharing one next_ret panel (segment path, one chunk
@@ -2066,8 +2088,9 @@ static void launch_cohort_js(hipStream_t st, const PfPlan& pl, int nJ, const int
     const int64_t r0 = grouped ? (int64_t)q * B : 0;   // J q's first workspace row of a month
     sj.PERM[q] = (uint16_t*)(w + perm_b) + r0 * PS;
     sj.OFF[q] = (int32_t*)(w + off_b) + r0 * (NB + 1);
-    sj.SWR[q] = (double*)(w + swr_b) + r0 * K * NB;   // (one cohort chunk)
-    sj.SW[q] = (double*)(w + sw_b) + r0 * K * NB;
+    const int swv = legs ? 2 : NB;   // partials per (row, age): k_cohort_seg's layout
+    sj.SWR[q] = (double*)(w + swr_b) + r0 * K * swv;   // (one cohort chunk)
+    sj.SW[q] = (double*)(w + sw_b) + r0 * K * swv;
   }
   const size_t lds = (size_t)(N + 1) * sizeof(double) +
                      (legs ? (size_t)nJ * K * 4 * sizeof(uint16_t) : (size_t)nJ * K * (NB + 1) * sizeof(int32_t));
@@ -2090,6 +2113,9 @@ struct PfLayout {
   int64_t perm_b, off_b, wsrt_b;     // byte offsets: uint16 [rows][N], int32 [rows][nb+1], f64 [rows][N]
   int64_t lm_b, nwm;                 // leg bitplanes uint64 [rows][2][nwm] (k_label_sort_legs_ew)
   int64_t lsf_b;                     // byte offset: int32 [TO_MAXQ][B] long-short leg flags (k_ls_flags)
+  int64_t lw_b;                      // byte offset: int32, the cohort partials' width per (row,
+                                     // age, chunk) the last cohort pass wrote: 2 = the legs-only
+                                     // two-leg layout, else n_bins (read on the device by k_overlap*)
 };
 static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax) {
   PfLayout l;
@@ -2121,7 +2147,8 @@ static PfLayout pf_layout(int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int
     l.bytes = al(l.lm_b + l.rows * 2 * l.nwm * 8);
   }
   l.lsf_b = (l.bytes + 255) / 256 * 256;
-  l.bytes = l.lsf_b + (int64_t)TO_MAXQ * B * 4 + 256;
+  l.lw_b = l.lsf_b + (int64_t)TO_MAXQ * B * 4;
+  l.bytes = l.lw_b + 4 + 256;
   return l;
 }
 
@@ -2181,7 +2208,7 @@ int64_t csm_portfolio_workspace(int32_t T_m, int32_t B, int64_t N, int32_t n_bin
 }
 
 static bool legs_masks(const PfLayout& lay, bool legs, int64_t N, int Kmax, int n_bins);
-static void planes_note(csm_ctx* ctx, void* ws, bool wrote);
+static void planes_note(csm_ctx* ctx, void* ws, unsigned bits);
 
 static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const double* W,
                        int32_t T_m, int32_t B, int64_t N, int32_t n_bins, int32_t Kmax,
@@ -2196,15 +2223,17 @@ static int cohort_sums(csm_ctx* ctx, const int8_t* L, const double* NR, const do
   const PfLayout lay = pf_layout(T_m, B, N, n_bins, Kmax);
   double* ws = (double*)workspace;
   hipStream_t st = ctx->stream;
+  bool dense = false;   // legs-only partials in the two-leg layout
   switch (n_bins) {
-#define PF_CASE(NBV) case NBV: launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b, legs, pa, lay.lm_b); break;
+#define PF_CASE(NBV) case NBV: dense = launch_cohort<NBV>(st, lay.p, L, NR, W, T_m, B, N, Kmax, ws + lay.swr, ws + lay.sw, ws + lay.fw, lay.seg ? (char*)workspace : nullptr, lay.perm_b, lay.off_b, lay.wsrt_b, legs, pa, lay.lm_b); break;
     PF_CASE(2) PF_CASE(3) PF_CASE(4) PF_CASE(5) PF_CASE(10) PF_CASE(20) PF_CASE(30)
 #undef PF_CASE
     default:
       return set_err(ctx, CSM_E_INVAL, "csm_cohort_sums: n_bins=%d unsupported (2,3,4,5,10,20,30)", n_bins);
   }
   LAUNCH_CHECK(ctx, "k_cohort");
-  planes_note(ctx, workspace, !W && legs_masks(lay, legs, N, Kmax, n_bins));
+  fill_i32(st, (int32_t*)((char*)workspace + lay.lw_b), 1, dense ? 2 : n_bins);
+  planes_note(ctx, workspace, !W && legs_masks(lay, legs, N, Kmax, n_bins) ? 1u : 0u);
   if (lay.p.C > 1) {
     hipLaunchKernelGGL(k_fw_fold, dim3((unsigned)((2 * lay.rows + 255) / 256)), dim3(256), 0, st,
                        (const double*)(ws + lay.fw), lay.rows, lay.p.C, ws + lay.fwt);
@@ -2258,7 +2287,9 @@ int csm_cohort_sums_js(csm_ctx* ctx, int32_t nJ, const int8_t* const* L, const d
 #undef PJ_CASE
   }
   LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret)");
-  for (int q = 0; q < nJ; ++q) planes_note(ctx, ws[q], legs_masks(lay, legs != 0, N, Kmax, n_bins));
+  for (int q = 0; q < nJ; ++q)
+    fill_i32(st, (int32_t*)(ws[q] + lay.lw_b), 1, legs ? 2 : n_bins);
+  for (int q = 0; q < nJ; ++q) planes_note(ctx, ws[q], legs_masks(lay, legs != 0, N, Kmax, n_bins) ? 1u : 0u);
   // (the shared path has one cohort chunk: each J's partials are its folded totals)
   return CSM_OK;
 }
@@ -2292,7 +2323,8 @@ int csm_cohort_sums_js_grouped(csm_ctx* ctx, int32_t nJ, const int8_t* L, const 
 #undef PJ_CASE
   }
   LAUNCH_CHECK(ctx, "k_cohort_seg (shared next_ret, grouped)");
-  planes_note(ctx, workspace, legs_masks(lay, legs != 0, N, Kmax, n_bins));
+  fill_i32(st, (int32_t*)(ws + lay.lw_b), 1, legs ? 2 : n_bins);
+  planes_note(ctx, workspace, legs_masks(lay, legs != 0, N, Kmax, n_bins) ? 1u : 0u);
   return CSM_OK;
 }
 
@@ -2321,23 +2353,27 @@ static bool legs_masks(const PfLayout& lay, bool legs, int64_t N, int Kmax, int 
 }
 
 // The cohort pass records, per workspace, whether it wrote the leg bitplanes (the
-// turnover pass must not infer it from knobs that may have changed in between)
-static void planes_note(csm_ctx* ctx, void* ws, bool wrote) {
+// turnover pass must not infer it from knobs that may have changed in between; bit 0).  (The
+// partials' layout is a word in the workspace itself, PfLayout::lw_b.)
+static void planes_note(csm_ctx* ctx, void* ws, unsigned bits) {
   int hit = -1;
   for (int i = 0; i < 32; ++i)
     if (ctx->planes_ws[i] == ws) { hit = i; break; }
-  if (wrote && hit < 0) {
-    ctx->planes_ws[ctx->planes_next] = ws;
+  if (bits && hit < 0) {
+    hit = ctx->planes_next;
+    ctx->planes_ws[hit] = ws;
     ctx->planes_next = (ctx->planes_next + 1) % 32;
-  } else if (!wrote && hit >= 0) {
+  } else if (!bits && hit >= 0) {
     ctx->planes_ws[hit] = nullptr;
   }
+  if (hit >= 0) ctx->planes_bits[hit] = (unsigned char)bits;
 }
-static bool planes_have(const csm_ctx* ctx, const void* ws) {
+static unsigned ws_bits(const csm_ctx* ctx, const void* ws) {
   for (int i = 0; i < 32; ++i)
-    if (ws && ctx->planes_ws[i] == ws) return true;
-  return false;
+    if (ws && ctx->planes_ws[i] == ws) return ctx->planes_bits[i];
+  return 0u;
 }
+static bool planes_have(const csm_ctx* ctx, const void* ws) { return (ws_bits(ctx, ws) & 1u) != 0; }
 
 static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W,
                                   int32_t T_m, int32_t B, int64_t N, int32_t n_bins,
@@ -2441,19 +2477,19 @@ static int portfolio_from_cohorts(csm_ctx* ctx, const int8_t* L, const double* W
                          (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks, Kmax,
                          n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
                          (const double*)(ws + lay.cost), lay.p.Ct, (int64_t)lay.rows, PRq, TURNq,
-                         COSTq, legs ? 1 : 0);
+                         COSTq, legs ? 1 : 0, (const int32_t*)((char*)workspace + lay.lw_b));
     else
     hipLaunchKernelGGL(k_overlap, dim3((unsigned)(((int64_t)ks.n * lay.rows * n_bins + 255) / 256)),
                        dim3(256), 0, st,
                        (const double*)(ws + lay.swr), (const double*)(ws + lay.sw), ks, Kmax,
                        lay.p.C, n_bins, costs ? (const double*)(ws + lay.turn) : nullptr,
                        (const double*)(ws + lay.cost), lay.p.Ct, (int64_t)lay.rows, PRq, TURNq,
-                       COSTq, legs ? 1 : 0);
+                       COSTq, legs ? 1 : 0, (const int32_t*)((char*)workspace + lay.lw_b));
     LAUNCH_CHECK(ctx, "k_overlap");
     if (B >= LS_PB && T_m > 0) {   // wide batches (C5): flags over month blocks, then one
       // thread per output (one workgroup per 64 panels: 227 -> 140 us per 800-panel launch)
       int32_t* lsf = (int32_t*)((char*)workspace + lay.lsf_b);
-      HIP_CHECK(ctx, hipMemsetAsync(lsf, 0, (size_t)ks.n * B * sizeof(int32_t), st));
+      fill_i32(st, lsf, (int64_t)ks.n * B, 0);
       hipLaunchKernelGGL(k_ls_flags, dim3((unsigned)((B + 63) / 64), (unsigned)ks.n,
                                           (unsigned)((T_m + LS_FM - 1) / LS_FM)),
                          dim3(256), 0, st, (const double*)PRq, T_m, B, n_bins, lsf);
