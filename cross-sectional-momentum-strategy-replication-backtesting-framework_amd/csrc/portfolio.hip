@@ -536,6 +536,9 @@ struct SegJ {
   double* SW[SEG_MAXJ];
   int n;
 };
+#ifndef SEG_PANEL_MAJOR
+#define SEG_PANEL_MAJOR 1
+#endif
 template <int NB, bool VW, bool LEGS = false>
 __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
     const double* __restrict__ NR, SegJ sj, const double* __restrict__ WSRT, int T_m, int B,
@@ -561,13 +564,22 @@ __global__ __launch_bounds__(PF_THREADS) void k_cohort_seg(
   int t;
   if (xcd) {   // C == 1
     // XCD-aware order: workgroups go round-robin to the 8 XCDs, so workgroup id -> (t, b)
-    // keeps panel b on XCD b % 8 with t advancing slowly; the K formation rows a panel's
-    // months re-read then stay in that XCD's L2.
+    // keeps panel b on XCD b % 8.  SEG_PANEL_MAJOR (default): an XCD's workgroups take one
+    // panel's months in order, then its next panel, so the K formation rows (member ids) a
+    // month re-reads were read by the months just before it, in that XCD's L2 (else: the
+    // XCD's panels for one month, then the next month -- the L2 then also holds the return
+    // rows of ~Bx other panels between two uses of a formation row).
     const int id = (int)blockIdx.x, x = id & 7, j = id >> 3;
     const int Bx = (B + 7) >> 3;
+#if SEG_PANEL_MAJOR
+    const int bj = j / T_m;
+    t = j - bj * T_m;
+    const int b = x + 8 * bj;
+#else
     t = j / Bx;
     const int b = x + 8 * (j - t * Bx);
-    if (b >= B || t >= T_m) return;
+#endif
+    if (b >= B || t >= T_m || j >= Bx * T_m) return;
     tb = (int64_t)t * B + b;
   } else {
     c = (int)(blockIdx.x % (unsigned)C);
