@@ -866,6 +866,11 @@ __global__ __launch_bounds__(TP_THREADS) void k_turn_prep(const double* __restri
   TPm[tb] = m;
 }
 
+// TO_GEN_TAB: the general equal-weight rows' non-full legs from per-row tables of the ages
+// 0..5 / 1..6 plus a walk over the ages >= 6, instead of a walk over every age (the same sums)
+#ifndef TO_GEN_TAB
+#define TO_GEN_TAB 1
+#endif
 template <bool VW, bool IMP, bool GEN, bool BM = false>
 __device__ __forceinline__ void turnover_body(
     int bid, const int8_t* __restrict__ L, const double* __restrict__ W,
@@ -1076,6 +1081,25 @@ __device__ __forceinline__ void turnover_body(
       for (int q = 0; q < nq; ++q)
         fullm |= (full[q][0] ? 1u : 0u) << (2 * q) | (full[q][1] ? 1u : 0u) << (2 * q + 1);
       const bool anyfree = fullm != (1u << (2 * nq)) - 1u;
+#if TO_GEN_TAB
+      // legs that are not full take x1 / x0 from per-row tables for the ages 0..5 / 1..6 (each
+      // entry the ascending sum of inv over its member ages: the walk's own additions, the
+      // +0.0 of a non-member age being exact for these non-negative sums), and walk only the
+      // ages >= 6: pairs with K_q <= 6 are charged straight from the tables
+      __shared__ double tabA[2][64], tabZ[2][64];
+      if (anyfree) {   // (row-uniform)
+        for (int i = tid; i < 256; i += PF_THREADS) {
+          const int li = i >> 7, z = (i >> 6) & 1, m = i & 63;
+          double sum = 0.0;
+          for (int bb = 0; bb < 6; ++bb) {
+            const int j = bb + z;   // tabA: ages 0..5, tabZ: ages 1..6
+            if ((m >> bb) & 1) sum += j <= Kmax ? inv[li][j] : 0.0;
+          }
+          (z ? tabZ : tabA)[li][m] = sum;
+        }
+        __syncthreads();
+      }
+#endif
       for (int64_t a4 = a0 + cw * tid; a4 < a1 && amask; a4 += cw * PF_THREADS) {
         uint32_t mt4[4] = {0, 0, 0, 0}, mb4[4] = {0, 0, 0, 0};
         if (cw == 4) {
@@ -1122,6 +1146,65 @@ __device__ __forceinline__ void turnover_body(
             sb[q] += e1 & e0;
           }
         }
+#if TO_GEN_TAB
+        if (anyfree) {
+          // x1 of the ages 0..5 and x0 of the ages 1..6 from the tables; pairs with K_q <= 6
+          // charged from them, cells and legs in order (each pair's terms in the walk's order)
+          double sa[4][2], sz[4][2];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sa[e][0] = tabA[0][mt4[e] & 63u]; sz[e][0] = tabZ[0][(mt4[e] >> 1) & 63u];
+            sa[e][1] = tabA[1][mb4[e] & 63u]; sz[e][1] = tabZ[1][(mb4[e] >> 1) & 63u];
+          }
+          uint32_t clo = 0;   // pairs (q, leg) with K_q <= 6 that are not full
+#pragma unroll
+          for (int q = 0; q < TO_MAXQ; ++q)
+            clo |= (q < nq && ks.K[q] <= 6) ? (3u << (2 * q)) & ~fullm : 0u;
+          if (clo) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (e >= ne) break;
+#pragma unroll
+              for (int li = 0; li < 2; ++li) {
+                const uint32_t mm = li == 0 ? mt4[e] : mb4[e];
+#pragma unroll
+                for (int q = 0; q < TO_MAXQ; ++q) {
+                  if (!((clo >> (2 * q + li)) & 1u)) continue;
+                  const uint32_t km = (1u << ks.K[q]) - 1u;
+                  charge(q, fabs(tabA[li][mm & km] * sk[q][li][0] -
+                                 tabZ[li][(mm >> 1) & km] * sk[q][li][1]), -1.0, 0.02);
+                }
+              }
+            }
+          }
+#pragma unroll 1
+          for (int j = 6; j <= kq; ++j) {
+            asm volatile("" ::: "memory");   // the factors are re-read (broadcasts), not held
+            const double iv0 = inv[0][j], iv1 = inv[1][j];
+            uint32_t cq = 0;   // pairs with K_q == j (> 6) charged now
+#pragma unroll
+            for (int q = 0; q < TO_MAXQ; ++q)
+              cq |= (q < nq && ks.K[q] == j && j > 6) ? (3u << (2 * q)) & ~fullm : 0u;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+#pragma unroll
+              for (int li = 0; li < 2; ++li) {
+                const uint32_t mm = li == 0 ? mt4[e] : mb4[e];
+                const double v = ((mm >> j) & 1u) ? (li == 0 ? iv0 : iv1) : 0.0;
+                if (cq && e < ne) {
+#pragma unroll
+                  for (int q = 0; q < TO_MAXQ; ++q)
+                    if ((cq >> (2 * q + li)) & 1u)
+                      charge(q, fabs(sa[e][li] * sk[q][li][0] - (sz[e][li] + v) * sk[q][li][1]),
+                             -1.0, 0.02);
+                }
+                sa[e][li] += v;
+                if (j >= 7) sz[e][li] += v;   // (the table holds age 6 already)
+              }
+            }
+          }
+        }
+#else
         if (anyfree) {
           // legs that are not full: x1 = sum of inv over the member ages 0..K-1 (month t's
           // window), x0 over 1..K (month t-1's), both ascending.  One walk over the ages for
@@ -1159,6 +1242,7 @@ __device__ __forceinline__ void turnover_body(
             }
           }
         }
+#endif
       }
     } else if constexpr (!BM) {
     // ages whose cohort is empty on both legs add 0.0 to every sum (inv 0.0) and make neither
@@ -1579,7 +1663,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
 // kernel keeps the registers of that path (the dense path's arrays would double them).
 template <bool VW, bool IMP, bool GEN, bool BM = false>
 #ifndef TO_MINB_BM
-#define TO_MINB_BM 1   // general equal-weight rows: workgroups per CU the VGPR budget must allow
+#define TO_MINB_BM 4   // general equal-weight rows: workgroups per CU the VGPR budget must allow
+                       // (4: the table walk's 129 VGPRs held to 128, no spills)
 #endif
 __global__ __launch_bounds__(PF_THREADS, BM ? TO_MINB_BM : 1) void k_turnover(
     const int8_t* __restrict__ L, const double* __restrict__ W, const double* __restrict__ FWp,
