@@ -867,9 +867,13 @@ __global__ __launch_bounds__(TP_THREADS) void k_turn_prep(const double* __restri
 }
 
 // TO_GEN_TAB: the general equal-weight rows' non-full legs from per-row tables of the ages
-// 0..5 / 1..6 plus a walk over the ages >= 6, instead of a walk over every age (the same sums)
+// 0..TB-1 / 1..TB (TB = TO_GEN_TB) plus a walk over the ages >= TB, instead of a walk over every
+// age (the same sums)
 #ifndef TO_GEN_TAB
 #define TO_GEN_TAB 1
+#endif
+#ifndef TO_GEN_TB
+#define TO_GEN_TB 8
 #endif
 template <bool VW, bool IMP, bool GEN, bool BM = false>
 __device__ __forceinline__ void turnover_body(
@@ -1082,17 +1086,18 @@ __device__ __forceinline__ void turnover_body(
         fullm |= (full[q][0] ? 1u : 0u) << (2 * q) | (full[q][1] ? 1u : 0u) << (2 * q + 1);
       const bool anyfree = fullm != (1u << (2 * nq)) - 1u;
 #if TO_GEN_TAB
-      // legs that are not full take x1 / x0 from per-row tables for the ages 0..5 / 1..6 (each
-      // entry the ascending sum of inv over its member ages: the walk's own additions, the
-      // +0.0 of a non-member age being exact for these non-negative sums), and walk only the
-      // ages >= 6: pairs with K_q <= 6 are charged straight from the tables
-      __shared__ double tabA[2][64], tabZ[2][64];
+      // legs that are not full take x1 / x0 from per-row tables for the ages 0..TB-1 / 1..TB
+      // (each entry the ascending sum of inv over its member ages: the walk's own additions,
+      // the +0.0 of a non-member age being exact for these non-negative sums), and walk only the
+      // ages >= TB: pairs with K_q <= TB are charged straight from the tables
+      constexpr int TB = TO_GEN_TB, TN = 1 << TO_GEN_TB;
+      __shared__ double tabA[2][TN], tabZ[2][TN];
       if (anyfree) {   // (row-uniform)
-        for (int i = tid; i < 256; i += PF_THREADS) {
-          const int li = i >> 7, z = (i >> 6) & 1, m = i & 63;
+        for (int i = tid; i < 4 * TN; i += PF_THREADS) {
+          const int li = i / (2 * TN), z = (i / TN) & 1, m = i & (TN - 1);
           double sum = 0.0;
-          for (int bb = 0; bb < 6; ++bb) {
-            const int j = bb + z;   // tabA: ages 0..5, tabZ: ages 1..6
+          for (int bb = 0; bb < TB; ++bb) {
+            const int j = bb + z;   // tabA: ages 0..TB-1, tabZ: ages 1..TB
             if ((m >> bb) & 1) sum += j <= Kmax ? inv[li][j] : 0.0;
           }
           (z ? tabZ : tabA)[li][m] = sum;
@@ -1148,18 +1153,18 @@ __device__ __forceinline__ void turnover_body(
         }
 #if TO_GEN_TAB
         if (anyfree) {
-          // x1 of the ages 0..5 and x0 of the ages 1..6 from the tables; pairs with K_q <= 6
+          // x1 of the ages 0..TB-1 and x0 of the ages 1..TB from the tables; pairs with K_q <= TB
           // charged from them, cells and legs in order (each pair's terms in the walk's order)
           double sa[4][2], sz[4][2];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            sa[e][0] = tabA[0][mt4[e] & 63u]; sz[e][0] = tabZ[0][(mt4[e] >> 1) & 63u];
-            sa[e][1] = tabA[1][mb4[e] & 63u]; sz[e][1] = tabZ[1][(mb4[e] >> 1) & 63u];
+            sa[e][0] = tabA[0][mt4[e] & (TN - 1u)]; sz[e][0] = tabZ[0][(mt4[e] >> 1) & (TN - 1u)];
+            sa[e][1] = tabA[1][mb4[e] & (TN - 1u)]; sz[e][1] = tabZ[1][(mb4[e] >> 1) & (TN - 1u)];
           }
-          uint32_t clo = 0;   // pairs (q, leg) with K_q <= 6 that are not full
+          uint32_t clo = 0;   // pairs (q, leg) with K_q <= TB that are not full
 #pragma unroll
           for (int q = 0; q < TO_MAXQ; ++q)
-            clo |= (q < nq && ks.K[q] <= 6) ? (3u << (2 * q)) & ~fullm : 0u;
+            clo |= (q < nq && ks.K[q] <= TB) ? (3u << (2 * q)) & ~fullm : 0u;
           if (clo) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -1178,13 +1183,13 @@ __device__ __forceinline__ void turnover_body(
             }
           }
 #pragma unroll 1
-          for (int j = 6; j <= kq; ++j) {
+          for (int j = TB; j <= kq; ++j) {
             asm volatile("" ::: "memory");   // the factors are re-read (broadcasts), not held
             const double iv0 = inv[0][j], iv1 = inv[1][j];
-            uint32_t cq = 0;   // pairs with K_q == j (> 6) charged now
+            uint32_t cq = 0;   // pairs with K_q == j (> TB) charged now
 #pragma unroll
             for (int q = 0; q < TO_MAXQ; ++q)
-              cq |= (q < nq && ks.K[q] == j && j > 6) ? (3u << (2 * q)) & ~fullm : 0u;
+              cq |= (q < nq && ks.K[q] == j && j > TB) ? (3u << (2 * q)) & ~fullm : 0u;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
 #pragma unroll
@@ -1199,7 +1204,7 @@ __device__ __forceinline__ void turnover_body(
                              -1.0, 0.02);
                 }
                 sa[e][li] += v;
-                if (j >= 7) sz[e][li] += v;   // (the table holds age 6 already)
+                if (j > TB) sz[e][li] += v;   // (the table holds age TB already)
               }
             }
           }
