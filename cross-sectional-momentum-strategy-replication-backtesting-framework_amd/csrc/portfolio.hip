@@ -1523,8 +1523,11 @@ __global__ __launch_bounds__(64 * TM_WAVES) void k_turnover_ew_mask(
 #ifndef VWG_U
 #define VWG_U 1   // cells per lane in flight in k_turnover_vwg (2 / 4 measured slower: C3 portfolio 0.241 -> 0.266 / 0.342 ms)
 #endif
+#ifndef VWG_WPE
+#define VWG_WPE 1   // waves per EU the VGPR budget must allow (A/B knob)
+#endif
 template <bool IMP>
-__global__ __launch_bounds__(PF_THREADS) void k_turnover_vwg(
+__global__ __launch_bounds__(PF_THREADS) __attribute__((amdgpu_waves_per_eu(VWG_WPE))) void k_turnover_vwg(
     const int8_t* __restrict__ L, const double* __restrict__ W, int T_m, int B, int64_t N,
     KSet ks, int n_bins, int64_t CH, int Ct, double half_spread, double k_impact, double aum,
     const double* __restrict__ ADV, const double* __restrict__ SIG, double* __restrict__ TURNp,
