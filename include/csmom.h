@@ -473,7 +473,9 @@ int csm_portfolio_from_cohorts_multi(csm_ctx* ctx, const int8_t* L, const double
  * holds the two legs (NaN elsewhere).  The reference's long-short rule needs every decile only
  * when a panel lacks one leg's column (run_demo.py:60-65): then *need_full (device int32, set to
  * 0 by the caller) becomes 1 and the caller reruns the full csm_cohort_sums /
- * csm_portfolio_from_cohorts_multi.
+ * csm_portfolio_from_cohorts_multi.  The legs pass stores its partials in a two-leg layout and
+ * records the layout in the workspace (the accounting reads it there): a full
+ * csm_portfolio_from_cohorts* needs the full cohort sums, as before.
  */
 /*
  * Equal-weight cohort sums of nJ (<= 4) label panels L[q] that share one next_ret panel NR (the
