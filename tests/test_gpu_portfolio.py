@@ -373,11 +373,12 @@ def test_portfolio_many_rows(engine, mode):
 
 
 @pytest.mark.parametrize("vw", [False, True])
-@pytest.mark.parametrize("B,n_bins", [(1, 10), (6, 10), (4, 3)])
+@pytest.mark.parametrize("B,n_bins", [(1, 10), (6, 10), (4, 3), (4, 2), (4, 20), (70, 10)])
 def test_legs_only_equals_full(engine, vw, B, n_bins):
     """Legs-only accounting (csm_cohort_sums_legs + csm_portfolio_from_cohorts_legs: only
-    deciles 0 and n_bins - 1 sorted and summed) gives the full path's LS / TURN / COST / NET bit
-    for bit and its PR on the two legs; the other deciles are NaN."""
+    deciles 0 and n_bins - 1 sorted and summed, the partials in the two-leg layout) gives the
+    full path's LS / TURN / COST / NET bit for bit and its PR on the two legs; the other deciles
+    are NaN.  n_bins 2 (both deciles are legs) to 20; 70 panels take the wide long-short."""
     L, NR, _, PM = _labels(engine, "c1")
     if n_bins != 10:
         _, M, NR = engine.momentum(PM, 12, 1)
