@@ -1430,6 +1430,9 @@ __device__ __forceinline__ void turnover_body(
 // the same integers, so the TURN / COST partials are k_turnover's bits.  Rows that are not all
 // full go onto the general launch's work list as k_turnover's steady launch puts them.
 #define TM_WAVES 4
+#ifndef TM_EARLY
+#define TM_EARLY 1   // the row's loads issued together (and its counts reduced packed)
+#endif
 __global__ __launch_bounds__(64 * TM_WAVES) void k_turnover_ew_mask(
     const uint64_t* __restrict__ LM, int64_t nwm, int T_m, int B, int64_t N, KSet ks, int64_t CH,
     int Ct, double half_spread, double* __restrict__ TURNp, double* __restrict__ COSTp,
@@ -1442,6 +1445,108 @@ __global__ __launch_bounds__(64 * TM_WAVES) void k_turnover_ew_mask(
   const int c = bid % Ct, tb = bid / Ct;
   const int t = tb / B, b = tb - t * B;
   const int nq = ks.n;
+#if TM_EARLY
+  // every load of the row at once -- its mask, its factors (lane q < nq), the plane words of
+  // months t and t - K_q (addresses clamped to month 0 for the rows the mask sends elsewhere:
+  // those loads are discarded) -- instead of mask -> words -> factors, three round trips
+  const uint32_t m = TPm[tb];
+  const int64_t w0 = (int64_t)c * CH / 64;
+  const int64_t a1 = (int64_t)(c + 1) * CH < N ? (int64_t)(c + 1) * CH : N;
+  const int64_t w1 = (a1 + 255) / 256 * 4;
+  const uint64_t* r1 = LM + (int64_t)tb * 2 * nwm;
+  const double* tp = TPv + (int64_t)tb * TP_STRIDE;
+  double f1[2] = {0.0, 0.0}, f0[2] = {0.0, 0.0}, fs[2] = {0.0, 0.0};
+  if (lane < nq) {
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      f1[li] = tp[li * (TO_MAXQ + 1)];
+      f0[li] = tp[li * (TO_MAXQ + 1) + 1 + lane];
+      fs[li] = tp[2 * (TO_MAXQ + 1) + 2 * lane + li];
+    }
+  }
+  constexpr int TMU = 2;   // word trips per lane in flight (N <= SEG_MAXN: at most 2)
+  uint64_t x1[TMU][2], x0[TMU][TO_MAXQ][2];
+#pragma unroll
+  for (int u = 0; u < TMU; ++u) {
+    const int64_t w = w0 + lane + 64 * u;
+    const bool in = w < w1;
+    const int64_t wi = in ? w : w0;
+#pragma unroll
+    for (int li = 0; li < 2; ++li) x1[u][li] = in ? r1[li * nwm + wi] : 0ull;
+#pragma unroll
+    for (int q = 0; q < TO_MAXQ; ++q) {
+      const int tq = q < nq ? (t - ks.K[q] >= 0 ? t - ks.K[q] : 0) : 0;
+      const uint64_t* r0 = LM + ((int64_t)tq * B + b) * 2 * nwm;
+#pragma unroll
+      for (int li = 0; li < 2; ++li) x0[u][q][li] = (in && q < nq) ? r0[li * nwm + wi] : 0ull;
+    }
+  }
+  if (m & TP_EMPTY) return;   // k_turn_prep wrote its partials
+  const uint32_t need = (1u << (2 * nq)) - 1u;
+  if ((m & need) != need) {   // the general launch's row
+    if (gen_list && lane == 0) {
+      const int slot = atomicAdd(gen_count, 1);
+      if (slot < rows * Ct) gen_list[slot] = bid;
+    }
+    return;
+  }
+  // member counts, both legs packed in one word (leg 0 low half; a chunk holds < 65536 cells)
+  uint32_t n1 = 0, n0[TO_MAXQ], nb[TO_MAXQ];
+#pragma unroll
+  for (int q = 0; q < TO_MAXQ; ++q) { n0[q] = 0; nb[q] = 0; }
+  auto count = [&](const uint64_t (&y1)[2], const uint64_t (&y0)[TO_MAXQ][2]) {
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      n1 += (uint32_t)__popcll(y1[li]) << (16 * li);
+#pragma unroll
+      for (int q = 0; q < TO_MAXQ; ++q) {
+        n0[q] += (uint32_t)__popcll(y0[q][li]) << (16 * li);
+        nb[q] += (uint32_t)__popcll(y1[li] & y0[q][li]) << (16 * li);
+      }
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < TMU; ++u) count(x1[u], x0[u]);
+  for (int64_t w = w0 + lane + 64 * TMU; w < w1; w += 64) {   // (wider chunks than SEG_MAXN)
+    uint64_t y1[2], y0[TO_MAXQ][2];
+#pragma unroll
+    for (int li = 0; li < 2; ++li) y1[li] = r1[li * nwm + w];
+#pragma unroll
+    for (int q = 0; q < TO_MAXQ; ++q) {
+      const uint64_t* r0 = LM + ((int64_t)(t - (q < nq ? ks.K[q] : 0)) * B + b) * 2 * nwm;
+#pragma unroll
+      for (int li = 0; li < 2; ++li) y0[q][li] = q < nq ? r0[li * nwm + w] : 0ull;
+    }
+    count(y1, y0);
+  }
+  auto wsum = [](uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+  n1 = wsum(n1);
+#pragma unroll
+  for (int q = 0; q < TO_MAXQ; ++q) {
+    if (q >= nq) break;
+    n0[q] = wsum(n0[q]);
+    nb[q] = wsum(nb[q]);
+  }
+  if (lane < nq) {
+    const int q = lane;
+    double x = 0.0;   // (k_turnover: the waves' f64 charge sums, +0.0 on an all-full row)
+#pragma unroll
+    for (int li = 0; li < 2; ++li) {
+      uint32_t c0 = 0, cb = 0;
+#pragma unroll
+      for (int qq = 0; qq < TO_MAXQ; ++qq)
+        if (qq == q) { c0 = (n0[qq] >> (16 * li)) & 0xFFFFu; cb = (nb[qq] >> (16 * li)) & 0xFFFFu; }
+      const uint32_t c1 = (n1 >> (16 * li)) & 0xFFFFu;
+      const double i1 = f1[li], i0 = f0[li], skq = fs[li];
+      x += ((double)(c1 - cb) * i1 + (double)(c0 - cb) * i0 + (double)cb * fabs(i1 - i0)) * skq;
+    }
+    TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.5 * x;
+    COSTp[((int64_t)q * rows + tb) * Ct + c] = x * half_spread;
+  }
+#else
   const uint32_t m = TPm[tb];
   if (m & TP_EMPTY) return;   // k_turn_prep wrote its partials
   const uint32_t need = (1u << (2 * nq)) - 1u;
@@ -1509,6 +1614,7 @@ __global__ __launch_bounds__(64 * TM_WAVES) void k_turnover_ew_mask(
     TURNp[((int64_t)q * rows + tb) * Ct + c] = 0.5 * x;
     COSTp[((int64_t)q * rows + tb) * Ct + c] = x * half_spread;
   }
+#endif
 }
 
 // Steady value-weight rows of the G = B / Bg panels that share one weight row (the grouped
