@@ -425,6 +425,15 @@ __device__ __forceinline__ uint32_t byte_eq0(uint32_t z) {   // 0x80 in each byt
 // not depend on the order).
 // LSO: prefix ranks by v_mbcnt (fewer VALU operations per label word than the popcount of the
 // masked ballot; the same values)
+// LS_STAGE: a row whose two legs hold at most LS_CAP ids (sentinels included) builds its segment
+// in the wave's LDS slice and stores it once, as 8-byte words of consecutive positions, instead
+// of each lane storing its own 2-byte ids a few positions apart (those stores were 280 of 1020
+// us per C5 batch, -DLS_NOSTORE timing); larger rows store directly.  The same ids at the same
+// positions.
+#ifndef LS_STAGE
+#define LS_STAGE 1
+#endif
+#define LS_CAP 2048
 template <int NB, bool LSO = false>
 __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
     const int8_t* __restrict__ L, int64_t N, int C, int64_t rows, uint16_t* __restrict__ PERM,
@@ -463,8 +472,21 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
   const int rb = (nb0 + 3) & ~3, rt = (nt0 + 3) & ~3;
   uint16_t* Pr = PERM + row * PS;
   if (lane <= NB) OFF[row * (NB + 1) + lane] = lane == 0 ? 0 : (lane < NB ? rb : rb + rt);
+#if LS_STAGE
+  __shared__ __attribute__((aligned(16))) uint16_t stg[PF_WAVES][LS_CAP];
+  uint16_t* sp = stg[threadIdx.x >> 6];
+  const bool staged = rb + rt <= LS_CAP;   // (wave-uniform)
+  if (staged) {
+    if (lane < rb - nb0) sp[nb0 + lane] = (uint16_t)N;               // sentinel ids
+    if (lane < rt - nt0) sp[rb + nt0 + lane] = (uint16_t)N;
+  } else {
+    if (lane < rb - nb0) Pr[nb0 + lane] = (uint16_t)N;
+    if (lane < rt - nt0) Pr[rb + nt0 + lane] = (uint16_t)N;
+  }
+#else
   if (lane < rb - nb0) Pr[nb0 + lane] = (uint16_t)N;               // sentinel ids
   if (lane < rt - nt0) Pr[rb + nt0 + lane] = (uint16_t)N;
+#endif
   for (int i = lane; i < 2 * C; i += 64) {   // leg totals in chunk 0 (leg 0 = top), zeros elsewhere
     const int c = i >> 1, leg = i & 1;
     FWp[(row * C + c) * 2 + leg] = c == 0 ? (double)(leg == 0 ? nt0 : nb0) : 0.0;
@@ -503,15 +525,37 @@ __global__ __launch_bounds__(PF_THREADS) void k_label_sort_legs_ew(
         LM[(row * 2 + 1) * nwm + w] = pw_b;
       }
     }
+#if LS_STAGE
+    if (staged) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {   // lane-major then byte order = ascending asset id
-      const uint16_t a = (uint16_t)(4 * wi + e);
-      if ((eb >> (8 * e + 7)) & 1u) Pr[bb++] = a;
-      if ((et >> (8 * e + 7)) & 1u) Pr[bt++] = a;
+      for (int e = 0; e < 4; ++e) {   // lane-major then byte order = ascending asset id
+        const uint16_t a = (uint16_t)(4 * wi + e);
+        if ((eb >> (8 * e + 7)) & 1u) sp[bb++] = a;
+        if ((et >> (8 * e + 7)) & 1u) sp[bt++] = a;
+      }
+    } else
+#endif
+    {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {   // lane-major then byte order = ascending asset id
+        const uint16_t a = (uint16_t)(4 * wi + e);
+        if ((eb >> (8 * e + 7)) & 1u) Pr[bb++] = a;
+        if ((et >> (8 * e + 7)) & 1u) Pr[bt++] = a;
+      }
     }
     pb += totb;
     pt += tott;
   }
+#if LS_STAGE
+  if (staged) {   // the whole segment out: 4 ids per 8-byte store, consecutive lanes
+    __builtin_amdgcn_wave_barrier();
+    const int nw8 = (rb + rt) >> 2;
+    const uint64_t* s8 = reinterpret_cast<const uint64_t*>(sp);
+    uint64_t* d8 = reinterpret_cast<uint64_t*>(Pr);
+    for (int i = lane; i < nw8; i += 64) d8[i] = s8[i];
+    __builtin_amdgcn_wave_barrier();
+  }
+#endif
 }
 
 // 16-lane groups, one (age, decile) segment per group at a time: a short reduction (4 steps)
