@@ -1151,30 +1151,37 @@ using dec_wide::k_deciles;
 #undef DEC_LU
 
 // =====================================================================================
-// Kernel E: long-short series (one workgroup; T_m * n_bins is tiny).
+// Kernel E: long-short series (one workgroup; T_m * n_bins is tiny).  LS_THREADS threads: a
+// thread's first month's counts and means are loaded before the leg-presence barrier and kept
+// for its long-short (one round trip where T_m <= LS_THREADS, instead of a flag pass and a
+// second pass over the months).
 // =====================================================================================
-__global__ __launch_bounds__(256) void k_long_short(const double* __restrict__ EW,
-                                                    const int32_t* __restrict__ CNT, int T_m,
-                                                    int nb, double* __restrict__ LS) {
+#define LS_THREADS 512
+__global__ __launch_bounds__(LS_THREADS) void k_long_short(const double* __restrict__ EW,
+                                                           const int32_t* __restrict__ CNT,
+                                                           int T_m, int nb,
+                                                           double* __restrict__ LS) {
   __shared__ int has_lo, has_hi;
-  if (threadIdx.x == 0) { has_lo = 0; has_hi = 0; }
-  __syncthreads();
-  for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
-    if (CNT[(int64_t)t * nb] > 0) atomicOr(&has_lo, 1);
-    if (CNT[(int64_t)t * nb + nb - 1] > 0) atomicOr(&has_hi, 1);
-  }
-  __syncthreads();
-  const bool both = has_lo && has_hi;
-  for (int t = threadIdx.x; t < T_m; t += blockDim.x) {
+  const int t0 = threadIdx.x;
+  int cv[MAXQ - 1];
+  double ev[MAXQ - 1];
+  auto load_row = [&](int t) {
     const double* e = EW + (int64_t)t * nb;
     const int32_t* c = CNT + (int64_t)t * nb;
-    int cv[MAXQ - 1];
-    double ev[MAXQ - 1];
 #pragma unroll
     for (int d = 0; d < MAXQ - 1; ++d) {   // the row's counts and means, all loads in flight
       cv[d] = d < nb ? c[d] : 0;
       ev[d] = d < nb ? e[d] : 0.0;
     }
+  };
+  auto legs_of = [&](int& lo_c, int& hi_c) {   // the row's decile-0 / decile-(nb-1) counts
+#pragma unroll
+    for (int d = 0; d < MAXQ - 1; ++d) {
+      if (d == 0) lo_c = cv[d];
+      if (d == nb - 1) hi_c = cv[d];
+    }
+  };
+  auto ls_of = [&](bool both) {
     bool any = false;
     double mx = -INFINITY, mn = INFINITY, lo = 0.0, hi = 0.0;
 #pragma unroll
@@ -1185,7 +1192,27 @@ __global__ __launch_bounds__(256) void k_long_short(const double* __restrict__ E
     }
     double v = qnan();
     if (any) v = both ? (hi - lo) : (mx - mn);
-    LS[t] = v;
+    return v;
+  };
+  if (t0 < T_m) load_row(t0);
+  if (t0 == 0) { has_lo = 0; has_hi = 0; }
+  __syncthreads();
+  if (t0 < T_m) {
+    int lc = 0, hc = 0;
+    legs_of(lc, hc);
+    if (lc > 0) atomicOr(&has_lo, 1);
+    if (hc > 0) atomicOr(&has_hi, 1);
+  }
+  for (int t = t0 + LS_THREADS; t < T_m; t += LS_THREADS) {
+    if (CNT[(int64_t)t * nb] > 0) atomicOr(&has_lo, 1);
+    if (CNT[(int64_t)t * nb + nb - 1] > 0) atomicOr(&has_hi, 1);
+  }
+  __syncthreads();
+  const bool both = has_lo && has_hi;
+  if (t0 < T_m) LS[t0] = ls_of(both);
+  for (int t = t0 + LS_THREADS; t < T_m; t += LS_THREADS) {
+    load_row(t);
+    LS[t] = ls_of(both);
   }
 }
 
@@ -2973,7 +3000,7 @@ int csm_long_short(csm_ctx* ctx, const double* EW, const int32_t* CNT, int32_t T
   if (!EW || !CNT || !LS || T_m < 0 || n_bins < 1)
     return set_err(ctx, CSM_E_INVAL, "csm_long_short: bad arguments");
   if (T_m == 0) return CSM_OK;
-  hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
+  hipLaunchKernelGGL(k_long_short, dim3(1), dim3(LS_THREADS), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
   LAUNCH_CHECK(ctx, "k_long_short");
   return CSM_OK;
 }
@@ -3082,7 +3109,7 @@ static int deciles_dispatch(csm_ctx* ctx, const char* who, bool v2, int32_t T_m,
   }
   LAUNCH_CHECK(ctx, who);
   if (LSw) {
-    hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LSw);
+    hipLaunchKernelGGL(k_long_short, dim3(1), dim3(LS_THREADS), 0, ctx->stream, EW, CNT, T_m, n_bins, LSw);
     LAUNCH_CHECK(ctx, "k_long_short");
   }
   return CSM_OK;
@@ -3193,7 +3220,7 @@ int csm_pipeline(csm_ctx* ctx, const double* P, int64_t T_d, int64_t N, const in
   r = deciles_dispatch(ctx, "csm_pipeline", v2, T_m, M, NR, N, n_bins, q, L, EW, CNT, NV, ids,
                        ids != nullptr, ids ? LS : nullptr);
   if (r || ids) return r;
-  hipLaunchKernelGGL(k_long_short, dim3(1), dim3(256), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
+  hipLaunchKernelGGL(k_long_short, dim3(1), dim3(LS_THREADS), 0, ctx->stream, EW, CNT, T_m, n_bins, LS);
   LAUNCH_CHECK(ctx, "k_long_short");
   return CSM_OK;
 }
