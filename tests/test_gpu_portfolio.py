@@ -626,3 +626,24 @@ def test_long_short_wide_batch_rule(engine, legs):
             for f in ("PR", "LS", "TURN", "COST", "NET"):
                 assert bits_equal(getattr(got[K], f).cpu().numpy(),
                                   getattr(full[K], f).cpu().numpy()), (K, f)
+
+
+@pytest.mark.parametrize("n_bins", [2, 4, 10])
+def test_legs_only_equals_full_wide_legs(engine, n_bins):
+    """The one-wave legs label sort stages a row's segment in LDS when its two legs hold at most
+    2,048 ids and stores it directly otherwise: 3,000-asset rows with n_bins 2 (every ranked cell
+    in a leg: the direct stores), 4 and 10 (staged) -- legs-only accounting equals the full path
+    bit for bit either way (LS / TURN / COST / NET, PR on the legs)."""
+    rng = np.random.default_rng(n_bins)
+    T_m, B, N = 60, 3, 3000
+    Lh = rng.integers(-1, n_bins, size=(T_m, B, N)).astype(np.int8)
+    NRh = rng.normal(0.01, 0.08, size=(T_m, B, N))
+    L, NR = _up(Lh.reshape(T_m, B * N)), _up(NRh.reshape(T_m, B * N))
+    full = engine.portfolio_multi(L, NR, n_bins, Ks=(1, 3, 12), B=B)
+    legs = engine.portfolio_multi(L, NR, n_bins, Ks=(1, 3, 12), B=B, legs_only=True)
+    for K in (1, 3, 12):
+        for f in ("LS", "TURN", "COST", "NET"):
+            assert bits_equal(getattr(legs[K], f).cpu().numpy(), getattr(full[K], f).cpu().numpy()), (K, f)
+        a, b = legs[K].PR.cpu().numpy(), full[K].PR.cpu().numpy()
+        for d in (0, n_bins - 1):
+            assert bits_equal(a[..., d], b[..., d]), (K, d)
